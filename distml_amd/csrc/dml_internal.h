@@ -1,0 +1,108 @@
+// dml_internal.h — types shared by the HIP kernels (dml_kernels.hip) and the
+// C-ABI host implementation (dml_store.hip). Not part of the public ABI.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+namespace dml {
+
+// One ordered batch chunk holds at most this many pushes (the slot table is
+// [rows][kMaxW] int32); longer batches run as consecutive chunks, in order.
+constexpr int kMaxW = 64;
+
+// Position of a byte in the batch, in reference processing order:
+// bucket-major, then byte offset inside the bucket (the order in which
+// handlePush's while-loop reads bytes, FloatMatrixStore.java:202-207).
+__host__ __device__ inline uint64_t pos_of(uint64_t bucket, uint64_t off) { return (bucket << 40) | off; }
+constexpr uint64_t kNoPos = ~0ull;
+constexpr uint64_t kOffMask = (1ull << 40) - 1;
+
+// Per-batch control block. Lives at the head of the slot-table allocation so
+// ONE hipMemsetAsync(0xFF) resets it and the slot table (-1 = no record).
+struct Ctrl {
+    unsigned long long cutoff;   // first key-out-of-shard position (exclusive apply limit)
+    unsigned long long neg_pos;  // first add that left an int32 counter negative
+    unsigned int no_dup;         // 0xFFFFFFFF = no row repeated inside one push; 0 = repeat seen
+    unsigned int pad[3];
+};
+static_assert(sizeof(Ctrl) == 32, "Ctrl layout");
+
+// Bucket table passed by value as a kernel argument (scalar-loaded).
+struct Batch {
+    const uint8_t* base[kMaxW];
+    int64_t len[kMaxW];
+    int64_t nrec[kMaxW];  // records whose key is complete (a truncated tail record included)
+    int32_t bidx[kMaxW];  // global push index of each column (positions use it; columns ascend)
+};
+
+// Running AdaGrad maxDelta state (FloatMatrixStoreAdaGrad.java:27-29), device resident.
+struct MaxDelta {
+    float value;
+    int32_t row;
+    int32_t col;
+    int32_t pad;
+};
+// Per-block AdaGrad candidate: the largest final delta of an element whose
+// delta rose in this batch, and the position where it last rose.
+struct DeltaCand {
+    float value;
+    int32_t valid;
+    unsigned long long pos;
+};
+
+struct AdaArgs {
+    float* alpha;
+    float* delta;
+    DeltaCand* cand;      // one per reduce block
+    float initial_alpha, min_alpha, factor;
+};
+
+enum ReduceMode : int {
+    kAdd = 0,          // f32 / f64 / i32-without-check
+    kAddCheckI32 = 1,  // IntMatrixStore dense: negativity check after each add
+    kAdaGrad = 2,      // FloatMatrixStoreAdaGrad dense
+    kRollbackI32 = 3,  // undo adds after the first negative (exact mod 2^32)
+    kPreReduce = 4,    // multi-GPU pre-reduce: acc starts at 0, every row written
+};
+
+enum VType : int { kI32 = 0, kF32 = 1, kF64 = 3 };
+
+// ---- launchers (dml_kernels.hip) ----
+hipError_t launch_index(const Batch& bt, int nb, int64_t max_nrec, int64_t stride, int K,
+                        int64_t first, int64_t rows, int32_t* slot, Ctrl* ctrl, hipStream_t st);
+hipError_t launch_reduce(int vtype, int mode, void* shard, int64_t rows, int32_t cols, const Batch& bt,
+                         int nb, int64_t stride, int K, const int32_t* slot, Ctrl* ctrl,
+                         uint64_t tail_cut, const AdaArgs& ada, hipStream_t st, int64_t* nblocks_out);
+hipError_t launch_rollback_i32(int32_t* shard, int64_t rows, int32_t cols, const Batch& bt, int nb,
+                               int64_t stride, int K, const int32_t* slot, Ctrl* ctrl,
+                               uint64_t tail_cut, hipStream_t st);
+hipError_t launch_maxdelta_finalize(const DeltaCand* cand, int64_t n, MaxDelta* md, const Batch& bt, int nb,
+                                    int64_t stride, int K, int V, hipStream_t st);
+hipError_t launch_array_validate(const Batch& bt, int nb, int64_t max_nrec, int64_t stride,
+                                 int K, int64_t first, int64_t rows, Ctrl* ctrl, hipStream_t st);
+hipError_t launch_array_apply(int vtype, void* shard, int64_t rows, const uint8_t* base, int64_t nrec,
+                              int b_global, int64_t stride, int K, int64_t first, Ctrl* ctrl,
+                              uint64_t tail_cut, hipStream_t st);
+hipError_t launch_array_rollback_i32(int32_t* shard, int64_t rows, const uint8_t* base, int64_t nrec,
+                                     int b_global, int64_t stride, int K, int64_t first, Ctrl* ctrl,
+                                     uint64_t tail_cut, hipStream_t st);
+hipError_t launch_fill(int vtype, void* p, int64_t n, double v, hipStream_t st);
+hipError_t launch_fill_f32(float* p, int64_t n, float v, hipStream_t st);
+hipError_t launch_apply_dense(int vtype, void* shard, const void* src, int64_t n, hipStream_t st);
+hipError_t launch_fetch(int vtype, const void* shard, const float* alpha, int32_t cols, const int64_t* keys,
+                        int64_t n, int64_t first, uint8_t* out, int64_t rec, int K, int value_slot,
+                        hipStream_t st);
+hipError_t launch_bswap(int V, const void* src, void* dst, int64_t n, hipStream_t st);
+hipError_t launch_synth_dense(uint8_t* out, int K, int vtype, int64_t first, int64_t shard_rows, int64_t nrec,
+                              int32_t cols, uint64_t s0, uint64_t pa, uint64_t pc, hipStream_t st);
+hipError_t launch_synth_sparse(uint8_t* out, int K, int vtype, int value_stride, int64_t first,
+                               int64_t key_space, int64_t nrec, uint64_t s0, uint64_t pa, uint64_t pc,
+                               hipStream_t st);
+hipError_t launch_synth_fill(int vtype, void* p, int64_t n, uint64_t s0, hipStream_t st);
+hipError_t launch_key_rows(const uint8_t* base, int64_t nrec, int64_t stride, int K, int64_t first, int64_t rows,
+                           int32_t* out, hipStream_t st);
+int64_t reduce_blocks(int vtype, int64_t rows, int32_t cols);
+
+uint64_t splitmix64(uint64_t x);
+
+}  // namespace dml

@@ -1,0 +1,714 @@
+// dml_kernels.hip — CDNA4 (gfx950) kernels of the parameter-server push path.
+//
+// Compiled with -ffp-contract=off and IEEE denormals (Java forbids FMA
+// contraction and flush-to-zero, JLS 15.4 / 4.2.3): every `acc + v` below is
+// one IEEE binary32/binary64 rounding, exactly the reference's `row[i] += v`.
+//
+// Kernels
+//   k_index         decode record keys -> per-row slot table (row -> record of push b)
+//   k_reduce<T,M>   ordered multi-push reduce: every element of a shard row
+//                   summed over the batch's pushes in push order, one RMW of
+//                   the row (FloatMatrixStore.java:210-222, IntMatrixStore.java:164-178,
+//                   DoubleMatrixStore.java:163-175, FloatMatrixStoreAdaGrad.java:249-284)
+//   k_array_*       ordered sparse scatter-add for the array stores
+//                   (FloatArrayStore.java:380-392, IntArrayStore.java:294-310,
+//                   DoubleArrayStore.java:115-127), one launch per push
+//   k_fetch, k_bswap, k_fill, k_apply_dense, k_synth_*  — fetch / checkpoint /
+//                   init / owner-apply / synthetic data.
+#include "dml_internal.h"
+
+#include <climits>
+
+namespace dml {
+
+typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+typedef u32x4 u32x4_u __attribute__((aligned(4)));  // records are 4-byte aligned only
+typedef int32_t i32x8 __attribute__((ext_vector_type(8)));
+typedef uint64_t u64x8 __attribute__((ext_vector_type(8)));
+
+// Loads through the global address space: bucket pointers come out of the
+// kernarg table as generic pointers, and flat loads would force vmcnt(0)+lgkmcnt(0)
+// waits (flat returns out of order).
+#define DML_GLOBAL __attribute__((address_space(1)))
+__device__ inline u32x4 ldg16(const uint8_t* p) { return *(const DML_GLOBAL u32x4_u*)(p); }
+__device__ inline uint32_t ldg32(const uint8_t* p) { return *(const DML_GLOBAL uint32_t*)(p); }
+
+__host__ __device__ inline uint64_t splitmix64_dev(uint64_t x) {
+    uint64_t z = x + 0x9E3779B97F4A7C15ull;
+    z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
+    z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
+    return z ^ (z >> 31);
+}
+uint64_t splitmix64(uint64_t x) { return splitmix64_dev(x); }
+
+__device__ inline uint32_t ld32(const uint8_t* p) { return ldg32(p); }
+__device__ inline int64_t ld_key(const uint8_t* p, int K) {
+    // DataDesc.readKey (DataDesc.java:131-138): LE int32 sign-extended, or LE int64.
+    if (K == 4) return (int64_t)(int32_t)ld32(p);
+    return (int64_t)((uint64_t)ld32(p) | ((uint64_t)ld32(p + 4) << 32));
+}
+// KeyRange indexOf: (int)(key - firstKey) (FloatMatrixStore.java:176-179); -1 if
+// localData[index] would throw ArrayIndexOutOfBoundsException.
+__device__ inline int64_t row_index(int64_t key, int64_t first, int64_t rows) {
+    int32_t idx = (int32_t)(uint32_t)((uint64_t)key - (uint64_t)first);
+    return (idx < 0 || (int64_t)idx >= rows) ? -1 : (int64_t)idx;
+}
+
+template <typename T> struct Elem;
+template <> struct Elem<float> {
+    static constexpr int VEC = 4;
+    __device__ static float from_bits(uint32_t lo, uint32_t) { return __uint_as_float(lo); }
+    __device__ static float load(const uint8_t* p) { return __uint_as_float(ld32(p)); }
+    __device__ static float add(float a, float b) { return __fadd_rn(a, b); }
+};
+template <> struct Elem<int32_t> {
+    static constexpr int VEC = 4;
+    __device__ static int32_t from_bits(uint32_t lo, uint32_t) { return (int32_t)lo; }
+    __device__ static int32_t load(const uint8_t* p) { return (int32_t)ld32(p); }
+    __device__ static int32_t add(int32_t a, int32_t b) { return (int32_t)((uint32_t)a + (uint32_t)b); }
+};
+template <> struct Elem<double> {
+    static constexpr int VEC = 2;
+    __device__ static double from_bits(uint32_t lo, uint32_t hi) {
+        return __longlong_as_double((long long)((uint64_t)lo | ((uint64_t)hi << 32)));
+    }
+    __device__ static double load(const uint8_t* p) { return from_bits(ld32(p), ld32(p + 4)); }
+    __device__ static double add(double a, double b) { return __dadd_rn(a, b); }
+};
+
+template <typename T>
+__device__ inline void unpack(const u32x4& r, T* o) {
+    if constexpr (sizeof(T) == 4) {
+        o[0] = Elem<T>::from_bits(r.x, 0); o[1] = Elem<T>::from_bits(r.y, 0);
+        o[2] = Elem<T>::from_bits(r.z, 0); o[3] = Elem<T>::from_bits(r.w, 0);
+    } else {
+        o[0] = Elem<T>::from_bits(r.x, r.y); o[1] = Elem<T>::from_bits(r.z, r.w);
+    }
+}
+template <typename T>
+__device__ inline u32x4 pack(const T* v) {
+    u32x4 r;
+    if constexpr (sizeof(T) == 4) {
+        r.x = __builtin_bit_cast(uint32_t, v[0]); r.y = __builtin_bit_cast(uint32_t, v[1]);
+        r.z = __builtin_bit_cast(uint32_t, v[2]); r.w = __builtin_bit_cast(uint32_t, v[3]);
+    } else {
+        uint64_t a = __builtin_bit_cast(uint64_t, v[0]), b = __builtin_bit_cast(uint64_t, v[1]);
+        r.x = (uint32_t)a; r.y = (uint32_t)(a >> 32); r.z = (uint32_t)b; r.w = (uint32_t)(b >> 32);
+    }
+    return r;
+}
+
+// ---------------------------------------------------------------------------
+// k_index: one thread per record of push b (blockIdx.y). Writes
+// slot[row][b] = record index; a row seen twice in one push clears no_dup
+// (the host then replays the batch through the exact sequential path); a key
+// outside the shard lowers ctrl->cutoff to the record's start position.
+__global__ __launch_bounds__(256) void k_index(const Batch bt, int64_t stride, int K,
+                                               int64_t first, int64_t rows, int32_t* __restrict__ slot,
+                                               Ctrl* __restrict__ ctrl) {
+    const int b = blockIdx.y;
+    const int64_t r = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (r >= bt.nrec[b]) return;
+    const int64_t off = r * stride;
+    const int64_t key = ld_key(bt.base[b] + off, K);
+    const int64_t idx = row_index(key, first, rows);
+    if (idx < 0) {
+        atomicMin(&ctrl->cutoff, (unsigned long long)pos_of((uint64_t)bt.bidx[b], (uint64_t)off));
+        return;
+    }
+    const int32_t old = atomicExch(&slot[idx * kMaxW + b], (int32_t)r);
+    if (old != -1) atomicAnd(&ctrl->no_dup, 0u);
+}
+
+hipError_t launch_index(const Batch& bt, int nb, int64_t max_nrec, int64_t stride, int K,
+                        int64_t first, int64_t rows, int32_t* slot, Ctrl* ctrl, hipStream_t st) {
+    if (max_nrec <= 0 || nb <= 0) return hipSuccess;
+    dim3 grid((unsigned)((max_nrec + 255) / 256), (unsigned)nb);
+    hipLaunchKernelGGL(k_index, grid, dim3(256), 0, st, bt, stride, K, first, rows, slot, ctrl);
+    return hipGetLastError();
+}
+
+// ---------------------------------------------------------------------------
+// k_reduce: one wave per (shard row, 64*VEC-column chunk); a 256-thread block =
+// 4 waves. The wave reads the row's slots (wave-uniform scalar loads), keeps
+// the row chunk in registers, adds every push's values in push order (loads of
+// up to 8 pushes in flight per lane, 16 B each), then writes the row once.
+// Elements at or past the batch cutoff (first key/truncation error) are not
+// applied — the state the reference leaves when its exception escapes.
+template <typename T, int MODE>
+__global__ __launch_bounds__(256) void k_reduce(T* __restrict__ shard, int64_t rows, int32_t cols, int32_t nchunks,
+                                                const Batch bt, int nb, int64_t stride, int K,
+                                                const int32_t* __restrict__ slot, Ctrl* __restrict__ ctrl,
+                                                uint64_t tail_cut, AdaArgs ada) {
+    constexpr int VEC = Elem<T>::VEC;
+    constexpr int G = 8;
+    const int lane = threadIdx.x & 63;
+    const int wid = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    const int64_t task = (int64_t)blockIdx.x * 4 + wid;
+    const int64_t ntask = rows * (int64_t)nchunks;
+
+    // AdaGrad maxDelta candidate of this lane.
+    float cand_v = 0.f;
+    uint64_t cand_p = kNoPos;
+    bool cand_ok = false;
+
+    if (task < ntask) do {
+        if (MODE != kPreReduce && ctrl->no_dup == 0u) break;  // host replays sequentially
+        const int64_t row = task / nchunks;
+        const int chunk = (int)(task - row * nchunks);
+        const int32_t c0 = (chunk * 64 + lane) * VEC;
+        const int nv = c0 < cols ? (cols - c0 < VEC ? cols - c0 : VEC) : 0;
+
+        uint64_t cut = ctrl->cutoff;
+        if (tail_cut < cut) cut = tail_cut;
+        const int cut_b = cut == kNoPos ? INT_MAX : (int)(cut >> 40);  // global push index of the cutoff
+        const uint64_t cut_off = cut & kOffMask;
+        uint64_t negcut = kNoPos;
+        if (MODE == kRollbackI32) {
+            negcut = ctrl->neg_pos;
+            if (negcut == kNoPos) break;
+        }
+
+        const int32_t* srow = slot + row * kMaxW;
+        T* prow = shard + row * (int64_t)cols + c0;
+        const int64_t voff = (int64_t)K + (int64_t)c0 * (int64_t)sizeof(T);  // value offset inside a record
+
+        T acc[VEC];
+        float dl[VEC], al[VEC];
+        bool touched = false;
+        bool negf = false;
+        uint64_t negpos = kNoPos;
+
+        auto load_row = [&]() {
+            if (MODE == kPreReduce) {
+#pragma unroll
+                for (int e = 0; e < VEC; ++e) acc[e] = T(0);
+            } else if (nv == VEC) {
+                const u32x4 t = *(const u32x4_u*)prow;
+                unpack<T>(t, acc);
+            } else {
+#pragma unroll
+                for (int e = 0; e < VEC; ++e) acc[e] = e < nv ? prow[e] : T(0);
+            }
+            if constexpr (MODE == kAdaGrad) {
+                const int64_t ei = row * (int64_t)cols + c0;
+#pragma unroll
+                for (int e = 0; e < VEC; ++e) {
+                    dl[e] = e < nv ? ada.delta[ei + e] : 0.f;
+                    al[e] = e < nv ? ada.alpha[ei + e] : 0.f;
+                }
+            }
+        };
+
+        // One contribution u to element e at batch position p.
+        auto apply = [&](int e, T u, uint64_t p) {
+            if constexpr (MODE == kRollbackI32) {
+                if (p > negcut) acc[e] = (T)((uint32_t)acc[e] - (uint32_t)u);
+            } else {
+                acc[e] = Elem<T>::add(acc[e], u);
+                if constexpr (MODE == kAddCheckI32) {
+                    if (!negf && acc[e] < 0) { negf = true; negpos = p; }
+                }
+                if constexpr (MODE == kAdaGrad) {
+                    // FloatMatrixStoreAdaGrad.java:265-277
+                    const float uu = __fmul_rn((float)u, (float)u);
+                    const float nd = __fadd_rn(dl[e], uu);
+                    if (nd > dl[e]) {  // delta rose: candidate for maxDelta (NaN never rises)
+                        if (!cand_ok || nd > cand_v || (nd == cand_v && p < cand_p)) {
+                            cand_ok = true; cand_v = nd; cand_p = p;
+                        }
+                    }
+                    dl[e] = nd;
+                    if ((double)nd > 1.0) {
+                        float a = (float)((double)ada.initial_alpha / ((double)ada.factor * sqrt((double)nd)));
+                        if (a < ada.min_alpha) a = ada.min_alpha;
+                        al[e] = a;
+                    }
+                }
+            }
+        };
+
+        const bool vec_ok = (cols % VEC) == 0;  // wave-uniform: every active lane holds VEC elements
+        if (nv == 0) break;                      // lanes past the row's last column idle
+
+        for (int b0 = 0; b0 < nb; b0 += G) {
+            // Wave-uniform scalar loads of 8 slots / push indices / bases at once;
+            // every index < kMaxW is in bounds of the slot row and the kernarg table.
+            const i32x8 sv = *(const i32x8*)(srow + b0);
+            const i32x8 gv = *(const i32x8*)(&bt.bidx[b0]);
+            const u64x8 pv = *(const u64x8*)(&bt.base[b0]);
+            int32_t rr[G];
+            int gbv[G];
+            const uint8_t* bp[G];
+#pragma unroll
+            for (int g = 0; g < G; ++g) {
+                const bool in = b0 + g < nb;
+                gbv[g] = in ? gv[g] : INT_MAX;
+                bp[g] = (const uint8_t*)pv[g];
+                rr[g] = (in && gbv[g] <= cut_b) ? sv[g] : -1;
+            }
+            bool any = false;
+#pragma unroll
+            for (int g = 0; g < G; ++g) any |= rr[g] >= 0;
+            if (!any) continue;
+            if (!touched) { load_row(); touched = true; }
+            const int glast = (nb - b0 < G ? nb - b0 : G) - 1;
+
+            if (vec_ok && gbv[glast] < cut_b) {
+                // Fast path: G independent 16-B loads in flight, no branches between
+                // them; an absent slot re-reads this lane's own row chunk (cache hit).
+                u32x4 raw[G];
+#pragma unroll
+                for (int g = 0; g < G; ++g) {
+                    const uint8_t* src = rr[g] >= 0 ? bp[g] + (int64_t)rr[g] * stride + voff : (const uint8_t*)prow;
+                    raw[g] = ldg16(src);
+                }
+#pragma unroll
+                for (int g = 0; g < G; ++g) {
+                    if (rr[g] < 0) continue;  // wave-uniform
+                    T u[VEC];
+                    unpack<T>(raw[g], u);
+                    const uint64_t pb = pos_of((uint64_t)gbv[g], (uint64_t)((int64_t)rr[g] * stride + voff));
+#pragma unroll
+                    for (int e = 0; e < VEC; ++e) apply(e, u[e], pb + (uint64_t)(e * (int)sizeof(T)));
+                }
+            } else {
+                // Generic path: ragged lanes, or the group holding the cutoff push.
+                for (int g = 0; g < G; ++g) {
+                    if (rr[g] < 0) continue;
+                    const int64_t roff = (int64_t)rr[g] * stride + voff;
+                    for (int e = 0; e < nv; ++e) {
+                        const uint64_t off = (uint64_t)(roff + e * (int64_t)sizeof(T));
+                        if (gbv[g] == cut_b && off >= cut_off) break;
+                        apply(e, Elem<T>::load(bp[g] + off), pos_of((uint64_t)gbv[g], off));
+                    }
+                }
+            }
+        }
+
+        if (MODE == kPreReduce && !touched) {
+#pragma unroll
+            for (int e = 0; e < VEC; ++e) acc[e] = T(0);
+            touched = true;
+        }
+        if (touched && nv > 0) {
+            if (nv == VEC) {
+                *(u32x4_u*)prow = pack<T>(acc);
+            } else {
+                for (int e = 0; e < nv; ++e) prow[e] = acc[e];
+            }
+            if constexpr (MODE == kAdaGrad) {
+                const int64_t ei = row * (int64_t)cols + c0;
+                for (int e = 0; e < nv; ++e) { ada.delta[ei + e] = dl[e]; ada.alpha[ei + e] = al[e]; }
+            }
+        }
+        if (MODE == kAddCheckI32 && negf) atomicMin(&ctrl->neg_pos, (unsigned long long)negpos);
+    } while (0);
+
+    if constexpr (MODE == kAdaGrad) {
+        // Block-wide best candidate: max value, then min position.
+        __shared__ float sv[256];
+        __shared__ unsigned long long sp[256];
+        __shared__ int sok[256];
+        sv[threadIdx.x] = cand_v; sp[threadIdx.x] = cand_p; sok[threadIdx.x] = cand_ok;
+        __syncthreads();
+        for (int s = 128; s > 0; s >>= 1) {
+            if ((int)threadIdx.x < s) {
+                const int o = threadIdx.x + s;
+                if (sok[o] && (!sok[threadIdx.x] || sv[o] > sv[threadIdx.x] ||
+                               (sv[o] == sv[threadIdx.x] && sp[o] < sp[threadIdx.x]))) {
+                    sv[threadIdx.x] = sv[o]; sp[threadIdx.x] = sp[o]; sok[threadIdx.x] = 1;
+                }
+            }
+            __syncthreads();
+        }
+        if (threadIdx.x == 0) {
+            DeltaCand c;
+            c.value = sv[0]; c.valid = sok[0]; c.pos = sp[0];
+            ada.cand[blockIdx.x] = c;
+        }
+    }
+}
+
+template <typename T, int MODE>
+static hipError_t launch_reduce_t(void* shard, int64_t rows, int32_t cols, const Batch& bt, int nb,
+                                  int64_t stride, int K, const int32_t* slot, Ctrl* ctrl, uint64_t tail_cut,
+                                  const AdaArgs& ada, hipStream_t st, int64_t* nblocks_out) {
+    constexpr int VEC = Elem<T>::VEC;
+    const int32_t nchunks = (cols + 64 * VEC - 1) / (64 * VEC);
+    const int64_t ntask = rows * nchunks;
+    const int64_t nblocks = (ntask + 3) / 4;
+    if (nblocks_out) *nblocks_out = nblocks;
+    if (nblocks <= 0) return hipSuccess;
+    hipLaunchKernelGGL((k_reduce<T, MODE>), dim3((unsigned)nblocks), dim3(256), 0, st, (T*)shard, rows, cols,
+                       nchunks, bt, nb, stride, K, slot, ctrl, tail_cut, ada);
+    return hipGetLastError();
+}
+
+int64_t reduce_blocks(int vtype, int64_t rows, int32_t cols) {
+    const int VEC = vtype == kF64 ? 2 : 4;
+    const int64_t nchunks = (cols + 64 * VEC - 1) / (64 * VEC);
+    return (rows * nchunks + 3) / 4;
+}
+
+hipError_t launch_reduce(int vtype, int mode, void* shard, int64_t rows, int32_t cols, const Batch& bt, int nb,
+                         int64_t stride, int K, const int32_t* slot, Ctrl* ctrl, uint64_t tail_cut,
+                         const AdaArgs& ada, hipStream_t st, int64_t* nblocks_out) {
+#define DML_R(T, M) launch_reduce_t<T, M>(shard, rows, cols, bt, nb, stride, K, slot, ctrl, tail_cut, ada, st, nblocks_out)
+    if (vtype == kF32) {
+        if (mode == kAdd) return DML_R(float, kAdd);
+        if (mode == kAdaGrad) return DML_R(float, kAdaGrad);
+        if (mode == kPreReduce) return DML_R(float, kPreReduce);
+    } else if (vtype == kI32) {
+        if (mode == kAdd) return DML_R(int32_t, kAdd);
+        if (mode == kAddCheckI32) return DML_R(int32_t, kAddCheckI32);
+        if (mode == kPreReduce) return DML_R(int32_t, kPreReduce);
+    } else if (vtype == kF64) {
+        if (mode == kAdd) return DML_R(double, kAdd);
+        if (mode == kPreReduce) return DML_R(double, kPreReduce);
+    }
+#undef DML_R
+    return hipErrorInvalidValue;
+}
+
+hipError_t launch_rollback_i32(int32_t* shard, int64_t rows, int32_t cols, const Batch& bt, int nb,
+                               int64_t stride, int K, const int32_t* slot, Ctrl* ctrl, uint64_t tail_cut,
+                               hipStream_t st) {
+    AdaArgs none{};
+    return launch_reduce_t<int32_t, kRollbackI32>(shard, rows, cols, bt, nb, stride, K, slot, ctrl,
+                                                  tail_cut, none, st, nullptr);
+}
+
+// ---------------------------------------------------------------------------
+// maxDelta finalize: reduce the per-block candidates and apply the reference's
+// strict `deltas[i] > maxDelta` update (FloatMatrixStoreAdaGrad.java:273-277).
+__global__ __launch_bounds__(256) void k_maxdelta(const DeltaCand* __restrict__ cand, int64_t n,
+                                                  MaxDelta* __restrict__ md, const Batch bt, int nb,
+                                                  int64_t stride, int K, int V) {
+    __shared__ float sv[256];
+    __shared__ unsigned long long sp[256];
+    __shared__ int sok[256];
+    float v = 0.f;
+    unsigned long long p = kNoPos;
+    int ok = 0;
+    for (int64_t i = threadIdx.x; i < n; i += 256) {
+        const DeltaCand c = cand[i];
+        if (c.valid && (!ok || c.value > v || (c.value == v && c.pos < p))) { ok = 1; v = c.value; p = c.pos; }
+    }
+    sv[threadIdx.x] = v; sp[threadIdx.x] = p; sok[threadIdx.x] = ok;
+    __syncthreads();
+    for (int s = 128; s > 0; s >>= 1) {
+        if ((int)threadIdx.x < s) {
+            const int o = threadIdx.x + s;
+            if (sok[o] && (!sok[threadIdx.x] || sv[o] > sv[threadIdx.x] ||
+                           (sv[o] == sv[threadIdx.x] && sp[o] < sp[threadIdx.x]))) {
+                sv[threadIdx.x] = sv[o]; sp[threadIdx.x] = sp[o]; sok[threadIdx.x] = 1;
+            }
+        }
+        __syncthreads();
+    }
+    if (threadIdx.x == 0 && sok[0] && sv[0] > md->value) {
+        const int gb = (int)(sp[0] >> 40);
+        int b = 0;
+        while (b < nb - 1 && bt.bidx[b] != gb) ++b;
+        const int64_t off = (int64_t)(sp[0] & kOffMask);
+        const int64_t r = off / stride;
+        md->value = sv[0];
+        md->row = (int32_t)ld_key(bt.base[b] + r * stride, K);  // maxDeltaRow = (int)key
+        md->col = (int32_t)((off - r * stride - K) / V);
+    }
+}
+
+hipError_t launch_maxdelta_finalize(const DeltaCand* cand, int64_t n, MaxDelta* md, const Batch& bt, int nb,
+                                    int64_t stride, int K, int V, hipStream_t st) {
+    hipLaunchKernelGGL(k_maxdelta, dim3(1), dim3(256), 0, st, cand, n, md, bt, nb, stride, K, V);
+    return hipGetLastError();
+}
+
+// ---------------------------------------------------------------------------
+// Array stores. Records [key][value] at stride K+VS.
+__global__ __launch_bounds__(256) void k_array_validate(const Batch bt, int64_t stride, int K,
+                                                        int64_t first, int64_t rows, Ctrl* __restrict__ ctrl) {
+    const int b = blockIdx.y;
+    const int64_t r = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (r >= bt.nrec[b]) return;
+    const int64_t off = r * stride;
+    if (row_index(ld_key(bt.base[b] + off, K), first, rows) < 0)
+        atomicMin(&ctrl->cutoff, (unsigned long long)pos_of((uint64_t)bt.bidx[b], (uint64_t)off));
+}
+
+hipError_t launch_array_validate(const Batch& bt, int nb, int64_t max_nrec, int64_t stride, int K,
+                                 int64_t first, int64_t rows, Ctrl* ctrl, hipStream_t st) {
+    if (max_nrec <= 0 || nb <= 0) return hipSuccess;
+    dim3 grid((unsigned)((max_nrec + 255) / 256), (unsigned)nb);
+    hipLaunchKernelGGL(k_array_validate, grid, dim3(256), 0, st, bt, stride, K, first, rows, ctrl);
+    return hipGetLastError();
+}
+
+// One thread per record of one push. Keys inside one push are distinct
+// (the writers serialize a HashMap), so each element receives at most one
+// add per launch and the float atomics reproduce the sequential sum exactly;
+// pushes are ordered by the stream.
+template <typename T, bool CHECK>
+__global__ __launch_bounds__(256) void k_array_apply(T* __restrict__ shard, int64_t rows, const uint8_t* __restrict__ base,
+                                                     int64_t nrec, int b_global, int64_t stride, int K,
+                                                     int64_t first, Ctrl* __restrict__ ctrl, uint64_t tail_cut) {
+    const int64_t r = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (r >= nrec) return;
+    uint64_t cut = ctrl->cutoff;
+    if (tail_cut < cut) cut = tail_cut;
+    const int64_t off = r * stride;
+    if (pos_of((uint64_t)b_global, (uint64_t)off) >= cut) return;
+    const int64_t idx = row_index(ld_key(base + off, K), first, rows);
+    if (idx < 0) return;  // unreachable: validated, positions before the cutoff are in range
+    const T u = Elem<T>::load(base + off + K);
+    if constexpr (CHECK) {
+        const int32_t old = atomicAdd((int32_t*)&shard[idx], (int32_t)u);
+        if ((int32_t)((uint32_t)old + (uint32_t)u) < 0)
+            atomicMin(&ctrl->neg_pos, (unsigned long long)pos_of((uint64_t)b_global, (uint64_t)(off + K)));
+    } else {
+        atomicAdd(&shard[idx], u);
+    }
+}
+
+hipError_t launch_array_apply(int vtype, void* shard, int64_t rows, const uint8_t* base, int64_t nrec, int b_global,
+                              int64_t stride, int K, int64_t first, Ctrl* ctrl, uint64_t tail_cut, hipStream_t st) {
+    if (nrec <= 0) return hipSuccess;
+    const dim3 grid((unsigned)((nrec + 255) / 256));
+    if (vtype == kF32)
+        hipLaunchKernelGGL((k_array_apply<float, false>), grid, dim3(256), 0, st, (float*)shard, rows, base, nrec,
+                           b_global, stride, K, first, ctrl, tail_cut);
+    else if (vtype == kI32)
+        hipLaunchKernelGGL((k_array_apply<int32_t, true>), grid, dim3(256), 0, st, (int32_t*)shard, rows, base, nrec,
+                           b_global, stride, K, first, ctrl, tail_cut);
+    else
+        hipLaunchKernelGGL((k_array_apply<double, false>), grid, dim3(256), 0, st, (double*)shard, rows, base, nrec,
+                           b_global, stride, K, first, ctrl, tail_cut);
+    return hipGetLastError();
+}
+
+// Undo (mod 2^32) every int32 array add positioned after the first negative.
+__global__ __launch_bounds__(256) void k_array_rollback(int32_t* __restrict__ shard, int64_t rows,
+                                                        const uint8_t* __restrict__ base, int64_t nrec, int b_global,
+                                                        int64_t stride, int K, int64_t first, Ctrl* __restrict__ ctrl,
+                                                        uint64_t tail_cut) {
+    const uint64_t neg = ctrl->neg_pos;
+    if (neg == kNoPos) return;
+    const int64_t r = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (r >= nrec) return;
+    uint64_t cut = ctrl->cutoff;
+    if (tail_cut < cut) cut = tail_cut;
+    const int64_t off = r * stride;
+    if (pos_of((uint64_t)b_global, (uint64_t)off) >= cut) return;
+    if (pos_of((uint64_t)b_global, (uint64_t)(off + K)) <= neg) return;
+    const int64_t idx = row_index(ld_key(base + off, K), first, rows);
+    if (idx < 0) return;
+    atomicSub(&shard[idx], (int32_t)ld32(base + off + K));
+}
+
+hipError_t launch_array_rollback_i32(int32_t* shard, int64_t rows, const uint8_t* base, int64_t nrec, int b_global,
+                                     int64_t stride, int K, int64_t first, Ctrl* ctrl, uint64_t tail_cut,
+                                     hipStream_t st) {
+    if (nrec <= 0) return hipSuccess;
+    hipLaunchKernelGGL(k_array_rollback, dim3((unsigned)((nrec + 255) / 256)), dim3(256), 0, st, shard, rows, base,
+                       nrec, b_global, stride, K, first, ctrl, tail_cut);
+    return hipGetLastError();
+}
+
+// ---------------------------------------------------------------------------
+template <typename T>
+__global__ void k_fill(T* __restrict__ p, int64_t n, T v) {
+    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x)
+        p[i] = v;
+}
+static unsigned grid_for(int64_t n) {
+    int64_t g = (n + 255) / 256;
+    if (g > 8192) g = 8192;
+    return (unsigned)(g < 1 ? 1 : g);
+}
+hipError_t launch_fill(int vtype, void* p, int64_t n, double v, hipStream_t st) {
+    if (n <= 0) return hipSuccess;
+    if (vtype == kF32) hipLaunchKernelGGL(k_fill<float>, dim3(grid_for(n)), dim3(256), 0, st, (float*)p, n, (float)v);
+    else if (vtype == kI32) hipLaunchKernelGGL(k_fill<int32_t>, dim3(grid_for(n)), dim3(256), 0, st, (int32_t*)p, n, (int32_t)v);
+    else hipLaunchKernelGGL(k_fill<double>, dim3(grid_for(n)), dim3(256), 0, st, (double*)p, n, v);
+    return hipGetLastError();
+}
+hipError_t launch_fill_f32(float* p, int64_t n, float v, hipStream_t st) {
+    if (n <= 0) return hipSuccess;
+    hipLaunchKernelGGL(k_fill<float>, dim3(grid_for(n)), dim3(256), 0, st, p, n, v);
+    return hipGetLastError();
+}
+
+// shard += src, element-wise (owner apply after a reduce-scatter).
+template <typename T>
+__global__ __launch_bounds__(256) void k_apply_dense(T* __restrict__ shard, const T* __restrict__ src, int64_t n) {
+    constexpr int VEC = Elem<T>::VEC;
+    const int64_t nvec = n / VEC;
+    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < nvec; i += (int64_t)gridDim.x * blockDim.x) {
+        T a[VEC], b[VEC];
+        unpack<T>(((const u32x4*)shard)[i], a);
+        unpack<T>(((const u32x4*)src)[i], b);
+#pragma unroll
+        for (int e = 0; e < VEC; ++e) a[e] = Elem<T>::add(a[e], b[e]);
+        ((u32x4*)shard)[i] = pack<T>(a);
+    }
+    const int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (t < n - nvec * VEC) shard[nvec * VEC + t] = Elem<T>::add(shard[nvec * VEC + t], src[nvec * VEC + t]);
+}
+hipError_t launch_apply_dense(int vtype, void* shard, const void* src, int64_t n, hipStream_t st) {
+    if (n <= 0) return hipSuccess;
+    const unsigned g = 256 * 8;
+    if (vtype == kF32) hipLaunchKernelGGL(k_apply_dense<float>, dim3(g), dim3(256), 0, st, (float*)shard, (const float*)src, n);
+    else if (vtype == kI32) hipLaunchKernelGGL(k_apply_dense<int32_t>, dim3(g), dim3(256), 0, st, (int32_t*)shard, (const int32_t*)src, n);
+    else hipLaunchKernelGGL(k_apply_dense<double>, dim3(g), dim3(256), 0, st, (double*)shard, (const double*)src, n);
+    return hipGetLastError();
+}
+
+// ---------------------------------------------------------------------------
+// handleFetch encode, dense-column layouts (FloatMatrixStore.java:140-153 etc.).
+// One thread per (key, column). `value_slot` = bytes per column in the output
+// record (4/8; 8 for AdaGrad value+alpha and FloatArrayStore's 8-byte slot).
+__device__ inline void st32(uint8_t* p, uint32_t v) { *(uint32_t*)p = v; }
+
+template <typename T>
+__global__ void k_fetch(const T* __restrict__ shard, const float* __restrict__ alpha, int32_t cols,
+                        const int64_t* __restrict__ keys, int64_t n, int64_t first, uint8_t* __restrict__ out,
+                        int64_t rec, int K, int value_slot) {
+    const int64_t total = n * (int64_t)cols;
+    for (int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; t < total; t += (int64_t)gridDim.x * blockDim.x) {
+        const int64_t j = t / cols;
+        const int32_t c = (int32_t)(t - j * cols);
+        const int64_t key = keys[j];
+        const int64_t idx = key - first;
+        uint8_t* o = out + j * rec;
+        if (c == 0) {
+            st32(o, (uint32_t)key);
+            if (K == 8) st32(o + 4, (uint32_t)((uint64_t)key >> 32));
+        }
+        uint8_t* v = o + K + (int64_t)c * value_slot;
+        const T x = shard[idx * cols + c];
+        if constexpr (sizeof(T) == 4) {
+            st32(v, __builtin_bit_cast(uint32_t, x));
+        } else {
+            const uint64_t u = __builtin_bit_cast(uint64_t, x);
+            st32(v, (uint32_t)u); st32(v + 4, (uint32_t)(u >> 32));
+        }
+        if (alpha) st32(v + 4, __float_as_uint(alpha[idx * cols + c]));
+    }
+}
+hipError_t launch_fetch(int vtype, const void* shard, const float* alpha, int32_t cols, const int64_t* keys, int64_t n,
+                        int64_t first, uint8_t* out, int64_t rec, int K, int value_slot, hipStream_t st) {
+    const int64_t total = n * (int64_t)cols;
+    if (total <= 0) return hipSuccess;
+    const dim3 g(grid_for(total));
+    if (vtype == kF32) hipLaunchKernelGGL(k_fetch<float>, g, dim3(256), 0, st, (const float*)shard, alpha, cols, keys, n, first, out, rec, K, value_slot);
+    else if (vtype == kI32) hipLaunchKernelGGL(k_fetch<int32_t>, g, dim3(256), 0, st, (const int32_t*)shard, alpha, cols, keys, n, first, out, rec, K, value_slot);
+    else hipLaunchKernelGGL(k_fetch<double>, g, dim3(256), 0, st, (const double*)shard, alpha, cols, keys, n, first, out, rec, K, value_slot);
+    return hipGetLastError();
+}
+
+// Big-endian <-> native byte swap (DataOutputStream.writeFloat/writeInt/writeDouble).
+__global__ void k_bswap4(const uint32_t* __restrict__ s, uint32_t* __restrict__ d, int64_t n) {
+    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x)
+        d[i] = __builtin_bswap32(s[i]);
+}
+__global__ void k_bswap8(const uint64_t* __restrict__ s, uint64_t* __restrict__ d, int64_t n) {
+    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x)
+        d[i] = __builtin_bswap64(s[i]);
+}
+hipError_t launch_bswap(int V, const void* src, void* dst, int64_t n, hipStream_t st) {
+    if (n <= 0) return hipSuccess;
+    if (V == 4) hipLaunchKernelGGL(k_bswap4, dim3(grid_for(n)), dim3(256), 0, st, (const uint32_t*)src, (uint32_t*)dst, n);
+    else hipLaunchKernelGGL(k_bswap8, dim3(grid_for(n)), dim3(256), 0, st, (const uint64_t*)src, (uint64_t*)dst, n);
+    return hipGetLastError();
+}
+
+// ---------------------------------------------------------------------------
+// Synthetic data (DESIGN.md §Synthetic data; CPU twin: oracle/dml_oracle.c).
+__device__ inline int32_t synth_grad_int(uint64_t h) {
+    const int32_t s = (int32_t)(h & 0xFFFF) + (int32_t)((h >> 16) & 0xFFFF) + (int32_t)((h >> 32) & 0xFFFF) +
+                      (int32_t)((h >> 48) & 0xFFFF);
+    return s - 131070;
+}
+__device__ inline void put_value(uint8_t* p, int vtype, uint64_t h) {
+    if (vtype == kF32) {
+        st32(p, __float_as_uint((float)synth_grad_int(h) * 0x1p-25f));
+    } else if (vtype == kF64) {
+        const uint64_t u = __builtin_bit_cast(uint64_t, (double)synth_grad_int(h) * 0x1p-25);
+        st32(p, (uint32_t)u); st32(p + 4, (uint32_t)(u >> 32));
+    } else {
+        st32(p, (uint32_t)((int32_t)(h % 5) - 2));
+    }
+}
+__device__ inline void put_key(uint8_t* p, int K, int64_t key) {
+    st32(p, (uint32_t)key);
+    if (K == 8) st32(p + 4, (uint32_t)((uint64_t)key >> 32));
+}
+
+// perm: record r -> row (pa*r + pc) mod n; host guarantees pa < 2^32, r < 2^32.
+__global__ void k_synth_dense(uint8_t* __restrict__ out, int K, int vtype, int64_t first, int64_t shard_rows,
+                              int64_t nrec, int32_t cols, uint64_t s0, uint64_t pa, uint64_t pc) {
+    const int V = vtype == kF64 ? 8 : 4;
+    const int64_t stride = K + (int64_t)V * cols;
+    const int64_t total = nrec * (int64_t)cols;
+    for (int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; t < total; t += (int64_t)gridDim.x * blockDim.x) {
+        const int64_t r = t / cols;
+        const int32_t c = (int32_t)(t - r * cols);
+        const uint64_t row = ((pa * (uint64_t)r) % (uint64_t)shard_rows + pc) % (uint64_t)shard_rows;
+        uint8_t* rec = out + r * stride;
+        if (c == 0) put_key(rec, K, first + (int64_t)row);
+        put_value(rec + K + (int64_t)V * c, vtype, splitmix64_dev(s0 + row * (uint64_t)cols + (uint64_t)c));
+    }
+}
+hipError_t launch_synth_dense(uint8_t* out, int K, int vtype, int64_t first, int64_t shard_rows, int64_t nrec,
+                              int32_t cols, uint64_t s0, uint64_t pa, uint64_t pc, hipStream_t st) {
+    hipLaunchKernelGGL(k_synth_dense, dim3(8192), dim3(256), 0, st, out, K, vtype, first, shard_rows, nrec, cols, s0, pa, pc);
+    return hipGetLastError();
+}
+
+__global__ void k_synth_sparse(uint8_t* __restrict__ out, int K, int vtype, int value_stride, int64_t first,
+                               int64_t key_space, int64_t nrec, uint64_t s0, uint64_t pa, uint64_t pc) {
+    const int64_t stride = K + value_stride;
+    for (int64_t r = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; r < nrec; r += (int64_t)gridDim.x * blockDim.x) {
+        const uint64_t i = ((pa * (uint64_t)r) % (uint64_t)key_space + pc) % (uint64_t)key_space;
+        uint8_t* rec = out + r * stride;
+        put_key(rec, K, first + (int64_t)i);
+        for (int z = 0; z < value_stride; z += 4) st32(rec + K + z, 0u);
+        put_value(rec + K, vtype, splitmix64_dev(s0 + i));
+    }
+}
+hipError_t launch_synth_sparse(uint8_t* out, int K, int vtype, int value_stride, int64_t first, int64_t key_space,
+                               int64_t nrec, uint64_t s0, uint64_t pa, uint64_t pc, hipStream_t st) {
+    hipLaunchKernelGGL(k_synth_sparse, dim3(8192), dim3(256), 0, st, out, K, vtype, value_stride, first, key_space, nrec,
+                       s0, pa, pc);
+    return hipGetLastError();
+}
+
+__global__ void k_synth_fill(int vtype, void* p, int64_t n, uint64_t s0) {
+    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
+        const uint64_t h = splitmix64_dev(s0 + (uint64_t)i);
+        if (vtype == kF32) ((float*)p)[i] = (float)((int32_t)(h % 100) - 50) * 0x1p-17f;
+        else if (vtype == kF64) ((double*)p)[i] = (double)((int32_t)(h % 100) - 50) * 0x1p-17;
+        else ((int32_t*)p)[i] = 64 + (int32_t)(h % 51);
+    }
+}
+hipError_t launch_synth_fill(int vtype, void* p, int64_t n, uint64_t s0, hipStream_t st) {
+    hipLaunchKernelGGL(k_synth_fill, dim3(8192), dim3(256), 0, st, vtype, p, n, s0);
+    return hipGetLastError();
+}
+
+// Row index of every record of one push (-1 outside the shard): the host's
+// duplicate-row replay reads these to split the push into unique-row layers.
+__global__ void k_key_rows(const uint8_t* __restrict__ base, int64_t nrec, int64_t stride, int K, int64_t first,
+                           int64_t rows, int32_t* __restrict__ out) {
+    for (int64_t r = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; r < nrec; r += (int64_t)gridDim.x * blockDim.x)
+        out[r] = (int32_t)row_index(ld_key(base + r * stride, K), first, rows);
+}
+hipError_t launch_key_rows(const uint8_t* base, int64_t nrec, int64_t stride, int K, int64_t first, int64_t rows,
+                           int32_t* out, hipStream_t st) {
+    if (nrec <= 0) return hipSuccess;
+    hipLaunchKernelGGL(k_key_rows, dim3(grid_for(nrec)), dim3(256), 0, st, base, nrec, stride, K, first, rows, out);
+    return hipGetLastError();
+}
+
+}  // namespace dml

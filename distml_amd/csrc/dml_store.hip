@@ -1,0 +1,953 @@
+// dml_store.hip — host implementation of the C-ABI in include/distml_ps.h.
+//
+// One dml_store = one DataStore shard (DataStore.java:17-38) resident in HBM on
+// one device, with its own HIP stream, a mutex (the reference calls a store
+// from three threads: PSAgent.java:278, PSActor.java:171-251, PSSync.java:131),
+// and a workspace: [Ctrl | slot table rows x kMaxW int32].
+//
+// A push batch runs per chunk of <= kMaxW pushes:
+//   memset(Ctrl+slots) -> k_index -> k_reduce (matrix)   or
+//   memset(Ctrl) -> k_array_validate -> k_array_apply x pushes (array)
+// and is "retired" later (next call, flush, or immediately in sync mode):
+// sync, read Ctrl, replay pushes that repeat a row (exact layered path), undo
+// int32 adds past the first negative counter (exact mod 2^32), and turn the
+// first failing position into the status code, key and column the reference's
+// exception carries.
+#include "distml_ps.h"
+#include "dml_internal.h"
+
+#include <algorithm>
+#include <cstdio>
+#include <cstring>
+#include <mutex>
+#include <string>
+#include <unordered_map>
+#include <vector>
+
+using namespace dml;
+
+static thread_local std::string g_err;
+
+static int set_err(int code, const std::string& msg) {
+    g_err = msg;
+    return code;
+}
+
+#define HIPCHK(x)                                                                                  \
+    do {                                                                                           \
+        hipError_t e_ = (x);                                                                       \
+        if (e_ != hipSuccess) return set_err(DML_E_HIP, std::string(#x) + ": " + hipGetErrorString(e_)); \
+    } while (0)
+
+namespace {
+
+struct DeviceGuard {
+    int prev = -1;
+    explicit DeviceGuard(int dev) {
+        if (hipGetDevice(&prev) != hipSuccess) prev = -1;
+        if (prev != dev) (void)hipSetDevice(dev);
+    }
+    ~DeviceGuard() {
+        int cur = -1;
+        if (prev >= 0 && hipGetDevice(&cur) == hipSuccess && cur != prev) (void)hipSetDevice(prev);
+    }
+};
+
+struct Chunk {
+    Batch bt{};
+    int nb = 0;
+    int64_t max_nrec = 0;
+    uint64_t tail_cut = kNoPos;
+    uint64_t tail_cut_keyok = kNoPos;  // tail errors whose record key is complete (key readable)
+};
+
+int vtype_of(const dml_desc& d) { return d.value_type; }
+
+}  // namespace
+
+struct dml_store {
+    std::mutex mu;
+    int device = 0;
+    hipStream_t stream = nullptr;
+    dml_desc desc{};
+    uint32_t flags = 0;
+    bool is_matrix = false, adagrad = false;
+    int K = 4, V = 4;           // DataDesc keySize / valueSize (DataDesc.java:50-51)
+    int array_vs = 4;           // array record value stride
+    int64_t first = 0, last = 0, rows = 0;
+    int32_t cols = 1;
+    int64_t stride = 0;         // record stride
+    void* data = nullptr;       // rows*cols values
+    float* alpha = nullptr;     // AdaGrad (FloatMatrixStoreAdaGrad.java:23-24)
+    float* delta = nullptr;
+    DeltaCand* cand = nullptr;
+    int64_t cand_n = 0;
+    MaxDelta* md = nullptr;
+    float initial_alpha = 0.f, min_alpha = 0.f, factor = 1.5f;  // :22, :26
+    uint8_t* ws = nullptr;      // Ctrl + slot table
+    size_t ws_bytes = 0;
+    Ctrl* ctrl = nullptr;
+    int32_t* slot = nullptr;
+    Ctrl* hctrl = nullptr;      // pinned mirror
+    // staging for host-memory pushes
+    uint8_t* hstage = nullptr;
+    uint8_t* dstage = nullptr;
+    size_t stage_cap = 0;
+    hipEvent_t h2d_done = nullptr;
+    // pending (un-retired) chunk
+    bool pending = false;
+    Chunk pend;
+    // sticky error (first failure)
+    int err = 0;
+    int64_t err_key = 0;
+    int32_t err_col = -1;
+    // timing of the dominant kernel
+    bool timing = false;
+    std::vector<std::pair<hipEvent_t, hipEvent_t>> ev_used, ev_free;
+    double timed_ms = 0.0;
+    int64_t timed_n = 0;
+};
+
+namespace {
+
+int value_read_bytes(const dml_store* s) { return s->V; }
+
+std::pair<hipEvent_t, hipEvent_t> ev_pair(dml_store* s) {
+    if (!s->ev_free.empty()) {
+        auto p = s->ev_free.back();
+        s->ev_free.pop_back();
+        return p;
+    }
+    std::pair<hipEvent_t, hipEvent_t> p{nullptr, nullptr};
+    (void)hipEventCreate(&p.first);
+    (void)hipEventCreate(&p.second);
+    return p;
+}
+
+// Collect elapsed times of recorded event pairs (stream must be synced).
+void ev_collect(dml_store* s) {
+    for (auto& p : s->ev_used) {
+        float ms = 0.f;
+        if (hipEventElapsedTime(&ms, p.first, p.second) == hipSuccess) {
+            s->timed_ms += ms;
+            s->timed_n += 1;
+        }
+        s->ev_free.push_back(p);
+    }
+    s->ev_used.clear();
+}
+
+int ensure_stage(dml_store* s, size_t bytes) {
+    if (bytes <= s->stage_cap) return DML_OK;
+    if (s->hstage) (void)hipHostFree(s->hstage);
+    if (s->dstage) (void)hipFree(s->dstage);
+    s->hstage = nullptr;
+    s->dstage = nullptr;
+    s->stage_cap = 0;
+    size_t cap = std::max<size_t>(bytes, 1 << 20);
+    HIPCHK(hipHostMalloc((void**)&s->hstage, cap, hipHostMallocDefault));
+    HIPCHK(hipMalloc((void**)&s->dstage, cap));
+    s->stage_cap = cap;
+    return DML_OK;
+}
+
+// Per-push record accounting: records with a complete key, and the position of
+// the first truncated access of a ragged tail (DataDesc.readInt past data.length).
+void plan_bucket(const dml_store* s, int64_t len, int gb, int64_t* nrec, uint64_t* tail_cut, bool* key_ok) {
+    const int64_t nfull = len / s->stride, tail = len % s->stride;
+    *nrec = nfull;
+    *tail_cut = kNoPos;
+    *key_ok = false;
+    if (tail == 0) return;
+    const int64_t t0 = nfull * s->stride;
+    if (s->is_matrix) {
+        if (tail < s->K) {
+            *tail_cut = pos_of((uint64_t)gb, (uint64_t)t0);
+        } else {
+            *nrec = nfull + 1;  // key complete: the index sees it (out-of-shard key reported first)
+            const int64_t nvals = (tail - s->K) / s->V;
+            *tail_cut = pos_of((uint64_t)gb, (uint64_t)(t0 + s->K + nvals * s->V));
+            *key_ok = true;
+        }
+    } else {
+        if (tail >= s->K + value_read_bytes(s)) {
+            *nrec = nfull + 1;  // readable record (FloatArrayStore 8-byte stride, short last slot)
+        } else {
+            *tail_cut = pos_of((uint64_t)gb, (uint64_t)t0);
+            *key_ok = tail >= s->K;
+        }
+    }
+}
+
+int reduce_mode(const dml_store* s) {
+    if (s->adagrad) return kAdaGrad;
+    if (s->desc.value_type == DML_ELEMENT_TYPE_INT && s->desc.dense_column) return kAddCheckI32;
+    return kAdd;
+}
+
+int launch_chunk(dml_store* s, const Chunk& c) {
+    const size_t clear = s->is_matrix ? s->ws_bytes : sizeof(Ctrl);
+    HIPCHK(hipMemsetAsync(s->ws, 0xFF, clear, s->stream));
+    if (s->is_matrix) {
+        HIPCHK(launch_index(c.bt, c.nb, c.max_nrec, s->stride, s->K, s->first, s->rows, s->slot, s->ctrl, s->stream));
+        std::pair<hipEvent_t, hipEvent_t> ev{};
+        if (s->timing) {
+            ev = ev_pair(s);
+            HIPCHK(hipEventRecord(ev.first, s->stream));
+        }
+        AdaArgs ada{s->alpha, s->delta, s->cand, s->initial_alpha, s->min_alpha, s->factor};
+        int64_t nblk = 0;
+        HIPCHK(launch_reduce(vtype_of(s->desc), reduce_mode(s), s->data, s->rows, s->cols, c.bt, c.nb, s->stride,
+                             s->K, s->slot, s->ctrl, c.tail_cut, ada, s->stream, &nblk));
+        if (s->timing) {
+            HIPCHK(hipEventRecord(ev.second, s->stream));
+            s->ev_used.push_back(ev);
+        }
+        if (s->adagrad)
+            HIPCHK(launch_maxdelta_finalize(s->cand, nblk, s->md, c.bt, c.nb, s->stride, s->K, s->V, s->stream));
+    } else {
+        HIPCHK(launch_array_validate(c.bt, c.nb, c.max_nrec, s->stride, s->K, s->first, s->rows, s->ctrl, s->stream));
+        for (int b = 0; b < c.nb; ++b) {
+            std::pair<hipEvent_t, hipEvent_t> ev{};
+            if (s->timing) {
+                ev = ev_pair(s);
+                HIPCHK(hipEventRecord(ev.first, s->stream));
+            }
+            HIPCHK(launch_array_apply(vtype_of(s->desc), s->data, s->rows, c.bt.base[b], c.bt.nrec[b], c.bt.bidx[b],
+                                      s->stride, s->K, s->first, s->ctrl, c.tail_cut, s->stream));
+            if (s->timing) {
+                HIPCHK(hipEventRecord(ev.second, s->stream));
+                s->ev_used.push_back(ev);
+            }
+        }
+    }
+    return DML_OK;
+}
+
+int read_ctrl(dml_store* s, Ctrl* out) {
+    HIPCHK(hipMemcpyAsync(s->hctrl, s->ctrl, sizeof(Ctrl), hipMemcpyDeviceToHost, s->stream));
+    HIPCHK(hipStreamSynchronize(s->stream));
+    *out = *s->hctrl;
+    return DML_OK;
+}
+
+// Exact replay of a chunk in which some push lists a row twice: split each push
+// into layers (k-th occurrence of each row), apply layers in (push, layer)
+// order. Per element the adds keep their reference order.
+int replay_layers(dml_store* s, const Chunk& c, Ctrl* ctl) {
+    std::vector<Chunk> vchunks(1);
+    std::vector<std::vector<int32_t>> vslots;  // per virtual column: (row, record) pairs flattened
+    struct VCol { int src_b; std::vector<std::pair<int32_t, int32_t>> rr; };
+    std::vector<VCol> cols;
+    int32_t* drows = nullptr;
+    HIPCHK(hipMalloc((void**)&drows, sizeof(int32_t) * std::max<int64_t>(c.max_nrec, 1)));
+    std::vector<int32_t> hrows;
+    for (int b = 0; b < c.nb; ++b) {
+        const int64_t n = c.bt.nrec[b];
+        hrows.resize((size_t)n);
+        if (n > 0) {
+            hipError_t e = launch_key_rows(c.bt.base[b], n, s->stride, s->K, s->first, s->rows, drows, s->stream);
+            if (e == hipSuccess) e = hipMemcpyAsync(hrows.data(), drows, sizeof(int32_t) * n, hipMemcpyDeviceToHost, s->stream);
+            if (e == hipSuccess) e = hipStreamSynchronize(s->stream);
+            if (e != hipSuccess) { (void)hipFree(drows); return set_err(DML_E_HIP, hipGetErrorString(e)); }
+        }
+        std::unordered_map<int32_t, int32_t> occ;
+        std::vector<VCol> layers;
+        for (int64_t r = 0; r < n; ++r) {
+            const int32_t row = hrows[(size_t)r];
+            if (row < 0) continue;  // out of shard: cutoff already covers it
+            const int32_t l = occ[row]++;
+            if ((int)layers.size() <= l) layers.push_back(VCol{b, {}});
+            layers[(size_t)l].rr.emplace_back(row, (int32_t)r);
+        }
+        for (auto& L : layers) cols.push_back(std::move(L));
+    }
+    (void)hipFree(drows);
+    // ctrl keeps the key-error cutoff of the first pass; clear neg/no_dup.
+    Ctrl init = *ctl;
+    init.neg_pos = kNoPos;
+    init.no_dup = 0xFFFFFFFFu;
+    HIPCHK(hipMemcpy(s->ctrl, &init, sizeof(Ctrl), hipMemcpyHostToDevice));
+    std::vector<int32_t> hslot((size_t)s->rows * kMaxW);
+    AdaArgs ada{s->alpha, s->delta, s->cand, s->initial_alpha, s->min_alpha, s->factor};
+    std::vector<Chunk> done;
+    for (size_t v0 = 0; v0 < cols.size(); v0 += kMaxW) {
+        Chunk vc;
+        vc.nb = (int)std::min<size_t>(kMaxW, cols.size() - v0);
+        vc.tail_cut = c.tail_cut;
+        std::fill(hslot.begin(), hslot.end(), -1);
+        for (int j = 0; j < vc.nb; ++j) {
+            const VCol& col = cols[v0 + (size_t)j];
+            vc.bt.base[j] = c.bt.base[col.src_b];
+            vc.bt.len[j] = c.bt.len[col.src_b];
+            vc.bt.nrec[j] = c.bt.nrec[col.src_b];
+            vc.bt.bidx[j] = c.bt.bidx[col.src_b];
+            for (auto& pr : col.rr) hslot[(size_t)pr.first * kMaxW + (size_t)j] = pr.second;
+        }
+        HIPCHK(hipMemcpy(s->slot, hslot.data(), hslot.size() * sizeof(int32_t), hipMemcpyHostToDevice));
+        int64_t nblk = 0;
+        HIPCHK(launch_reduce(vtype_of(s->desc), reduce_mode(s), s->data, s->rows, s->cols, vc.bt, vc.nb, s->stride,
+                             s->K, s->slot, s->ctrl, vc.tail_cut, ada, s->stream, &nblk));
+        if (s->adagrad)
+            HIPCHK(launch_maxdelta_finalize(s->cand, nblk, s->md, vc.bt, vc.nb, s->stride, s->K, s->V, s->stream));
+        HIPCHK(hipStreamSynchronize(s->stream));
+        done.push_back(vc);
+    }
+    int rc = read_ctrl(s, ctl);
+    if (rc) return rc;
+    if (ctl->neg_pos != kNoPos) {
+        // undo every add after the first negative, across all layers
+        for (auto& vc : done) {
+            std::fill(hslot.begin(), hslot.end(), -1);
+            size_t v0 = (size_t)(&vc - &done[0]) * kMaxW;
+            for (int j = 0; j < vc.nb; ++j)
+                for (auto& pr : cols[v0 + (size_t)j].rr) hslot[(size_t)pr.first * kMaxW + (size_t)j] = pr.second;
+            HIPCHK(hipMemcpy(s->slot, hslot.data(), hslot.size() * sizeof(int32_t), hipMemcpyHostToDevice));
+            HIPCHK(launch_rollback_i32((int32_t*)s->data, s->rows, s->cols, vc.bt, vc.nb, s->stride, s->K, s->slot,
+                                       s->ctrl, vc.tail_cut, s->stream));
+            HIPCHK(hipStreamSynchronize(s->stream));
+        }
+    }
+    return DML_OK;
+}
+
+int64_t read_key_at(dml_store* s, const uint8_t* dev_rec) {
+    uint8_t kb[8] = {0};
+    if (hipMemcpy(kb, dev_rec, (size_t)s->K, hipMemcpyDeviceToHost) != hipSuccess) return 0;
+    if (s->K == 4) {
+        int32_t k;
+        std::memcpy(&k, kb, 4);
+        return k;
+    }
+    int64_t k;
+    std::memcpy(&k, kb, 8);
+    return k;
+}
+
+const uint8_t* base_of(const Chunk& c, int gb) {
+    for (int b = 0; b < c.nb; ++b)
+        if (c.bt.bidx[b] == gb) return c.bt.base[b];
+    return nullptr;
+}
+
+int record_error(dml_store* s, int code, int64_t key, int32_t col) {
+    if (!s->err) {
+        s->err = code;
+        s->err_key = key;
+        s->err_col = col;
+    }
+    static const char* names[] = {"", "IllegalArgumentException", "ArrayIndexOutOfBoundsException (key outside shard)",
+                                  "ArrayIndexOutOfBoundsException (truncated push)", "IllegalStateException (negative counter)"};
+    char buf[160];
+    std::snprintf(buf, sizeof buf, "%s: key=%lld col=%d", names[code], (long long)key, col);
+    return set_err(code, buf);
+}
+
+// Retire the pending chunk: see file header.
+int retire(dml_store* s) {
+    if (!s->pending) return DML_OK;
+    s->pending = false;
+    const Chunk& c = s->pend;
+    Ctrl ctl;
+    int rc = read_ctrl(s, &ctl);
+    if (rc) return rc;
+    if (s->timing) ev_collect(s);
+    if (s->is_matrix && ctl.no_dup == 0u) {
+        rc = replay_layers(s, c, &ctl);
+        if (rc) return rc;
+    } else if (ctl.neg_pos != kNoPos) {
+        if (s->is_matrix) {
+            HIPCHK(launch_rollback_i32((int32_t*)s->data, s->rows, s->cols, c.bt, c.nb, s->stride, s->K, s->slot,
+                                       s->ctrl, c.tail_cut, s->stream));
+        } else {
+            for (int b = 0; b < c.nb; ++b)
+                HIPCHK(launch_array_rollback_i32((int32_t*)s->data, s->rows, c.bt.base[b], c.bt.nrec[b], c.bt.bidx[b],
+                                                 s->stride, s->K, s->first, s->ctrl, c.tail_cut, s->stream));
+        }
+        HIPCHK(hipStreamSynchronize(s->stream));
+    }
+    const uint64_t cut = std::min<uint64_t>(ctl.cutoff, c.tail_cut);
+    if (ctl.neg_pos != kNoPos && ctl.neg_pos < cut) {
+        const int gb = (int)(ctl.neg_pos >> 40);
+        const int64_t off = (int64_t)(ctl.neg_pos & kOffMask);
+        const int64_t r = off / s->stride;
+        const int32_t col = s->is_matrix ? (int32_t)((off - r * s->stride - s->K) / s->V) : -1;
+        return record_error(s, DML_E_NEGATIVE_COUNTER, read_key_at(s, base_of(c, gb) + r * s->stride), col);
+    }
+    if (cut != kNoPos) {
+        const int gb = (int)(cut >> 40);
+        const int64_t off = (int64_t)(cut & kOffMask);
+        const int64_t r = off / s->stride;
+        const uint8_t* rec = base_of(c, gb) + r * s->stride;
+        if (ctl.cutoff <= c.tail_cut) return record_error(s, DML_E_KEY_OUT_OF_SHARD, read_key_at(s, rec), -1);
+        // truncated: the key is known when the record's key bytes were complete
+        int64_t len = 0;
+        for (int b = 0; b < c.nb; ++b)
+            if (c.bt.bidx[b] == gb) len = c.bt.len[b];
+        const bool key_ok = len - r * s->stride >= s->K;
+        int32_t col = -1;
+        if (s->is_matrix && key_ok) col = (int32_t)((off - r * s->stride - s->K) / s->V);
+        return record_error(s, DML_E_TRUNCATED, key_ok ? read_key_at(s, rec) : 0, col);
+    }
+    return DML_OK;
+}
+
+// Run `n` device-resident pushes (global indices b0..b0+n-1) as ordered chunks.
+// The last chunk stays pending (retired by the caller or a later call).
+int run_batch(dml_store* s, const uint8_t* const* dptr, const int64_t* lens, int n) {
+    for (int c0 = 0; c0 < n; c0 += kMaxW) {
+        if (s->pending) {
+            int rc = retire(s);
+            if (rc) return rc;
+        }
+        Chunk c;
+        c.nb = std::min(kMaxW, n - c0);
+        for (int j = 0; j < c.nb; ++j) {
+            const int gb = c0 + j;
+            int64_t nrec;
+            uint64_t tcut;
+            bool key_ok;
+            plan_bucket(s, lens[gb], gb, &nrec, &tcut, &key_ok);
+            c.bt.base[j] = dptr[gb];
+            c.bt.len[j] = lens[gb];
+            c.bt.nrec[j] = nrec;
+            c.bt.bidx[j] = gb;
+            c.max_nrec = std::max(c.max_nrec, nrec);
+            c.tail_cut = std::min(c.tail_cut, tcut);
+        }
+        if (c.max_nrec == 0 && c.tail_cut == kNoPos) continue;  // empty pushes: nothing to apply
+        int rc = launch_chunk(s, c);
+        if (rc) return rc;
+        s->pend = c;
+        s->pending = true;
+    }
+    return DML_OK;
+}
+
+int check_store(dml_store* s) {
+    if (!s) return set_err(DML_E_INVALID_ARG, "null store");
+    return DML_OK;
+}
+
+// Entry check shared by every mutating/reading call: retire pending work and
+// refuse to run once the store has failed (the reference's PSAgent loop ends
+// with the exception, PSAgent.java:188-191).
+int begin_call(dml_store* s) {
+    int rc = retire(s);
+    if (rc) return rc;
+    return DML_OK;
+}
+
+}  // namespace
+
+// ===========================================================================
+extern "C" {
+
+const char* dml_last_error(void) { return g_err.c_str(); }
+const char* dml_version(void) { return "distml_amd 0.1 (gfx950)"; }
+
+int dml_linear_split(int64_t first_key, int64_t last_key, int32_t n, int64_t* first_out, int64_t* last_out) {
+    if (n <= 0 || !first_out || !last_out) return set_err(DML_E_INVALID_ARG, "bad linear_split args");
+    // KeyRange.linearSplit (KeyRange.java:68-80)
+    int64_t start = first_key;
+    const int64_t step = (last_key - first_key + n) / n;
+    for (int32_t i = 0; i < n; ++i) {
+        const int64_t end = std::min(start + step - 1, last_key);
+        first_out[i] = start;
+        last_out[i] = end;
+        start += step;
+    }
+    return DML_OK;
+}
+
+int dml_store_create_range(const dml_desc* desc, int64_t first_key, int64_t last_key, int32_t cols, int32_t device,
+                           uint32_t flags, dml_store** out) {
+    if (!desc || !out) return set_err(DML_E_INVALID_ARG, "null argument");
+    *out = nullptr;
+    const dml_desc d = *desc;
+    // DataStore.createStore dispatch (DataStore.java:50-92)
+    if ((d.data_type != 0 && d.data_type != 1) || (d.key_type != 0 && d.key_type != 1) ||
+        (d.value_type != DML_ELEMENT_TYPE_INT && d.value_type != DML_ELEMENT_TYPE_FLOAT &&
+         d.value_type != DML_ELEMENT_TYPE_DOUBLE))
+        return set_err(DML_E_BAD_DESC, "Unrecognized matrix type (DataStore.createStore)");
+    if (d.data_type == 1 && !d.dense_column)
+        return set_err(DML_E_UNSUPPORTED, "sparse-column matrix pushes are not supported (SURVEY defect 3)");
+    if (last_key < first_key) return set_err(DML_E_INVALID_ARG, "empty KeyRange shard");
+    if (d.data_type == 1 && cols <= 0) return set_err(DML_E_INVALID_ARG, "cols must be > 0");
+    const int64_t rows = last_key - first_key + 1;
+    if (rows > INT32_MAX) return set_err(DML_E_INVALID_ARG, "shard larger than a Java array");
+    int ndev = 0;
+    if (hipGetDeviceCount(&ndev) != hipSuccess || ndev <= 0) return set_err(DML_E_HIP, "no HIP device");
+    if (device < 0 || device >= ndev) return set_err(DML_E_INVALID_ARG, "bad device ordinal");
+    DeviceGuard g(device);
+
+    auto* s = new (std::nothrow) dml_store();
+    if (!s) return set_err(DML_E_NOMEM, "out of host memory");
+    s->device = device;
+    s->desc = d;
+    s->flags = flags;
+    s->is_matrix = d.data_type == 1;
+    s->adagrad = s->is_matrix && d.value_type == DML_ELEMENT_TYPE_FLOAT && d.ada_grad;
+    s->K = d.key_type == 0 ? 4 : 8;
+    s->V = (d.value_type == DML_ELEMENT_TYPE_INT || d.value_type == DML_ELEMENT_TYPE_FLOAT) ? 4 : 8;
+    s->array_vs = s->V;
+    if (!s->is_matrix && d.value_type == DML_ELEMENT_TYPE_FLOAT && (flags & DML_FLAG_FLOAT_ARRAY_REF_STRIDE))
+        s->array_vs = 8;  // FloatArrayStore.VALUE_SIZE (FloatArrayStore.java:15)
+    s->first = first_key;
+    s->last = last_key;
+    s->rows = rows;
+    s->cols = s->is_matrix ? cols : 1;
+    s->stride = s->is_matrix ? s->K + (int64_t)s->V * s->cols : s->K + s->array_vs;
+
+    auto fail = [&](hipError_t e, const char* what) {
+        dml_store_destroy(s);
+        return set_err(DML_E_HIP, std::string(what) + ": " + hipGetErrorString(e));
+    };
+    hipError_t e;
+    if ((e = hipStreamCreateWithFlags(&s->stream, hipStreamNonBlocking)) != hipSuccess) return fail(e, "stream");
+    const size_t nbytes = (size_t)rows * (size_t)s->cols * (size_t)s->V;
+    if ((e = hipMalloc(&s->data, nbytes)) != hipSuccess) return fail(e, "shard alloc");
+    if ((e = hipMemsetAsync(s->data, 0, nbytes, s->stream)) != hipSuccess) return fail(e, "shard zero");
+    if (s->adagrad) {
+        const size_t n = (size_t)rows * (size_t)s->cols;
+        if ((e = hipMalloc((void**)&s->alpha, n * 4)) != hipSuccess) return fail(e, "alpha alloc");
+        if ((e = hipMalloc((void**)&s->delta, n * 4)) != hipSuccess) return fail(e, "delta alloc");
+        if ((e = hipMemsetAsync(s->alpha, 0, n * 4, s->stream)) != hipSuccess) return fail(e, "alpha zero");
+        if ((e = hipMemsetAsync(s->delta, 0, n * 4, s->stream)) != hipSuccess) return fail(e, "delta zero");
+        s->cand_n = reduce_blocks(d.value_type, rows, s->cols);
+        if ((e = hipMalloc((void**)&s->cand, sizeof(DeltaCand) * (size_t)std::max<int64_t>(s->cand_n, 1))) != hipSuccess)
+            return fail(e, "cand alloc");
+        if ((e = hipMalloc((void**)&s->md, sizeof(MaxDelta))) != hipSuccess) return fail(e, "md alloc");
+        if ((e = hipMemsetAsync(s->md, 0, sizeof(MaxDelta), s->stream)) != hipSuccess) return fail(e, "md zero");
+    }
+    s->ws_bytes = sizeof(Ctrl) + (s->is_matrix ? (size_t)rows * kMaxW * sizeof(int32_t) : 0);
+    if ((e = hipMalloc((void**)&s->ws, s->ws_bytes)) != hipSuccess) return fail(e, "workspace alloc");
+    s->ctrl = (Ctrl*)s->ws;
+    s->slot = (int32_t*)(s->ws + sizeof(Ctrl));
+    if ((e = hipHostMalloc((void**)&s->hctrl, sizeof(Ctrl), hipHostMallocDefault)) != hipSuccess) return fail(e, "ctrl");
+    if ((e = hipEventCreateWithFlags(&s->h2d_done, hipEventDisableTiming)) != hipSuccess) return fail(e, "event");
+    if ((e = hipStreamSynchronize(s->stream)) != hipSuccess) return fail(e, "init sync");
+    *out = s;
+    return DML_OK;
+}
+
+void dml_store_destroy(dml_store* s) {
+    if (!s) return;
+    {
+        std::lock_guard<std::mutex> lk(s->mu);
+        DeviceGuard g(s->device);
+        if (s->stream) (void)hipStreamSynchronize(s->stream);
+        for (auto& p : s->ev_used) { (void)hipEventDestroy(p.first); (void)hipEventDestroy(p.second); }
+        for (auto& p : s->ev_free) { (void)hipEventDestroy(p.first); (void)hipEventDestroy(p.second); }
+        if (s->h2d_done) (void)hipEventDestroy(s->h2d_done);
+        (void)hipFree(s->data);
+        (void)hipFree(s->alpha);
+        (void)hipFree(s->delta);
+        (void)hipFree(s->cand);
+        (void)hipFree(s->md);
+        (void)hipFree(s->ws);
+        (void)hipFree(s->dstage);
+        if (s->hstage) (void)hipHostFree(s->hstage);
+        if (s->hctrl) (void)hipHostFree(s->hctrl);
+        if (s->stream) (void)hipStreamDestroy(s->stream);
+    }
+    delete s;
+}
+
+static int push_host(dml_store* s, const uint8_t* const* bufs, const int64_t* lens, int32_t n) {
+    if (n < 0 || (n > 0 && (!bufs || !lens))) return set_err(DML_E_INVALID_ARG, "bad push arguments");
+    int rc = begin_call(s);
+    if (rc) return rc;
+    if (s->err) return set_err(s->err, "store is in a failed state (see dml_store_error_state)");
+    size_t total = 0;
+    std::vector<size_t> offs((size_t)n);
+    for (int32_t i = 0; i < n; ++i) {
+        if (lens[i] < 0 || (lens[i] > 0 && !bufs[i])) return set_err(DML_E_INVALID_ARG, "bad push buffer");
+        offs[(size_t)i] = total;
+        total += ((size_t)lens[i] + 255) & ~(size_t)255;
+    }
+    rc = ensure_stage(s, total);
+    if (rc) return rc;
+    // Stage: pageable -> pinned (CPU copy) -> HBM (one async DMA).
+    for (int32_t i = 0; i < n; ++i)
+        if (lens[i] > 0) std::memcpy(s->hstage + offs[(size_t)i], bufs[i], (size_t)lens[i]);
+    if (total > 0) HIPCHK(hipMemcpyAsync(s->dstage, s->hstage, total, hipMemcpyHostToDevice, s->stream));
+    std::vector<const uint8_t*> dptr((size_t)n);
+    for (int32_t i = 0; i < n; ++i) dptr[(size_t)i] = s->dstage + offs[(size_t)i];
+    rc = run_batch(s, dptr.data(), lens, n);
+    if (rc) return rc;
+    if (!(s->flags & DML_FLAG_ASYNC)) return retire(s);
+    // async: the caller's bytes are already copied into pinned staging.
+    return DML_OK;
+}
+
+int dml_store_push(dml_store* s, const uint8_t* data, int64_t len) {
+    if (int rc = check_store(s)) return rc;
+    std::lock_guard<std::mutex> lk(s->mu);
+    DeviceGuard g(s->device);
+    const uint8_t* bufs[1] = {data};
+    return push_host(s, bufs, &len, 1);
+}
+
+int dml_store_push_batch(dml_store* s, const uint8_t* const* bufs, const int64_t* lens, int32_t n) {
+    if (int rc = check_store(s)) return rc;
+    std::lock_guard<std::mutex> lk(s->mu);
+    DeviceGuard g(s->device);
+    return push_host(s, bufs, lens, n);
+}
+
+int dml_store_push_batch_device(dml_store* s, const void* const* dev_bufs, const int64_t* lens, int32_t n) {
+    if (int rc = check_store(s)) return rc;
+    std::lock_guard<std::mutex> lk(s->mu);
+    DeviceGuard g(s->device);
+    if (n < 0 || (n > 0 && (!dev_bufs || !lens))) return set_err(DML_E_INVALID_ARG, "bad push arguments");
+    int rc = begin_call(s);
+    if (rc) return rc;
+    if (s->err) return set_err(s->err, "store is in a failed state (see dml_store_error_state)");
+    for (int32_t i = 0; i < n; ++i)
+        if (lens[i] < 0 || (lens[i] > 0 && !dev_bufs[i])) return set_err(DML_E_INVALID_ARG, "bad push buffer");
+    return run_batch(s, (const uint8_t* const*)dev_bufs, lens, n);
+}
+
+int dml_store_flush(dml_store* s) {
+    if (int rc = check_store(s)) return rc;
+    std::lock_guard<std::mutex> lk(s->mu);
+    DeviceGuard g(s->device);
+    int rc = retire(s);
+    if (rc) return rc;
+    HIPCHK(hipStreamSynchronize(s->stream));
+    return DML_OK;
+}
+
+int dml_store_error_state(dml_store* s, int64_t* bad_key, int32_t* bad_col) {
+    if (int rc = check_store(s)) return rc;
+    std::lock_guard<std::mutex> lk(s->mu);
+    if (bad_key) *bad_key = s->err_key;
+    if (bad_col) *bad_col = s->err_col;
+    return s->err;
+}
+
+void dml_store_clear_error(dml_store* s) {
+    if (!s) return;
+    std::lock_guard<std::mutex> lk(s->mu);
+    s->err = 0;
+    s->err_key = 0;
+    s->err_col = -1;
+}
+
+int dml_store_shape(dml_store* s, int64_t* rows, int32_t* cols) {
+    if (int rc = check_store(s)) return rc;
+    if (rows) *rows = s->rows;
+    if (cols) *cols = s->cols;
+    return DML_OK;
+}
+
+int dml_store_read_dense(dml_store* s, void* host_dst, int64_t bytes) {
+    if (int rc = check_store(s)) return rc;
+    std::lock_guard<std::mutex> lk(s->mu);
+    DeviceGuard g(s->device);
+    const int64_t need = s->rows * s->cols * s->V;
+    if (!host_dst || bytes < need) return set_err(DML_E_CAPACITY, "destination too small");
+    if (int rc = begin_call(s)) return rc;
+    HIPCHK(hipMemcpyAsync(host_dst, s->data, (size_t)need, hipMemcpyDeviceToHost, s->stream));
+    HIPCHK(hipStreamSynchronize(s->stream));
+    return DML_OK;
+}
+
+int dml_store_write_dense(dml_store* s, const void* host_src, int64_t bytes) {
+    if (int rc = check_store(s)) return rc;
+    std::lock_guard<std::mutex> lk(s->mu);
+    DeviceGuard g(s->device);
+    const int64_t need = s->rows * s->cols * s->V;
+    if (!host_src || bytes != need) return set_err(DML_E_CAPACITY, "source size does not match the shard");
+    if (int rc = begin_call(s)) return rc;
+    HIPCHK(hipMemcpyAsync(s->data, host_src, (size_t)need, hipMemcpyHostToDevice, s->stream));
+    HIPCHK(hipStreamSynchronize(s->stream));
+    return DML_OK;
+}
+
+int dml_store_device_ptr(dml_store* s, void** dev_ptr) {
+    if (int rc = check_store(s)) return rc;
+    if (!dev_ptr) return set_err(DML_E_INVALID_ARG, "null out");
+    *dev_ptr = s->data;
+    return DML_OK;
+}
+
+int dml_store_read_adagrad(dml_store* s, float* alpha_dst, float* delta_dst, int64_t elems) {
+    if (int rc = check_store(s)) return rc;
+    std::lock_guard<std::mutex> lk(s->mu);
+    DeviceGuard g(s->device);
+    if (!s->adagrad) return set_err(DML_E_UNSUPPORTED, "not an AdaGrad store");
+    if (elems < s->rows * s->cols) return set_err(DML_E_CAPACITY, "destination too small");
+    if (int rc = begin_call(s)) return rc;
+    const size_t n = (size_t)(s->rows * s->cols) * 4;
+    if (alpha_dst) HIPCHK(hipMemcpyAsync(alpha_dst, s->alpha, n, hipMemcpyDeviceToHost, s->stream));
+    if (delta_dst) HIPCHK(hipMemcpyAsync(delta_dst, s->delta, n, hipMemcpyDeviceToHost, s->stream));
+    HIPCHK(hipStreamSynchronize(s->stream));
+    return DML_OK;
+}
+
+int dml_store_fill(dml_store* s, double v) {
+    if (int rc = check_store(s)) return rc;
+    std::lock_guard<std::mutex> lk(s->mu);
+    DeviceGuard g(s->device);
+    if (int rc = begin_call(s)) return rc;
+    HIPCHK(launch_fill(vtype_of(s->desc), s->data, s->rows * s->cols, v, s->stream));
+    HIPCHK(hipStreamSynchronize(s->stream));
+    return DML_OK;
+}
+
+int dml_store_set_alpha(dml_store* s, float initial_alpha, float min_alpha, float factor) {
+    if (int rc = check_store(s)) return rc;
+    std::lock_guard<std::mutex> lk(s->mu);
+    DeviceGuard g(s->device);
+    if (!s->adagrad) return set_err(DML_E_UNSUPPORTED, "not an AdaGrad store");
+    if (int rc = begin_call(s)) return rc;
+    // setAlpha: setAlphaValue(initialAlpha) then the three fields (FloatMatrixStoreAdaGrad.java:77-82)
+    HIPCHK(launch_fill_f32(s->alpha, s->rows * s->cols, initial_alpha, s->stream));
+    HIPCHK(hipStreamSynchronize(s->stream));
+    s->initial_alpha = initial_alpha;
+    s->min_alpha = min_alpha;
+    s->factor = factor;
+    return DML_OK;
+}
+
+int dml_store_max_delta(dml_store* s, float* max_delta, int32_t* row, int32_t* col) {
+    if (int rc = check_store(s)) return rc;
+    std::lock_guard<std::mutex> lk(s->mu);
+    DeviceGuard g(s->device);
+    if (!s->adagrad) return set_err(DML_E_UNSUPPORTED, "not an AdaGrad store");
+    if (int rc = begin_call(s)) return rc;
+    MaxDelta m;
+    HIPCHK(hipMemcpyAsync(&m, s->md, sizeof m, hipMemcpyDeviceToHost, s->stream));
+    HIPCHK(hipStreamSynchronize(s->stream));
+    if (max_delta) *max_delta = m.value;
+    if (row) *row = m.row;
+    if (col) *col = m.col;
+    return DML_OK;
+}
+
+static int fetch_impl(dml_store* s, const int64_t* keys, int64_t nkeys, uint8_t* out, int64_t cap, int64_t* out_len) {
+    if (nkeys < 0 || (nkeys > 0 && !keys) || !out_len) return set_err(DML_E_INVALID_ARG, "bad fetch arguments");
+    // record layout of handleFetch (dense column)
+    int64_t rec;
+    int value_slot;
+    if (s->is_matrix) {
+        value_slot = s->adagrad ? 8 : s->V;
+        rec = s->K + (int64_t)s->cols * value_slot;
+    } else {
+        value_slot = (s->desc.value_type == DML_ELEMENT_TYPE_FLOAT) ? 8 : s->V;  // FloatArrayStore VALUE_SIZE 8
+        rec = s->K + value_slot;
+    }
+    *out_len = nkeys * rec;
+    if (!out || cap < *out_len) return set_err(DML_E_CAPACITY, "fetch output buffer too small");
+    for (int64_t j = 0; j < nkeys; ++j) {
+        const int32_t idx = (int32_t)(uint32_t)((uint64_t)keys[j] - (uint64_t)s->first);
+        if (idx < 0 || idx >= s->rows) return record_error(s, DML_E_KEY_OUT_OF_SHARD, keys[j], -1);
+    }
+    if (nkeys == 0) return DML_OK;
+    int64_t* dkeys = nullptr;
+    uint8_t* dout = nullptr;
+    HIPCHK(hipMallocAsync((void**)&dkeys, (size_t)nkeys * 8, s->stream));
+    HIPCHK(hipMallocAsync((void**)&dout, (size_t)*out_len, s->stream));
+    HIPCHK(hipMemcpyAsync(dkeys, keys, (size_t)nkeys * 8, hipMemcpyHostToDevice, s->stream));
+    HIPCHK(hipMemsetAsync(dout, 0, (size_t)*out_len, s->stream));
+    HIPCHK(launch_fetch(vtype_of(s->desc), s->data, s->adagrad ? s->alpha : nullptr, s->cols, dkeys, nkeys, s->first,
+                        dout, rec, s->K, value_slot, s->stream));
+    HIPCHK(hipMemcpyAsync(out, dout, (size_t)*out_len, hipMemcpyDeviceToHost, s->stream));
+    HIPCHK(hipFreeAsync(dkeys, s->stream));
+    HIPCHK(hipFreeAsync(dout, s->stream));
+    HIPCHK(hipStreamSynchronize(s->stream));
+    return DML_OK;
+}
+
+int dml_store_fetch(dml_store* s, const int64_t* keys, int64_t nkeys, uint8_t* out, int64_t cap, int64_t* out_len) {
+    if (int rc = check_store(s)) return rc;
+    std::lock_guard<std::mutex> lk(s->mu);
+    DeviceGuard g(s->device);
+    if (int rc = begin_call(s)) return rc;
+    return fetch_impl(s, keys, nkeys, out, cap, out_len);
+}
+
+int dml_store_fetch_range(dml_store* s, int64_t first_key, int64_t last_key, uint8_t* out, int64_t cap,
+                          int64_t* out_len) {
+    if (int rc = check_store(s)) return rc;
+    std::lock_guard<std::mutex> lk(s->mu);
+    DeviceGuard g(s->device);
+    if (int rc = begin_call(s)) return rc;
+    // KeyRange.intersect (KeyRange.java:124-136): clip to the shard, ascending
+    const int64_t lo = std::max(first_key, s->first), hi = std::min(last_key, s->last);
+    std::vector<int64_t> keys;
+    if (lo <= hi) {
+        keys.resize((size_t)(hi - lo + 1));
+        for (int64_t k = lo; k <= hi; ++k) keys[(size_t)(k - lo)] = k;
+    }
+    if (!out_len) return set_err(DML_E_INVALID_ARG, "null out_len");
+    return fetch_impl(s, keys.data(), (int64_t)keys.size(), out, cap, out_len);
+}
+
+int dml_store_write_all(dml_store* s, uint8_t* out_be, int64_t cap, int64_t* out_len) {
+    if (int rc = check_store(s)) return rc;
+    std::lock_guard<std::mutex> lk(s->mu);
+    DeviceGuard g(s->device);
+    if (int rc = begin_call(s)) return rc;
+    const int64_t n = s->rows * s->cols, bytes = n * s->V;
+    if (out_len) *out_len = bytes;
+    if (!out_be || cap < bytes) return set_err(DML_E_CAPACITY, "writeAll buffer too small");
+    void* tmp = nullptr;
+    HIPCHK(hipMallocAsync(&tmp, (size_t)std::max<int64_t>(bytes, 1), s->stream));
+    HIPCHK(launch_bswap(s->V, s->data, tmp, n, s->stream));
+    HIPCHK(hipMemcpyAsync(out_be, tmp, (size_t)bytes, hipMemcpyDeviceToHost, s->stream));
+    HIPCHK(hipFreeAsync(tmp, s->stream));
+    HIPCHK(hipStreamSynchronize(s->stream));
+    return DML_OK;
+}
+
+int dml_store_read_all(dml_store* s, const uint8_t* in_be, int64_t len) {
+    if (int rc = check_store(s)) return rc;
+    std::lock_guard<std::mutex> lk(s->mu);
+    DeviceGuard g(s->device);
+    if (int rc = begin_call(s)) return rc;
+    const int64_t n = s->rows * s->cols, bytes = n * s->V;
+    // DataInputStream.readFloat past the end throws EOFException (an IOException)
+    if (!in_be || len < bytes) return set_err(DML_E_TRUNCATED, "readAll: stream shorter than the shard");
+    void* tmp = nullptr;
+    HIPCHK(hipMallocAsync(&tmp, (size_t)std::max<int64_t>(bytes, 1), s->stream));
+    HIPCHK(hipMemcpyAsync(tmp, in_be, (size_t)bytes, hipMemcpyHostToDevice, s->stream));
+    HIPCHK(launch_bswap(s->V, tmp, s->data, n, s->stream));
+    HIPCHK(hipFreeAsync(tmp, s->stream));
+    HIPCHK(hipStreamSynchronize(s->stream));
+    return DML_OK;
+}
+
+int dml_store_stream(dml_store* s, void** stream) {
+    if (int rc = check_store(s)) return rc;
+    if (!stream) return set_err(DML_E_INVALID_ARG, "null out");
+    *stream = (void*)s->stream;
+    return DML_OK;
+}
+
+int dml_store_set_timing(dml_store* s, int32_t enable) {
+    if (int rc = check_store(s)) return rc;
+    std::lock_guard<std::mutex> lk(s->mu);
+    s->timing = enable != 0;
+    return DML_OK;
+}
+
+int dml_store_kernel_time(dml_store* s, double* total_ms, int64_t* launches, int32_t reset) {
+    if (int rc = check_store(s)) return rc;
+    std::lock_guard<std::mutex> lk(s->mu);
+    DeviceGuard g(s->device);
+    HIPCHK(hipStreamSynchronize(s->stream));
+    ev_collect(s);
+    if (total_ms) *total_ms = s->timed_ms;
+    if (launches) *launches = s->timed_n;
+    if (reset) {
+        s->timed_ms = 0.0;
+        s->timed_n = 0;
+    }
+    return DML_OK;
+}
+
+int dml_store_apply_dense_device(dml_store* s, const void* dev_src, int64_t elems) {
+    if (int rc = check_store(s)) return rc;
+    std::lock_guard<std::mutex> lk(s->mu);
+    DeviceGuard g(s->device);
+    if (int rc = begin_call(s)) return rc;
+    if (!dev_src || elems != s->rows * s->cols) return set_err(DML_E_INVALID_ARG, "apply size mismatch");
+    std::pair<hipEvent_t, hipEvent_t> ev{};
+    if (s->timing) {
+        ev = ev_pair(s);
+        HIPCHK(hipEventRecord(ev.first, s->stream));
+    }
+    HIPCHK(launch_apply_dense(vtype_of(s->desc), s->data, dev_src, elems, s->stream));
+    if (s->timing) {
+        HIPCHK(hipEventRecord(ev.second, s->stream));
+        s->ev_used.push_back(ev);
+    }
+    return DML_OK;
+}
+
+// Stand-alone ordered pre-reduce (multi-GPU): per-device scratch for Ctrl+slots.
+int dml_reduce_buckets_dense(const dml_desc* desc, int64_t first_key, int64_t rows, int32_t cols,
+                             const void* const* dev_bufs, const int64_t* lens, int32_t n, void* dev_out, void* stream) {
+    if (!desc || !dev_out || rows <= 0 || cols <= 0 || n < 0 || (n > 0 && (!dev_bufs || !lens)))
+        return set_err(DML_E_INVALID_ARG, "bad reduce arguments");
+    if (desc->data_type != 1 || !desc->dense_column || desc->ada_grad)
+        return set_err(DML_E_UNSUPPORTED, "pre-reduce supports dense-column plain matrices");
+    const int vt = desc->value_type;
+    if (vt != 0 && vt != 1 && vt != 3) return set_err(DML_E_BAD_DESC, "bad value type");
+    const int K = desc->key_type == 0 ? 4 : 8, V = vt == 3 ? 8 : 4;
+    const int64_t stride = K + (int64_t)V * cols;
+    hipStream_t st = (hipStream_t)stream;
+    uint8_t* ws = nullptr;
+    const size_t wsb = sizeof(Ctrl) + (size_t)rows * kMaxW * sizeof(int32_t);
+    HIPCHK(hipMallocAsync((void**)&ws, wsb, st));
+    Ctrl* ctrl = (Ctrl*)ws;
+    int32_t* slot = (int32_t*)(ws + sizeof(Ctrl));
+    AdaArgs none{};
+    int rc = DML_OK;
+    for (int c0 = 0; c0 < std::max(n, 1) && rc == DML_OK; c0 += kMaxW) {
+        Batch bt{};
+        const int nb = std::max(0, std::min(kMaxW, n - c0));
+        int64_t max_nrec = 0;
+        for (int j = 0; j < nb; ++j) {
+            bt.base[j] = (const uint8_t*)dev_bufs[c0 + j];
+            bt.len[j] = lens[c0 + j];
+            bt.nrec[j] = lens[c0 + j] / stride;
+            bt.bidx[j] = c0 + j;
+            if (lens[c0 + j] % stride) rc = set_err(DML_E_TRUNCATED, "ragged full-range bucket");
+            max_nrec = std::max(max_nrec, bt.nrec[j]);
+        }
+        if (rc) break;
+        hipError_t e = hipMemsetAsync(ws, 0xFF, wsb, st);
+        if (e == hipSuccess) e = launch_index(bt, nb, max_nrec, stride, K, first_key, rows, slot, ctrl, st);
+        if (e == hipSuccess)
+            e = launch_reduce(vt, c0 == 0 ? kPreReduce : kAdd, dev_out, rows, cols, bt, nb, stride, K, slot, ctrl,
+                              kNoPos, none, st, nullptr);
+        Ctrl h;
+        if (e == hipSuccess) e = hipMemcpyAsync(&h, ctrl, sizeof h, hipMemcpyDeviceToHost, st);
+        if (e == hipSuccess) e = hipStreamSynchronize(st);
+        if (e != hipSuccess) rc = set_err(DML_E_HIP, hipGetErrorString(e));
+        else if (h.cutoff != kNoPos) rc = set_err(DML_E_KEY_OUT_OF_SHARD, "pre-reduce: key outside the matrix");
+        else if (h.no_dup == 0u) rc = set_err(DML_E_UNSUPPORTED, "pre-reduce: a bucket repeats a row");
+        if (n == 0) break;
+    }
+    (void)hipFreeAsync(ws, st);
+    return rc;
+}
+
+// ---- synthetic data --------------------------------------------------------
+int dml_synth_dense_bucket(void* dev_out, const dml_desc* desc, int64_t first_key, int64_t shard_rows, int64_t nrec,
+                           int32_t cols, uint64_t seed, uint64_t perm_a, uint64_t perm_c, void* stream) {
+    if (!dev_out || !desc || shard_rows <= 0 || nrec < 0 || cols <= 0) return set_err(DML_E_INVALID_ARG, "bad synth args");
+    if (perm_a >= (1ull << 32) || (uint64_t)nrec >= (1ull << 32)) return set_err(DML_E_INVALID_ARG, "perm_a/nrec must be < 2^32");
+    const int K = desc->key_type == 0 ? 4 : 8;
+    HIPCHK(launch_synth_dense((uint8_t*)dev_out, K, desc->value_type, first_key, shard_rows, nrec, cols,
+                              splitmix64(seed), perm_a % (uint64_t)shard_rows, perm_c % (uint64_t)shard_rows,
+                              (hipStream_t)stream));
+    return DML_OK;
+}
+
+int dml_synth_sparse_bucket(void* dev_out, const dml_desc* desc, int64_t first_key, int64_t key_space, int64_t nrec,
+                            uint64_t seed, uint64_t perm_a, uint64_t perm_c, void* stream) {
+    if (!dev_out || !desc || key_space <= 0 || nrec < 0) return set_err(DML_E_INVALID_ARG, "bad synth args");
+    if (perm_a >= (1ull << 32) || (uint64_t)nrec >= (1ull << 32)) return set_err(DML_E_INVALID_ARG, "perm_a/nrec must be < 2^32");
+    const int K = desc->key_type == 0 ? 4 : 8;
+    const int V = desc->value_type == DML_ELEMENT_TYPE_DOUBLE ? 8 : 4;
+    HIPCHK(launch_synth_sparse((uint8_t*)dev_out, K, desc->value_type, V, first_key, key_space, nrec, splitmix64(seed),
+                               perm_a % (uint64_t)key_space, perm_c % (uint64_t)key_space, (hipStream_t)stream));
+    return DML_OK;
+}
+
+int dml_synth_fill_store(dml_store* s, uint64_t seed) {
+    if (int rc = check_store(s)) return rc;
+    std::lock_guard<std::mutex> lk(s->mu);
+    DeviceGuard g(s->device);
+    if (int rc = begin_call(s)) return rc;
+    HIPCHK(launch_synth_fill(vtype_of(s->desc), s->data, s->rows * s->cols, splitmix64(seed), s->stream));
+    HIPCHK(hipStreamSynchronize(s->stream));
+    return DML_OK;
+}
+
+}  // extern "C"

@@ -1,0 +1,204 @@
+/*
+ * distml_ps.h — C-ABI of the MI355X parameter-server push-reduce path.
+ *
+ * Drop-in boundary: this library replaces the body of DistML's server-side
+ * plugin `abstract class DataStore` (reference: src/main/java/com/intel/distml/
+ * util/DataStore.java:17-92) and its seven typed implementations under
+ * util/store/. Every entry point names the reference method it replaces.
+ * Plain C types only: a JNI shim, ctypes, or C++ can bind it.
+ *
+ * Threading: every call on one store is serialized by a mutex inside the store
+ * (the reference calls a store from the PSAgent selector thread, Akka dispatcher
+ * threads and the PSSync thread, PSAgent.java:278, PSActor.java:171-251,
+ * PSSync.java:131). Each store owns one HIP stream on its device; every call
+ * does hipSetDevice, so any host thread may call.
+ *
+ * Status codes map 1:1 to the exceptions the reference throws:
+ *   DML_E_BAD_DESC          IllegalArgumentException  (DataStore.java:91)
+ *   DML_E_KEY_OUT_OF_SHARD  ArrayIndexOutOfBoundsException (localData[indexOf(key)])
+ *   DML_E_TRUNCATED         ArrayIndexOutOfBoundsException (readInt/readFloat past data.length)
+ *   DML_E_NEGATIVE_COUNTER  IllegalStateException (IntMatrixStore.java:174-176, IntArrayStore.java:108-110)
+ * After one of these four the store holds exactly the values the reference
+ * store holds when its exception escapes handlePush (every add before the
+ * failing position applied, nothing after it), and the error is recorded in
+ * dml_store_error_state(). DML_E_* codes >= 16 are library/usage errors with
+ * no reference counterpart.
+ */
+#ifndef DISTML_PS_H
+#define DISTML_PS_H
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+/* DataDesc constants (DataDesc.java:10-19). */
+#define DML_DATA_TYPE_ARRAY   0
+#define DML_DATA_TYPE_MATRIX  1
+#define DML_KEY_TYPE_INT      0
+#define DML_KEY_TYPE_LONG     1
+#define DML_ELEMENT_TYPE_INT    0
+#define DML_ELEMENT_TYPE_FLOAT  1
+#define DML_ELEMENT_TYPE_LONG   2
+#define DML_ELEMENT_TYPE_DOUBLE 3
+
+/* Status codes. */
+#define DML_OK                   0
+#define DML_E_BAD_DESC           1
+#define DML_E_KEY_OUT_OF_SHARD   2
+#define DML_E_TRUNCATED          3
+#define DML_E_NEGATIVE_COUNTER   4
+#define DML_E_INVALID_ARG       16
+#define DML_E_HIP               17
+#define DML_E_NOMEM             18
+#define DML_E_UNSUPPORTED       19
+#define DML_E_CAPACITY          20
+
+/* Store option flags (dml_store_create_range `flags`). */
+/* FloatArrayStore reads records with VALUE_SIZE = 8 (FloatArrayStore.java:15)
+ * although every writer emits key|f32 records (SparseArray.java:63-76). The
+ * default follows the writer (stride keySize+4); this flag reproduces the
+ * reference's stride keySize+8 read bit for bit (SURVEY.md defect 1). */
+#define DML_FLAG_FLOAT_ARRAY_REF_STRIDE  0x1
+/* Apply pushes asynchronously: dml_store_push returns once the bytes are
+ * captured (staged); a deferred error surfaces at the next call. Default is
+ * synchronous: the call returns after the apply, like the reference's ack
+ * (PSAgent.java:278-281). */
+#define DML_FLAG_ASYNC                   0x2
+
+/* Mirrors the six big-endian int32s DataDesc puts on the wire, in wire order
+ * (DataDesc.java:62-69). key/value sizes derive as in DataDesc.java:50-51. */
+typedef struct dml_desc {
+    int32_t data_type;
+    int32_t key_type;
+    int32_t value_type;
+    int32_t dense_row;
+    int32_t dense_column;
+    int32_t ada_grad;
+} dml_desc;
+
+typedef struct dml_store dml_store; /* opaque; one per (matrix, shard) */
+
+/* --- lifecycle --------------------------------------------------------- */
+
+/* == DataStore.createStore(serverIndex, matrix) (DataStore.java:50-92) for a
+ * KeyRange shard [first_key, last_key] (KeyRange.linearSplit, KeyRange.java:68-80),
+ * followed by the store's init(keys[, cols]) (e.g. FloatMatrixStore.java:28-37):
+ * the shard is zero-filled in HBM. `cols` is ignored for ARRAY stores. */
+int dml_store_create_range(const dml_desc* desc, int64_t first_key, int64_t last_key,
+                           int32_t cols, int32_t device, uint32_t flags, dml_store** out);
+void dml_store_destroy(dml_store* s);
+
+/* KeyRange.linearSplit(n) (KeyRange.java:68-80): shard i = [first_out[i], last_out[i]]. */
+int dml_linear_split(int64_t first_key, int64_t last_key, int32_t n,
+                     int64_t* first_out, int64_t* last_out);
+
+/* --- the hot path: handlePush ------------------------------------------ */
+
+/* == store.handlePush(format, data) (DataStore.java:30; FloatMatrixStore.java:200-238,
+ * FloatArrayStore.java:380-392, IntMatrixStore.java:154-195, IntArrayStore.java:294-310,
+ * FloatMatrixStoreAdaGrad.java:239-306, DoubleArrayStore.java:115-127,
+ * DoubleMatrixStore.java:153-190). `data` is a host buffer BORROWED for the
+ * call only (the JVM byte[]). Records use the store's own DataDesc
+ * (PSAgent.java:279 passes the server-side format). */
+int dml_store_push(dml_store* s, const uint8_t* data, int64_t len);
+
+/* n sequential handlePush calls, bucket 0 first, applied as ONE ordered
+ * multi-bucket reduce: each element is summed in push order, so the result is
+ * bit-identical to calling handlePush n times. Host buffers, borrowed. */
+int dml_store_push_batch(dml_store* s, const uint8_t* const* bufs, const int64_t* lens, int32_t n);
+
+/* Same, for buckets already resident in device memory on the store's device
+ * (the device-resident north-star path). Buffers must stay valid until the
+ * next dml_store_flush (or any read call). */
+int dml_store_push_batch_device(dml_store* s, const void* const* dev_bufs, const int64_t* lens, int32_t n);
+
+/* Read barrier: every accepted push is applied; returns any deferred error. */
+int dml_store_flush(dml_store* s);
+
+/* First error the store has seen (sticky until dml_store_clear_error):
+ * status code, the key and column the reference would report, 0 if none. */
+int dml_store_error_state(dml_store* s, int64_t* bad_key, int32_t* bad_col);
+void dml_store_clear_error(dml_store* s);
+
+/* --- shard access ------------------------------------------------------ */
+
+/* KeyRange size (KeyRange.java:92-94) and rowSize() (FloatMatrixStore.java:24-26;
+ * 1 for arrays). */
+int dml_store_shape(dml_store* s, int64_t* rows, int32_t* cols);
+
+/* Raw row-major shard values (rows*cols elements of the store's value type)
+ * to/from host memory; test/oracle access and initial load. */
+int dml_store_read_dense(dml_store* s, void* host_dst, int64_t bytes);
+int dml_store_write_dense(dml_store* s, const void* host_src, int64_t bytes);
+/* Device pointer of the value array (rows*cols elements), valid until destroy. */
+int dml_store_device_ptr(dml_store* s, void** dev_ptr);
+/* AdaGrad side arrays (FloatMatrixStoreAdaGrad.java:23-24), f32 row-major. */
+int dml_store_read_adagrad(dml_store* s, float* alpha_dst, float* delta_dst, int64_t elems);
+
+/* set(String)/zero()/setValue (FloatMatrixStore.java:53-71): fill every value. */
+int dml_store_fill(dml_store* s, double v);
+/* FloatMatrixStoreAdaGrad.setAlpha(initialAlpha, minAlpha, factor) (:77-82). */
+int dml_store_set_alpha(dml_store* s, float initial_alpha, float min_alpha, float factor);
+/* maxDelta / maxDeltaRow / maxDeltaCol printed by AdaGrad handlePush (:246, :273-277). */
+int dml_store_max_delta(dml_store* s, float* max_delta, int32_t* row, int32_t* col);
+
+/* == handleFetch(format, rows), dense-column layout (FloatMatrixStore.java:113-174,
+ * IntMatrixStore.java:81-140, FloatArrayStore.java:358-378, IntArrayStore.java:274-292,
+ * DoubleArrayStore.java handleFetch, FloatMatrixStoreAdaGrad.java:146-213).
+ * `keys` are the intersected keys in the caller's iteration order; every key
+ * must lie in the shard. Writes the reference byte layout to `out`. */
+int dml_store_fetch(dml_store* s, const int64_t* keys, int64_t nkeys,
+                    uint8_t* out, int64_t cap, int64_t* out_len);
+/* Same for a KeyRange request: keys first..last ascending (KeyRange.intersect). */
+int dml_store_fetch_range(dml_store* s, int64_t first_key, int64_t last_key,
+                          uint8_t* out, int64_t cap, int64_t* out_len);
+
+/* writeAll/readAll (FloatMatrixStore.java:74-91 etc.): big-endian row-major
+ * values, the bytes DataOutputStream.writeFloat/writeInt/writeDouble emit. */
+int dml_store_write_all(dml_store* s, uint8_t* out_be, int64_t cap, int64_t* out_len);
+int dml_store_read_all(dml_store* s, const uint8_t* in_be, int64_t len);
+
+/* --- stream / timing / device reduce building blocks ------------------- */
+
+/* hipStream_t of the store, as void*. */
+int dml_store_stream(dml_store* s, void** stream);
+/* When enabled, the store brackets every launch of its dominant reduce kernel
+ * with HIP events on its stream; dml_store_kernel_time returns the summed
+ * elapsed ms and the number of timed launches since the last reset. */
+int dml_store_set_timing(dml_store* s, int32_t enable);
+int dml_store_kernel_time(dml_store* s, double* total_ms, int64_t* launches, int32_t reset);
+
+/* Elementwise shard += src for a dense device buffer of rows*cols values in the
+ * store's layout (owner-side apply after a reduce-scatter). */
+int dml_store_apply_dense_device(dml_store* s, const void* dev_src, int64_t elems);
+
+/* Ordered reduce of n device-resident full-range buckets into a dense device
+ * buffer `dev_out` (rows*cols values of `value_type`, row = key - first_key):
+ * out = b0 + b1 + ... in push order (rows no bucket touches are zero).
+ * The multi-GPU pre-reduce before the reduce-scatter. Runs on `stream`. */
+int dml_reduce_buckets_dense(const dml_desc* desc, int64_t first_key, int64_t rows, int32_t cols,
+                             const void* const* dev_bufs, const int64_t* lens, int32_t n,
+                             void* dev_out, void* stream);
+
+/* --- synthetic workload generators (bench/test support) ----------------- *
+ * Counter-based (SplitMix64) so the CPU oracle regenerates the same bytes.
+ * Spec in DESIGN.md §Synthetic data. Run on `stream` (void* hipStream_t). */
+int dml_synth_dense_bucket(void* dev_out, const dml_desc* desc, int64_t first_key,
+                           int64_t shard_rows, int64_t nrec, int32_t cols, uint64_t seed,
+                           uint64_t perm_a, uint64_t perm_c, void* stream);
+int dml_synth_sparse_bucket(void* dev_out, const dml_desc* desc, int64_t first_key,
+                            int64_t key_space, int64_t nrec, uint64_t seed,
+                            uint64_t perm_a, uint64_t perm_c, void* stream);
+int dml_synth_fill_store(dml_store* s, uint64_t seed);
+
+/* --- misc --------------------------------------------------------------- */
+const char* dml_last_error(void);   /* thread-local message for the last failure */
+const char* dml_version(void);
+
+#ifdef __cplusplus
+}
+#endif
+
+#endif /* DISTML_PS_H */

@@ -1,0 +1,387 @@
+"""GPU parity: libdistml_ps (HIP, gfx950) against the CPU oracle, bit for bit.
+
+Every comparison is exact (bytes equal): fp32/fp64 adds happen in push order
+with one IEEE rounding each, int32 wraps; tolerance 0. Runs through the C-ABI
+(via the distml_amd mirror) on cuda:0.
+"""
+import ctypes as C
+import io
+
+import numpy as np
+import pytest
+
+import kat
+
+pytestmark = pytest.mark.gpu
+
+torch = pytest.importorskip("torch")
+
+
+@pytest.fixture(scope="module", autouse=True)
+def _gpu():
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    torch.cuda.init()
+
+
+def mk_store(case_or_desc, first=None, last=None, cols=1, ref_stride=False, async_push=False):
+    from distml_amd import DataDesc, DataStore, KeyRange
+    if isinstance(case_or_desc, dict):
+        c = case_or_desc
+        d = c["desc"]
+        fmt = DataDesc(d["data_type"], d["key_type"], d["value_type"], False, bool(d["dense_column"]),
+                       bool(d["ada_grad"]))
+        return DataStore(fmt, KeyRange(c["first"], c["last"]), c["cols"],
+                         float_array_ref_stride=bool(c["float_array_ref_stride"]), async_push=async_push), fmt
+    fmt = case_or_desc
+    return DataStore(fmt, KeyRange(first, last), cols, float_array_ref_stride=ref_stride,
+                     async_push=async_push), fmt
+
+
+def oracle_store(oracle, fmt, first, last, cols=1, ref_stride=False):
+    return oracle.OracleStore(fmt.dataType, fmt.keyType, fmt.valueType, first, last, cols,
+                              int(fmt.denseColumn), int(fmt.adaGrad), int(ref_stride))
+
+
+# --------------------------------------------------------------------------- KATs
+@pytest.mark.parametrize("mode", ["sequential", "batch"])
+@pytest.mark.parametrize("case", kat.cases(), ids=lambda c: c["name"])
+def test_kat_on_gpu(case, mode):
+    from distml_amd import DistMLException
+    s, fmt = mk_store(case)
+    s.load_values(kat.init_array(case))
+    if case["ada"]:
+        s.setAlpha(*case["ada"])
+    exp = case["expected"]
+    err = None
+    try:
+        if mode == "sequential":
+            for p in kat.pushes(case):
+                s.handlePush(fmt, p)
+        else:
+            s.handlePushBatch(fmt, kat.pushes(case))
+    except DistMLException as e:
+        err = e
+    if exp["status"]:
+        assert err is not None and (err.code, err.key, err.col) == (exp["status"], exp["key"], exp["col"])
+    else:
+        assert err is None
+    assert kat.bits_equal(s.values(), kat.expected_array(case))
+    if case["ada"]:
+        a, d = s.adagrad_state()
+        assert kat.bits_equal(a, kat.expected_array(case, "alpha_hex", "<f4"))
+        assert kat.bits_equal(d, kat.expected_array(case, "delta_hex", "<f4"))
+        v, r, c = s.maxDelta()
+        assert [v, r, c] == exp["max_delta"]
+    s.close()
+
+
+# ----------------------------------------------------------------- random parity
+def rand_matrix_pushes(rng, first, rows, cols, key_type, value_type, n, row_frac=1.0, dup=False):
+    from distml_amd import encode_matrix_push
+    out = []
+    for b in range(n):
+        k = max(1, int(rows * row_frac))
+        r = rng.choice(rows, size=k, replace=False)
+        if dup:
+            r = np.concatenate([r, rng.choice(r, size=max(1, k // 3))])
+            rng.shuffle(r)
+        if value_type == 0:
+            v = rng.integers(-2, 3, size=(len(r), cols)).astype(np.int32)
+        elif value_type == 1:
+            v = (rng.standard_normal((len(r), cols)) * 1e-3).astype(np.float32)
+        else:
+            v = rng.standard_normal((len(r), cols)) * 1e-3
+        out.append(encode_matrix_push(first + r, v, key_type, value_type))
+    return out
+
+
+@pytest.mark.parametrize("value_type,key_type,cols,nb,frac,dup", [
+    (1, 0, 1024, 3, 1.0, False), (1, 0, 200, 9, 0.5, False), (1, 1, 37, 70, 0.3, False),
+    (1, 0, 5, 4, 1.0, True), (3, 0, 10, 6, 0.7, False), (3, 1, 33, 3, 1.0, True),
+    (0, 0, 1000, 5, 0.2, False), (0, 0, 7, 66, 0.5, False), (0, 1, 16, 3, 1.0, True),
+])
+@pytest.mark.parametrize("api", ["batch", "device"])
+def test_matrix_random_parity(oracle, value_type, key_type, cols, nb, frac, dup, api):
+    from distml_amd import DataDesc
+    rng = np.random.default_rng(cols * 1000 + nb)
+    first, rows = 1000, 300
+    fmt = DataDesc(1, key_type, value_type)
+    s, _ = mk_store(fmt, first, first + rows - 1, cols)
+    o = oracle_store(oracle, fmt, first, first + rows - 1, cols)
+    if value_type == 0:
+        init = rng.integers(100, 200, size=(rows, cols)).astype(np.int32)
+    else:
+        init = rng.standard_normal((rows, cols)).astype(s.dtype)
+    s.load_values(init)
+    o.data[:] = init
+    pushes = rand_matrix_pushes(rng, first, rows, cols, key_type, value_type, nb, frac, dup)
+    for p in pushes:
+        assert o.push(p) == 0
+    if api == "batch":
+        s.handlePushBatch(fmt, pushes)
+    else:
+        bufs = [torch.frombuffer(bytearray(p), dtype=torch.uint8).cuda() for p in pushes]
+        torch.cuda.synchronize()
+        s.pushDevice([b.data_ptr() for b in bufs], [b.numel() for b in bufs])
+        s.flush()
+    assert kat.bits_equal(s.values(), o.data)
+    s.close()
+
+
+@pytest.mark.parametrize("value_type,key_type,ref_stride", [(1, 1, False), (1, 1, True), (1, 0, False),
+                                                             (0, 0, False), (3, 0, False), (3, 1, False)])
+def test_array_random_parity(oracle, value_type, key_type, ref_stride):
+    from distml_amd import DataDesc, encode_array_push
+    rng = np.random.default_rng(value_type * 10 + key_type)
+    first, rows = 5, 100_000
+    fmt = DataDesc(0, key_type, value_type)
+    s, _ = mk_store(fmt, first, first + rows - 1, ref_stride=ref_stride)
+    o = oracle_store(oracle, fmt, first, first + rows - 1, ref_stride=ref_stride)
+    init = (rng.integers(50, 60, size=(rows, 1)).astype(np.int32) if value_type == 0
+            else rng.standard_normal((rows, 1)).astype(s.dtype))
+    s.load_values(init)
+    o.data[:] = init
+    vs = 8 if (ref_stride and value_type == 1) else None
+    pushes = []
+    for b in range(12):
+        k = rng.choice(rows, size=20_000, replace=False)
+        v = (rng.integers(-2, 3, size=len(k)) if value_type == 0 else rng.standard_normal(len(k)) * 1e-3)
+        pushes.append(encode_array_push(first + k, v, key_type, value_type, value_stride=vs))
+    for p in pushes:
+        assert o.push(p) == 0
+    s.handlePushBatch(fmt, pushes)
+    assert kat.bits_equal(s.values(), o.data)
+
+
+# ----------------------------------------------------------------- error semantics
+@pytest.mark.parametrize("kind", ["key", "trunc", "neg"])
+def test_batch_error_state_matches_sequential(oracle, kind):
+    from distml_amd import DataDesc, DistMLException, encode_matrix_push
+    rng = np.random.default_rng(7)
+    first, rows, cols = 0, 64, 48
+    vt = 0 if kind == "neg" else 1
+    fmt = DataDesc(1, 0, vt)
+    pushes = rand_matrix_pushes(rng, first, rows, cols, 0, vt, 6, 0.8)
+    if kind == "key":
+        cut = 5 * (4 + 4 * cols)
+        pushes[3] = pushes[3][:cut] + encode_matrix_push([rows + 3], np.ones((1, cols)), 0, vt) + pushes[3][cut:]
+    elif kind == "trunc":
+        pushes[2] = pushes[2][:-(4 * cols // 2 + 2)]
+    else:
+        bad = np.zeros((1, cols), np.int32)
+        bad[0, 17] = -1000
+        pushes[2] = pushes[2] + encode_matrix_push([9], bad, 0, 0) + encode_matrix_push([10], bad, 0, 0)
+    o = oracle_store(oracle, fmt, first, rows - 1, cols)
+    init = (rng.integers(5, 9, size=(rows, cols)).astype(np.int32) if vt == 0
+            else rng.standard_normal((rows, cols)).astype(np.float32))
+    o.data[:] = init
+    rc = 0
+    for p in pushes:
+        rc = o.push(p)
+        if rc:
+            break
+    assert rc != 0
+    for api in ("sequential", "batch"):
+        s, _ = mk_store(fmt, first, rows - 1, cols)
+        s.load_values(init)
+        with pytest.raises(DistMLException) as ei:
+            if api == "batch":
+                s.handlePushBatch(fmt, pushes)
+            else:
+                for p in pushes:
+                    s.handlePush(fmt, p)
+        assert (ei.value.code, ei.value.key, ei.value.col) == o.error()
+        assert kat.bits_equal(s.values(), o.data)
+        # the failed store refuses further pushes (the reference's PS loop has ended)
+        with pytest.raises(DistMLException):
+            s.handlePush(fmt, pushes[0])
+        s.close()
+
+
+def test_async_push_defers_error_to_flush(oracle):
+    from distml_amd import DataDesc, IllegalStateException, encode_matrix_push
+    fmt = DataDesc(1, 0, 0)
+    s, _ = mk_store(fmt, 0, 3, 2, async_push=True)
+    s.handlePush(fmt, encode_matrix_push([1], [[-1, 0]], 0, 0))  # returns before the check
+    with pytest.raises(IllegalStateException):
+        s.flush()
+    assert s.values()[1, 0] == -1
+
+
+# ----------------------------------------------------------------- fetch / checkpoint
+def test_fetch_layouts_match_oracle(oracle):
+    from distml_amd import DataDesc, KeyList, KeyRange
+    rng = np.random.default_rng(3)
+    for dt, kt, vt, cols, ada in [(1, 0, 1, 17, False), (1, 1, 0, 5, False), (1, 0, 3, 3, False),
+                                  (1, 0, 1, 4, True), (0, 1, 1, 1, False), (0, 0, 0, 1, False), (0, 0, 3, 1, False)]:
+        fmt = DataDesc(dt, kt, vt, False, True, ada)
+        s, _ = mk_store(fmt, 40, 139, cols)
+        o = oracle_store(oracle, fmt, 40, 139, cols)
+        init = (rng.integers(0, 100, size=(100, cols)).astype(np.int32) if vt == 0
+                else rng.standard_normal((100, cols)).astype(s.dtype))
+        s.load_values(init)
+        o.data[:] = init
+        if ada:
+            s.setAlpha(0.5, 0.01, 1.5)
+            o.set_alpha(0.5, 0.01, 1.5)
+        keys = [139, 40, 77, 78, 100]
+        assert s.handleFetch(fmt, KeyList(keys + [5, 500])) == o.fetch(keys)
+        assert s.handleFetch(fmt, KeyRange(130, 200)) == o.fetch(list(range(130, 140)))
+        s.close()
+
+
+def test_write_all_read_all_round_trip(oracle):
+    from distml_amd import DataDesc
+    rng = np.random.default_rng(5)
+    for vt in (0, 1, 3):
+        fmt = DataDesc(1, 0, vt)
+        s, _ = mk_store(fmt, 0, 999, 13)
+        o = oracle_store(oracle, fmt, 0, 999, 13)
+        init = (rng.integers(-50, 50, size=(1000, 13)).astype(np.int32) if vt == 0
+                else rng.standard_normal((1000, 13)).astype(s.dtype))
+        s.load_values(init)
+        o.data[:] = init
+        blob = s.writeAll()
+        assert blob == o.write_all()
+        s.zero()
+        assert not s.values().any()
+        s.readAll(io.BytesIO(blob))
+        assert kat.bits_equal(s.values(), init)
+        buf = io.BytesIO()
+        s.syncTo(buf, 10, 20)
+        assert buf.getvalue() == blob[10 * 13 * s.values().itemsize: 21 * 13 * s.values().itemsize]
+        s.close()
+
+
+# ------------------------------------------------------- full-size configs (BASELINE.json)
+def synth_device_buckets(L, desc, first, shard_rows, nrec, cols, seeds, perms):
+    from distml_amd.datadesc import DataDesc
+    K = 4 if desc.key_type == 0 else 8
+    V = 8 if desc.value_type == 3 else 4
+    n = nrec * (K + V * cols)
+    bufs = []
+    st = torch.cuda.current_stream().cuda_stream
+    for sd, (pa, pc) in zip(seeds, perms):
+        t = torch.empty(n, dtype=torch.uint8, device="cuda")
+        assert L.dml_synth_dense_bucket(t.data_ptr(), C.byref(desc), first, shard_rows, nrec, cols, sd, pa, pc,
+                                        C.c_void_p(st)) == 0
+        bufs.append(t)
+    torch.cuda.synchronize()
+    return bufs
+
+
+def test_synth_kernel_matches_oracle_generator(oracle):
+    from distml_amd import _lib
+    from distml_amd.datadesc import DataDesc
+    L = _lib.load()
+    for kt, vt, cols in [(0, 1, 1024), (1, 3, 7), (0, 0, 1000)]:
+        d = DataDesc(1, kt, vt).to_c()
+        b = synth_device_buckets(L, d, 3, 509, 509, cols, [11], [(7, 5)])[0]
+        want = oracle.synth_dense_bucket(kt, vt, 3, 509, 509, cols, 11, 7, 5)
+        assert b.cpu().numpy().tobytes() == want.tobytes()
+    d = DataDesc(0, 1, 1).to_c()
+    t = torch.empty(1000 * 12, dtype=torch.uint8, device="cuda")
+    assert L.dml_synth_sparse_bucket(t.data_ptr(), C.byref(d), 0, 10**9, 1000, 9, 123457, 99, C.c_void_p(0)) == 0
+    torch.cuda.synchronize()
+    assert t.cpu().numpy().tobytes() == oracle.synth_sparse_bucket(1, 1, 0, 10**9, 1000, 9, 123457, 99).tobytes()
+
+
+def config2_perm(b, rows=16384):
+    # ascending row order (Java HashMap<Integer> order) for even pushes, a seeded permutation for odd
+    return (1, 0) if b % 2 == 0 else ((2 * b + 1) * 2654435761 % rows | 1, (b * 7919) % rows)
+
+
+def test_config2_dense_fp32_full_size_bit_exact(oracle):
+    """Config 2: 32 pushes x 64 MiB ([int32 key][1024 x f32] x 16384) -> one 64 MiB shard."""
+    from distml_amd import DataDesc
+    rows, cols, W = 16384, 1024, 32
+    fmt = DataDesc(1, 0, 1)
+    s, _ = mk_store(fmt, 0, rows - 1, cols)
+    s.rand(7)
+    o = oracle_store(oracle, fmt, 0, rows - 1, cols)
+    o.synth_fill(7)
+    assert kat.bits_equal(s.values(), o.data)
+    from distml_amd import _lib
+    L = _lib.load()
+    perms = [config2_perm(b) for b in range(W)]
+    bufs = synth_device_buckets(L, fmt.to_c(), 0, rows, rows, cols, [1000 + b for b in range(W)], perms)
+    s.pushDevice([b.data_ptr() for b in bufs], [b.numel() for b in bufs])
+    s.flush()
+    host = [oracle.synth_dense_bucket(0, 1, 0, rows, rows, cols, 1000 + b, *perms[b]) for b in range(W)]
+    assert o.push_many(host, threads=8) == 0
+    assert kat.bits_equal(s.values(), o.data)
+
+
+def test_config3_sparse_fp32_full_size_bit_exact(oracle):
+    """Config 3: 1e9-dim fp32 array shard, 32 pushes x 1e6 unique keys (12-byte records)."""
+    from distml_amd import DataDesc, _lib
+    dim, nnz, W = 10**9, 10**6, 32
+    fmt = DataDesc(0, 1, 1)
+    s, _ = mk_store(fmt, 0, dim - 1)
+    L = _lib.load()
+    d = fmt.to_c()
+    bufs, host = [], []
+    for b in range(W):
+        pa, pc = (2 * b + 3) * 999_999_937 % dim, (b * 12_345_701) % dim
+        while pa % 2 == 0 or pa % 5 == 0:
+            pa += 1
+        t = torch.empty(nnz * 12, dtype=torch.uint8, device="cuda")
+        assert L.dml_synth_sparse_bucket(t.data_ptr(), C.byref(d), 0, dim, nnz, 2000 + b, pa, pc, C.c_void_p(0)) == 0
+        bufs.append(t)
+        host.append((pa, pc))
+    torch.cuda.synchronize()
+    s.pushDevice([b.data_ptr() for b in bufs], [b.numel() for b in bufs])
+    s.flush()
+    o = oracle_store(oracle, fmt, 0, dim - 1)
+    for b, (pa, pc) in enumerate(host):
+        assert o.push(oracle.synth_sparse_bucket(1, 1, 0, dim, nnz, 2000 + b, pa, pc).tobytes()) == 0
+    assert kat.bits_equal(s.values(), o.data)
+
+
+def test_config5_lda_int32_shard_bit_exact(oracle):
+    """Config 5, one GPU's shard of linearSplit(8): 125 000 x 1 000 int32 counts,
+    32 pushes x 8 192 distinct rows, deltas in {-2..2}, init U{64..114} (no negatives)."""
+    from distml_amd import DataDesc, _lib
+    rows, cols, W, nrec = 125_000, 1000, 32, 8192
+    fmt = DataDesc(1, 0, 0)
+    s, _ = mk_store(fmt, 0, rows - 1, cols)
+    s.rand(11)
+    o = oracle_store(oracle, fmt, 0, rows - 1, cols)
+    o.synth_fill(11)
+    L = _lib.load()
+    perms = [((4000 + b) * 2654435761 % rows | 1, b * 331 % rows) for b in range(W)]
+    perms = [(pa if np.gcd(pa, rows) == 1 else pa + 2, pc) for pa, pc in perms]
+    assert all(np.gcd(pa, rows) == 1 for pa, _ in perms)
+    bufs = synth_device_buckets(L, fmt.to_c(), 0, rows, nrec, cols, [4000 + b for b in range(W)], perms)
+    s.pushDevice([b.data_ptr() for b in bufs], [b.numel() for b in bufs])
+    s.flush()
+    host = [oracle.synth_dense_bucket(0, 0, 0, rows, nrec, cols, 4000 + b, *perms[b]) for b in range(W)]
+    assert o.push_many(host, threads=8) == 0
+    assert kat.bits_equal(s.values(), o.data)
+
+
+def test_config4_adagrad_rows_bit_exact(oracle):
+    """Config 4 rows (AdaGrad Word2Vec store, 200 cols), reduced to 20 000 rows x 8 pushes;
+    large gradients so delta crosses 1.0 and alpha/minAlpha paths run."""
+    from distml_amd import DataDesc, encode_matrix_push
+    rng = np.random.default_rng(44)
+    rows, cols, W = 20_000, 200, 8
+    fmt = DataDesc(1, 0, 1, False, True, True)
+    s, _ = mk_store(fmt, 0, rows - 1, cols)
+    o = oracle_store(oracle, fmt, 0, rows - 1, cols)
+    s.setAlpha(0.025, 0.0001, 1.5)
+    o.set_alpha(0.025, 0.0001, 1.5)
+    pushes = []
+    for b in range(W):
+        r = rng.permutation(rows)[: rows // 2]
+        v = (rng.standard_normal((len(r), cols)) * 0.6).astype(np.float32)
+        pushes.append(encode_matrix_push(r, v, 0, 1))
+    for p in pushes:
+        assert o.push(p) == 0
+    s.handlePushBatch(fmt, pushes)
+    assert kat.bits_equal(s.values(), o.data)
+    a, d = s.adagrad_state()
+    assert kat.bits_equal(a, o.alpha)
+    assert kat.bits_equal(d, o.delta)
+    assert s.maxDelta() == o.max_delta()
