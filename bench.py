@@ -1,0 +1,202 @@
+"""Benchmark: device-resident gradient-bucket reduce GiB/s (BASELINE.json metric).
+
+N=1 (default) — config 2 of BASELINE.json: a 16 384 x 1 024 fp32 shard (64 MiB,
+DataDesc MATRIX/INT/FLOAT dense) receives 32 pushes of 64 MiB each
+([int32 key][1 024 x f32] x 16 384 records = 67 174 400 B), resident in HBM.
+One step = dml_store_push_batch_device(32 pushes): slot-table reset, key
+index kernel (side stream, overlapping the previous batch's reduce), the
+ordered multi-push reduce kernel, the error check; the timed region ends with
+flush() (every batch applied and error-checked) and a device synchronize.
+Algorithmic bytes per step = 32 x 67 174 400 + 2 x 67 108 864 = 2 283 798 528.
+
+N>1 (torchrun, one rank per GPU, RCCL) — weak scaling: every rank holds 32
+full-range pushes of the same 64 MiB model, whose rows are linearSplit over
+the N ranks; step = ordered pre-reduce of the 32 local pushes, RCCL
+reduce-scatter of the partials, owner apply.
+
+Also reported: the dominant kernel's HBM roofline (achieved from HIP events
+around every k_reduce launch, on the store's stream) and the CPU baseline
+(the oracle's restatement of FloatMatrixStore.updateRow, 1 thread, timed on
+this host on the same pushes).
+"""
+from __future__ import annotations
+
+import argparse
+import ctypes as C
+import json
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+ROWS, COLS, W = 16384, 1024, 32
+REC = 4 + 4 * COLS
+BUCKET = ROWS * REC                      # 67 174 400 B
+SHARD = ROWS * COLS * 4                  # 67 108 864 B
+HBM_PEAK_GBS = 8000.0                    # MI355X_MICROARCH.md: HBM3E 8.0 TB/s (spec)
+
+
+def perm_for(b: int):
+    # even pushes list rows ascending (Java HashMap<Integer> order), odd ones a seeded permutation
+    return (1, 0) if b % 2 == 0 else (((2 * b + 1) * 2654435761) % ROWS | 1, (b * 7919) % ROWS)
+
+
+def make_buckets(L, torch, fmt, n, rows_total):
+    st = torch.cuda.current_stream().cuda_stream
+    bufs = []
+    for b in range(n):
+        t = torch.empty(rows_total * REC, dtype=torch.uint8, device="cuda")
+        pa, pc = perm_for(b)
+        rc = L.dml_synth_dense_bucket(t.data_ptr(), C.byref(fmt.to_c()), 0, rows_total, rows_total, COLS,
+                                      1000 + b, pa % rows_total, pc % rows_total, C.c_void_p(st))
+        assert rc == 0, rc
+        bufs.append(t)
+    torch.cuda.synchronize()
+    return bufs
+
+
+def cpu_baseline(budget_s: float = 12.0):
+    """Oracle (C restatement of FloatMatrixStore.updateRow, single thread) on the
+    same 32 x 64 MiB pushes, repeated until `budget_s` of CPU work."""
+    sys.path.insert(0, os.path.join(ROOT, "oracle"))
+    import pyoracle
+    bufs = [pyoracle.synth_dense_bucket(0, 1, 0, ROWS, ROWS, COLS, 1000 + b, *perm_for(b)) for b in range(W)]
+    o = pyoracle.OracleStore(1, 0, 1, 0, ROWS - 1, COLS)
+    o.synth_fill(7)
+    reps, t0 = 0, time.perf_counter()
+    while True:
+        assert o.push_many(bufs, threads=1) == 0
+        reps += 1
+        el = time.perf_counter() - t0
+        if el >= budget_s or reps >= 50:
+            break
+    algo = W * BUCKET + 2 * SHARD
+    return {"value": round(reps * algo / el / 2**30, 3), "unit": "GiB/s", "cores": 1, "kind": "port",
+            "sample": f"full config-2 workload (32 x 64 MiB pushes -> 16384x1024 fp32 shard) x{reps} reps, "
+                      f"{el:.1f} s, oracle/dml_oracle.c single thread"}
+
+
+def load_traffic():
+    p = os.path.join(ROOT, "profiles", "pmc_traffic.json")
+    if not os.path.exists(p):
+        return None
+    try:
+        d = json.load(open(p))
+        return d.get("hbm_bytes_per_launch")
+    except Exception:
+        return None
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--no-cpu", action="store_true", help="skip the CPU baseline leg")
+    args = ap.parse_args()
+
+    import torch
+    import torch.distributed as dist
+    from distml_amd import DataDesc, DataStore, KeyRange, _lib
+    from distml_amd.group import ShardGroup
+    from distml_amd.store import DeviceBatch
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    assert world == args.gpus, f"--gpus {args.gpus} but WORLD_SIZE={world}"
+    torch.cuda.set_device(local)
+    if world > 1:
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+    L = _lib.load()
+    fmt = DataDesc(DataDesc.DATA_TYPE_MATRIX, DataDesc.KEY_TYPE_INT, DataDesc.ELEMENT_TYPE_FLOAT)
+
+    def barrier():
+        if world > 1:
+            dist.barrier()
+        torch.cuda.synchronize()
+
+    if world == 1:
+        store = DataStore(fmt, KeyRange(0, ROWS - 1), COLS, device=local)
+        store.rand(7)
+        bufs = make_buckets(L, torch, fmt, W, ROWS)
+        batch = DeviceBatch([b.data_ptr() for b in bufs], [b.numel() for b in bufs])
+
+        def step():
+            # async: ack once captured; the store keeps <= 2 batches in flight and the
+            # key index of batch k+1 overlaps the reduce of batch k
+            store.pushDevice(batch)
+
+        def finish():
+            store.flush()  # every pushed batch applied and error-checked
+        timed_store = store
+        algo_per_rank = W * BUCKET + 2 * SHARD
+    else:
+        group = ShardGroup(fmt, ROWS, COLS, rank, world, device=local)
+        bufs = make_buckets(L, torch, fmt, W, ROWS)
+        ptrs, lens = [b.data_ptr() for b in bufs], [b.numel() for b in bufs]
+        st = torch.cuda.current_stream().cuda_stream
+
+        def step():
+            group.push_full_range(ptrs, lens, st)
+
+        def finish():
+            group.flush()
+        timed_store = group.store
+        algo_per_rank = W * BUCKET + 2 * group.shard.size() * COLS * 4
+
+    for _ in range(args.warmup):
+        step()
+    finish()
+    timed_store.set_timing(True)
+    timed_store.kernel_time(reset=True)
+    barrier()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        step()
+    finish()
+    barrier()
+    el = time.perf_counter() - t0
+    k_ms, k_n = timed_store.kernel_time(reset=True)
+    timed_store.set_timing(False)
+    t = torch.tensor([el], dtype=torch.float64, device="cuda")
+    if world > 1:
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    el = float(t.item())
+
+    total_bytes = algo_per_rank * world * args.steps
+    value = total_bytes / el / 2**30
+    line = {
+        "metric": "device-resident gradient-bucket reduce GiB/s (dense fp32 + sparse scatter-add)",
+        "value": round(value, 2), "unit": "GiB/s", "n_gpus": world, "steps": args.steps,
+        "warmup": args.warmup, "ms_per_step": round(el / args.steps * 1e3, 4), "higher_is_better": True,
+        "scaling": "weak", "vs_baseline": None, "dtype": "f32", "data": "synthetic",
+        "config": {"workload": "config2: dense fp32 reduce, 32 device-resident pushes x 64 MiB "
+                               "([int32 key][1024 x f32] x 16384) -> 16384x1024 fp32 shard per model",
+                   "pushes_per_gpu": W, "push_bytes": BUCKET, "model_rows": ROWS, "cols": COLS,
+                   "parallelism": "single shard" if world == 1 else f"linearSplit({world}) + RCCL reduce-scatter",
+                   "algorithmic_bytes_per_step_per_gpu": algo_per_rank},
+    }
+    if rank == 0:
+        if world == 1 and k_n > 0:
+            avg_s = k_ms / k_n / 1e3
+            achieved = algo_per_rank / avg_s / 1e9
+            traffic = load_traffic()
+            line["roofline"] = {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS,
+                                "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic,
+                                "kernel": "k_reduce<float,kAdd>", "avg_kernel_us": round(avg_s * 1e6, 2),
+                                "launches": k_n}
+        elif k_n > 0:
+            line["roofline"] = {"bound": "hbm", "achieved": None, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                                "frac": None, "traffic": None, "note": "apply kernel only timed at N>1"}
+        if world == 1 and not args.no_cpu:
+            line["cpu_baseline"] = cpu_baseline()
+        print(json.dumps(line), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

@@ -17,8 +17,9 @@ __host__ __device__ inline uint64_t pos_of(uint64_t bucket, uint64_t off) { retu
 constexpr uint64_t kNoPos = ~0ull;
 constexpr uint64_t kOffMask = (1ull << 40) - 1;
 
-// Per-batch control block. Lives at the head of the slot-table allocation so
-// ONE hipMemsetAsync(0xFF) resets it and the slot table (-1 = no record).
+// Per-batch control block. Lives at the head of the workspace
+// [Ctrl | slot rows x kMaxW int32 | rowflag rows x uint32]: one hipMemsetAsync(0xFF)
+// resets Ctrl and the slot table (-1 = no record); rowflag is zeroed separately.
 struct Ctrl {
     unsigned long long cutoff;   // first key-out-of-shard position (exclusive apply limit)
     unsigned long long neg_pos;  // first add that left an int32 counter negative
@@ -33,7 +34,15 @@ struct Batch {
     int64_t len[kMaxW];
     int64_t nrec[kMaxW];  // records whose key is complete (a truncated tail record included)
     int32_t bidx[kMaxW];  // global push index of each column (positions use it; columns ascend)
+    const Ctrl* prev;     // control block of the chunk enqueued just before (pipelining), or null
 };
+
+// A chunk whose predecessor ended abnormally (error, or rows to replay) must
+// not run ahead of the host's fix-up: its kernels turn into no-ops and the
+// host relaunches (replay) or drops (error) it.
+__host__ __device__ inline bool ctrl_abnormal(const Ctrl* c) {
+    return c->cutoff != kNoPos || c->neg_pos != kNoPos || c->no_dup == 0u;
+}
 
 // Running AdaGrad maxDelta state (FloatMatrixStoreAdaGrad.java:27-29), device resident.
 struct MaxDelta {
@@ -67,22 +76,31 @@ enum ReduceMode : int {
 
 enum VType : int { kI32 = 0, kF32 = 1, kF64 = 3 };
 
+// Optional start/stop events carried in the dispatch packet (hipExtLaunchKernel):
+// kernel timing and cross-stream dependencies without extra marker packets.
+struct LaunchEv {
+    hipEvent_t start = nullptr;
+    hipEvent_t stop = nullptr;
+};
+
 // ---- launchers (dml_kernels.hip) ----
 hipError_t launch_index(const Batch& bt, int nb, int64_t max_nrec, int64_t stride, int K,
-                        int64_t first, int64_t rows, int32_t* slot, Ctrl* ctrl, hipStream_t st);
+                        int64_t first, int64_t rows, int32_t* slot, uint32_t* rowflag, Ctrl* ctrl,
+                        uint64_t tail_cut, hipStream_t st);
 hipError_t launch_reduce(int vtype, int mode, void* shard, int64_t rows, int32_t cols, const Batch& bt,
-                         int nb, int64_t stride, int K, const int32_t* slot, Ctrl* ctrl,
-                         uint64_t tail_cut, const AdaArgs& ada, hipStream_t st, int64_t* nblocks_out);
+                         int nb, int64_t stride, int K, const int32_t* slot, const uint32_t* rowflag, Ctrl* ctrl,
+                         uint64_t tail_cut, const AdaArgs& ada, hipStream_t st, int64_t* nblocks_out,
+                         LaunchEv ev = {});
 hipError_t launch_rollback_i32(int32_t* shard, int64_t rows, int32_t cols, const Batch& bt, int nb,
-                               int64_t stride, int K, const int32_t* slot, Ctrl* ctrl,
+                               int64_t stride, int K, const int32_t* slot, const uint32_t* rowflag, Ctrl* ctrl,
                                uint64_t tail_cut, hipStream_t st);
 hipError_t launch_maxdelta_finalize(const DeltaCand* cand, int64_t n, MaxDelta* md, const Batch& bt, int nb,
                                     int64_t stride, int K, int V, hipStream_t st);
 hipError_t launch_array_validate(const Batch& bt, int nb, int64_t max_nrec, int64_t stride,
-                                 int K, int64_t first, int64_t rows, Ctrl* ctrl, hipStream_t st);
+                                 int K, int64_t first, int64_t rows, Ctrl* ctrl, uint64_t tail_cut, hipStream_t st);
 hipError_t launch_array_apply(int vtype, void* shard, int64_t rows, const uint8_t* base, int64_t nrec,
                               int b_global, int64_t stride, int K, int64_t first, Ctrl* ctrl,
-                              uint64_t tail_cut, hipStream_t st);
+                              uint64_t tail_cut, const Ctrl* prev, hipStream_t st, LaunchEv ev = {});
 hipError_t launch_array_rollback_i32(int32_t* shard, int64_t rows, const uint8_t* base, int64_t nrec,
                                      int b_global, int64_t stride, int K, int64_t first, Ctrl* ctrl,
                                      uint64_t tail_cut, hipStream_t st);

@@ -17,7 +17,11 @@
 //                   init / owner-apply / synthetic data.
 #include "dml_internal.h"
 
+#include <hip/hip_ext.h>
+
+#include <algorithm>
 #include <climits>
+#include <cstdlib>
 
 namespace dml {
 
@@ -32,6 +36,12 @@ typedef uint64_t u64x8 __attribute__((ext_vector_type(8)));
 #define DML_GLOBAL __attribute__((address_space(1)))
 __device__ inline u32x4 ldg16(const uint8_t* p) { return *(const DML_GLOBAL u32x4_u*)(p); }
 __device__ inline uint32_t ldg32(const uint8_t* p) { return *(const DML_GLOBAL uint32_t*)(p); }
+// Streamed-once bucket bytes: non-temporal policy (no L2 retention).
+__device__ inline u32x4 ldg16_nt(const uint8_t* p) {
+    return __builtin_nontemporal_load((const DML_GLOBAL u32x4_u*)(p));
+}
+__device__ inline void stg16_nt(void* p, u32x4 v) { __builtin_nontemporal_store(v, (DML_GLOBAL u32x4_u*)(p)); }
+__device__ inline void stg16(void* p, u32x4 v) { *(DML_GLOBAL u32x4_u*)(p) = v; }
 
 __host__ __device__ inline uint64_t splitmix64_dev(uint64_t x) {
     uint64_t z = x + 0x9E3779B97F4A7C15ull;
@@ -99,15 +109,19 @@ __device__ inline u32x4 pack(const T* v) {
 }
 
 // ---------------------------------------------------------------------------
-// k_index: one thread per record of push b (blockIdx.y). Writes
-// slot[row][b] = record index; a row seen twice in one push clears no_dup
-// (the host then replays the batch through the exact sequential path); a key
-// outside the shard lowers ctrl->cutoff to the record's start position.
-__global__ __launch_bounds__(256) void k_index(const Batch bt, int64_t stride, int K,
-                                               int64_t first, int64_t rows, int32_t* __restrict__ slot,
-                                               Ctrl* __restrict__ ctrl) {
+// k_index: one thread per record of push b (blockIdx.y): slot[row][b] = record.
+// A key outside the shard lowers ctrl->cutoff to the record's start position.
+// Rows listed twice by one push are flagged (rowflag[row] = 1): the reduce
+// skips them and the host replays just those rows through the exact layered
+// path. PLAIN: plain stores + k_verify (no scattered returning atomics);
+// otherwise atomicExch detects the repeat directly.
+template <bool PLAIN>
+__global__ __launch_bounds__(256) void k_index(const Batch bt, int64_t stride, int K, int64_t first, int64_t rows,
+                                               int32_t* __restrict__ slot, uint32_t* __restrict__ rowflag,
+                                               Ctrl* __restrict__ ctrl, uint64_t tail_cut) {
     const int b = blockIdx.y;
     const int64_t r = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (r == 0 && b == 0 && tail_cut != kNoPos) atomicMin(&ctrl->cutoff, (unsigned long long)tail_cut);
     if (r >= bt.nrec[b]) return;
     const int64_t off = r * stride;
     const int64_t key = ld_key(bt.base[b] + off, K);
@@ -116,15 +130,52 @@ __global__ __launch_bounds__(256) void k_index(const Batch bt, int64_t stride, i
         atomicMin(&ctrl->cutoff, (unsigned long long)pos_of((uint64_t)bt.bidx[b], (uint64_t)off));
         return;
     }
-    const int32_t old = atomicExch(&slot[idx * kMaxW + b], (int32_t)r);
-    if (old != -1) atomicAnd(&ctrl->no_dup, 0u);
+    if constexpr (PLAIN) {
+        *(DML_GLOBAL int32_t*)&slot[idx * kMaxW + b] = (int32_t)r;
+    } else {
+        const int32_t old = atomicExch(&slot[idx * kMaxW + b], (int32_t)r);
+        if (old != -1) {
+            rowflag[idx] = 1u;
+            ctrl->no_dup = 0u;  // benign race: every writer stores the same value
+        }
+    }
 }
 
-hipError_t launch_index(const Batch& bt, int nb, int64_t max_nrec, int64_t stride, int K,
-                        int64_t first, int64_t rows, int32_t* slot, Ctrl* ctrl, hipStream_t st) {
-    if (max_nrec <= 0 || nb <= 0) return hipSuccess;
-    dim3 grid((unsigned)((max_nrec + 255) / 256), (unsigned)nb);
-    hipLaunchKernelGGL(k_index, grid, dim3(256), 0, st, bt, stride, K, first, rows, slot, ctrl);
+// k_verify (after k_index<true>): a record whose slot holds another record lost
+// a race with a record of the same row and push -> flag the row.
+__global__ __launch_bounds__(256) void k_verify(const Batch bt, int64_t stride, int K, int64_t first, int64_t rows,
+                                                const int32_t* __restrict__ slot, uint32_t* __restrict__ rowflag,
+                                                Ctrl* __restrict__ ctrl) {
+    const int b = blockIdx.y;
+    const int64_t r = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (r >= bt.nrec[b]) return;
+    const int64_t idx = row_index(ld_key(bt.base[b] + r * stride, K), first, rows);
+    if (idx < 0) return;
+    if (slot[idx * kMaxW + b] != (int32_t)r) {
+        rowflag[idx] = 1u;
+        ctrl->no_dup = 0u;
+    }
+}
+
+int index_variant() {
+    const char* v = getenv("DML_INDEX_VARIANT");
+    return v ? atoi(v) : 0;
+}
+
+hipError_t launch_index(const Batch& bt, int nb, int64_t max_nrec, int64_t stride, int K, int64_t first,
+                        int64_t rows, int32_t* slot, uint32_t* rowflag, Ctrl* ctrl, uint64_t tail_cut, hipStream_t st) {
+    if (nb <= 0) return hipSuccess;
+    dim3 grid((unsigned)std::max<int64_t>(1, (max_nrec + 255) / 256), (unsigned)nb);
+    if (index_variant() == 0) {
+        hipLaunchKernelGGL(k_index<false>, grid, dim3(256), 0, st, bt, stride, K, first, rows, slot, rowflag, ctrl,
+                           tail_cut);
+        return hipGetLastError();
+    }
+    hipLaunchKernelGGL(k_index<true>, grid, dim3(256), 0, st, bt, stride, K, first, rows, slot, rowflag, ctrl,
+                       tail_cut);
+    hipError_t e = hipGetLastError();
+    if (e != hipSuccess) return e;
+    hipLaunchKernelGGL(k_verify, grid, dim3(256), 0, st, bt, stride, K, first, rows, slot, rowflag, ctrl);
     return hipGetLastError();
 }
 
@@ -135,16 +186,16 @@ hipError_t launch_index(const Batch& bt, int nb, int64_t max_nrec, int64_t strid
 // up to 8 pushes in flight per lane, 16 B each), then writes the row once.
 // Elements at or past the batch cutoff (first key/truncation error) are not
 // applied — the state the reference leaves when its exception escapes.
-template <typename T, int MODE>
-__global__ __launch_bounds__(256) void k_reduce(T* __restrict__ shard, int64_t rows, int32_t cols, int32_t nchunks,
+template <typename T, int MODE, int G, bool NT, int WPB, bool SNT = false>
+__global__ __launch_bounds__(64 * WPB) void k_reduce(T* __restrict__ shard, int64_t rows, int32_t cols, int32_t nchunks,
                                                 const Batch bt, int nb, int64_t stride, int K,
-                                                const int32_t* __restrict__ slot, Ctrl* __restrict__ ctrl,
-                                                uint64_t tail_cut, AdaArgs ada) {
+                                                const int32_t* __restrict__ slot, const uint32_t* __restrict__ rowflag,
+                                                Ctrl* __restrict__ ctrl, uint64_t tail_cut, AdaArgs ada) {
     constexpr int VEC = Elem<T>::VEC;
-    constexpr int G = 8;
+    static_assert(G == 8 || G == 16, "slot groups are loaded 8 at a time");
     const int lane = threadIdx.x & 63;
     const int wid = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-    const int64_t task = (int64_t)blockIdx.x * 4 + wid;
+    const int64_t task = (int64_t)blockIdx.x * WPB + wid;
     const int64_t ntask = rows * (int64_t)nchunks;
 
     // AdaGrad maxDelta candidate of this lane.
@@ -153,8 +204,9 @@ __global__ __launch_bounds__(256) void k_reduce(T* __restrict__ shard, int64_t r
     bool cand_ok = false;
 
     if (task < ntask) do {
-        if (MODE != kPreReduce && ctrl->no_dup == 0u) break;  // host replays sequentially
+        if (bt.prev && ctrl_abnormal(bt.prev)) break;  // predecessor needs the host first
         const int64_t row = task / nchunks;
+        if (rowflag && rowflag[row]) break;  // a push repeats this row: the host replays it exactly
         const int chunk = (int)(task - row * nchunks);
         const int32_t c0 = (chunk * 64 + lane) * VEC;
         const int nv = c0 < cols ? (cols - c0 < VEC ? cols - c0 : VEC) : 0;
@@ -184,7 +236,7 @@ __global__ __launch_bounds__(256) void k_reduce(T* __restrict__ shard, int64_t r
 #pragma unroll
                 for (int e = 0; e < VEC; ++e) acc[e] = T(0);
             } else if (nv == VEC) {
-                const u32x4 t = *(const u32x4_u*)prow;
+                const u32x4 t = SNT ? ldg16_nt((const uint8_t*)prow) : ldg16((const uint8_t*)prow);
                 unpack<T>(t, acc);
             } else {
 #pragma unroll
@@ -228,24 +280,31 @@ __global__ __launch_bounds__(256) void k_reduce(T* __restrict__ shard, int64_t r
             }
         };
 
-        const bool vec_ok = (cols % VEC) == 0;  // wave-uniform: every active lane holds VEC elements
-        if (nv == 0) break;                      // lanes past the row's last column idle
+        const bool vec_ok = cols >= VEC;   // wave-uniform: vector loads for every active lane
+        if (nv == 0) break;                 // lanes past the row's last column idle
+        // A ragged row's last lane (nv < VEC) loads the 16 B that END at its last
+        // element (in bounds: c0 >= VEC - nv) and shifts them down by `sh` elements.
+        const int sh = VEC - nv;
+        const int64_t shb = (int64_t)sh * (int64_t)sizeof(T);
 
         for (int b0 = 0; b0 < nb; b0 += G) {
             // Wave-uniform scalar loads of 8 slots / push indices / bases at once;
             // every index < kMaxW is in bounds of the slot row and the kernarg table.
-            const i32x8 sv = *(const i32x8*)(srow + b0);
-            const i32x8 gv = *(const i32x8*)(&bt.bidx[b0]);
-            const u64x8 pv = *(const u64x8*)(&bt.base[b0]);
             int32_t rr[G];
             int gbv[G];
             const uint8_t* bp[G];
 #pragma unroll
-            for (int g = 0; g < G; ++g) {
-                const bool in = b0 + g < nb;
-                gbv[g] = in ? gv[g] : INT_MAX;
-                bp[g] = (const uint8_t*)pv[g];
-                rr[g] = (in && gbv[g] <= cut_b) ? sv[g] : -1;
+            for (int h = 0; h < G; h += 8) {
+                const i32x8 sv = *(const i32x8*)(srow + b0 + h);
+                const i32x8 gv = *(const i32x8*)(&bt.bidx[b0 + h]);
+                const u64x8 pv = *(const u64x8*)(&bt.base[b0 + h]);
+#pragma unroll
+                for (int g = 0; g < 8; ++g) {
+                    const bool in = b0 + h + g < nb;
+                    gbv[h + g] = in ? gv[g] : INT_MAX;
+                    bp[h + g] = (const uint8_t*)pv[g];
+                    rr[h + g] = (in && gbv[h + g] <= cut_b) ? sv[g] : -1;
+                }
             }
             bool any = false;
 #pragma unroll
@@ -260,20 +319,27 @@ __global__ __launch_bounds__(256) void k_reduce(T* __restrict__ shard, int64_t r
                 u32x4 raw[G];
 #pragma unroll
                 for (int g = 0; g < G; ++g) {
-                    const uint8_t* src = rr[g] >= 0 ? bp[g] + (int64_t)rr[g] * stride + voff : (const uint8_t*)prow;
-                    raw[g] = ldg16(src);
+                    const uint8_t* src = (rr[g] >= 0 ? bp[g] + (int64_t)rr[g] * stride + voff : (const uint8_t*)prow) - shb;
+                    raw[g] = NT ? ldg16_nt(src) : ldg16(src);
                 }
 #pragma unroll
                 for (int g = 0; g < G; ++g) {
                     if (rr[g] < 0) continue;  // wave-uniform
-                    T u[VEC];
-                    unpack<T>(raw[g], u);
+                    T t[VEC], u[VEC];
+                    unpack<T>(raw[g], t);
+#pragma unroll
+                    for (int e = 0; e < VEC; ++e) {  // u[e] = t[e + sh] without runtime register indexing
+                        u[e] = t[e];
+#pragma unroll
+                        for (int k = 1; k < VEC - e; ++k) u[e] = sh == k ? t[e + k] : u[e];
+                    }
                     const uint64_t pb = pos_of((uint64_t)gbv[g], (uint64_t)((int64_t)rr[g] * stride + voff));
 #pragma unroll
-                    for (int e = 0; e < VEC; ++e) apply(e, u[e], pb + (uint64_t)(e * (int)sizeof(T)));
+                    for (int e = 0; e < VEC; ++e)
+                        if (e < nv) apply(e, u[e], pb + (uint64_t)(e * (int)sizeof(T)));
                 }
             } else {
-                // Generic path: ragged lanes, or the group holding the cutoff push.
+                // Generic path: rows narrower than one vector, or the group holding the cutoff push.
                 for (int g = 0; g < G; ++g) {
                     if (rr[g] < 0) continue;
                     const int64_t roff = (int64_t)rr[g] * stride + voff;
@@ -293,7 +359,8 @@ __global__ __launch_bounds__(256) void k_reduce(T* __restrict__ shard, int64_t r
         }
         if (touched && nv > 0) {
             if (nv == VEC) {
-                *(u32x4_u*)prow = pack<T>(acc);
+                if (SNT) stg16_nt(prow, pack<T>(acc));
+                else stg16(prow, pack<T>(acc));
             } else {
                 for (int e = 0; e < nv; ++e) prow[e] = acc[e];
             }
@@ -307,6 +374,7 @@ __global__ __launch_bounds__(256) void k_reduce(T* __restrict__ shard, int64_t r
 
     if constexpr (MODE == kAdaGrad) {
         // Block-wide best candidate: max value, then min position.
+        static_assert(WPB == 4, "AdaGrad reduction assumes 256-thread blocks");
         __shared__ float sv[256];
         __shared__ unsigned long long sp[256];
         __shared__ int sok[256];
@@ -330,19 +398,38 @@ __global__ __launch_bounds__(256) void k_reduce(T* __restrict__ shard, int64_t r
     }
 }
 
-template <typename T, int MODE>
+template <typename T, int MODE, int G = 8, bool NT = false, int WPB = 4, bool SNT = false>
 static hipError_t launch_reduce_t(void* shard, int64_t rows, int32_t cols, const Batch& bt, int nb,
-                                  int64_t stride, int K, const int32_t* slot, Ctrl* ctrl, uint64_t tail_cut,
-                                  const AdaArgs& ada, hipStream_t st, int64_t* nblocks_out) {
+                                  int64_t stride, int K, const int32_t* slot, const uint32_t* rowflag, Ctrl* ctrl,
+                                  uint64_t tail_cut,
+                                  const AdaArgs& ada, hipStream_t st, int64_t* nblocks_out, LaunchEv ev = {}) {
     constexpr int VEC = Elem<T>::VEC;
     const int32_t nchunks = (cols + 64 * VEC - 1) / (64 * VEC);
     const int64_t ntask = rows * nchunks;
-    const int64_t nblocks = (ntask + 3) / 4;
+    const int64_t nblocks = (ntask + WPB - 1) / WPB;
     if (nblocks_out) *nblocks_out = nblocks;
     if (nblocks <= 0) return hipSuccess;
-    hipLaunchKernelGGL((k_reduce<T, MODE>), dim3((unsigned)nblocks), dim3(256), 0, st, (T*)shard, rows, cols,
-                       nchunks, bt, nb, stride, K, slot, ctrl, tail_cut, ada);
+    if (ev.start || ev.stop)
+        hipExtLaunchKernelGGL((k_reduce<T, MODE, G, NT, WPB, SNT>), dim3((unsigned)nblocks), dim3(64 * WPB), 0, st,
+                              ev.start, ev.stop, 0, (T*)shard, rows, cols, nchunks, bt, nb, stride, K, slot, rowflag,
+                              ctrl, tail_cut, ada);
+    else
+        hipLaunchKernelGGL((k_reduce<T, MODE, G, NT, WPB, SNT>), dim3((unsigned)nblocks), dim3(64 * WPB), 0, st, (T*)shard,
+                           rows, cols, nchunks, bt, nb, stride, K, slot, rowflag, ctrl, tail_cut, ada);
     return hipGetLastError();
+}
+
+// f32 kAdd variants (env DML_REDUCE_VARIANT, read per launch; default 3 = measured best):
+// 0: G=8 plain, 1: G=8 nt, 2: G=16 plain, 3: G=16 nt, 4-6: 1/8-wave blocks
+int reduce_variant() {
+    const char* v = getenv("DML_REDUCE_VARIANT");
+    return v ? atoi(v) : 3;
+}
+
+// pre-reduce variants (DML_PREREDUCE_VARIANT): 0 G=8 plain, 1 G=8 nt
+static int prereduce_variant() {
+    const char* v = getenv("DML_PREREDUCE_VARIANT");
+    return v ? atoi(v) : 1;
 }
 
 int64_t reduce_blocks(int vtype, int64_t rows, int32_t cols) {
@@ -352,13 +439,31 @@ int64_t reduce_blocks(int vtype, int64_t rows, int32_t cols) {
 }
 
 hipError_t launch_reduce(int vtype, int mode, void* shard, int64_t rows, int32_t cols, const Batch& bt, int nb,
-                         int64_t stride, int K, const int32_t* slot, Ctrl* ctrl, uint64_t tail_cut,
-                         const AdaArgs& ada, hipStream_t st, int64_t* nblocks_out) {
-#define DML_R(T, M) launch_reduce_t<T, M>(shard, rows, cols, bt, nb, stride, K, slot, ctrl, tail_cut, ada, st, nblocks_out)
+                         int64_t stride, int K, const int32_t* slot, const uint32_t* rowflag, Ctrl* ctrl,
+                         uint64_t tail_cut, const AdaArgs& ada, hipStream_t st, int64_t* nblocks_out, LaunchEv ev) {
+#define DML_R(T, M) launch_reduce_t<T, M, 8, true>(shard, rows, cols, bt, nb, stride, K, slot, rowflag, ctrl, tail_cut, ada, st, nblocks_out, ev)
     if (vtype == kF32) {
-        if (mode == kAdd) return DML_R(float, kAdd);
+        if (mode == kAdd) {
+            // tuning variants (DML_REDUCE_VARIANT=<g>,<nt>), default from measurement
+            switch (reduce_variant()) {
+                case 1: return launch_reduce_t<float, kAdd, 8, true>(shard, rows, cols, bt, nb, stride, K, slot, rowflag, ctrl, tail_cut, ada, st, nblocks_out, ev);
+                case 2: return launch_reduce_t<float, kAdd, 16, false>(shard, rows, cols, bt, nb, stride, K, slot, rowflag, ctrl, tail_cut, ada, st, nblocks_out, ev);
+                case 3: return launch_reduce_t<float, kAdd, 16, true>(shard, rows, cols, bt, nb, stride, K, slot, rowflag, ctrl, tail_cut, ada, st, nblocks_out, ev);
+                case 4: return launch_reduce_t<float, kAdd, 8, true, 1>(shard, rows, cols, bt, nb, stride, K, slot, rowflag, ctrl, tail_cut, ada, st, nblocks_out, ev);
+                case 5: return launch_reduce_t<float, kAdd, 8, true, 8>(shard, rows, cols, bt, nb, stride, K, slot, rowflag, ctrl, tail_cut, ada, st, nblocks_out, ev);
+                case 6: return launch_reduce_t<float, kAdd, 16, true, 8>(shard, rows, cols, bt, nb, stride, K, slot, rowflag, ctrl, tail_cut, ada, st, nblocks_out, ev);
+                case 7: return launch_reduce_t<float, kAdd, 16, true, 4, true>(shard, rows, cols, bt, nb, stride, K, slot, rowflag, ctrl, tail_cut, ada, st, nblocks_out, ev);
+                case 8: return launch_reduce_t<float, kAdd, 8, true, 4, true>(shard, rows, cols, bt, nb, stride, K, slot, rowflag, ctrl, tail_cut, ada, st, nblocks_out, ev);
+                case 0: return launch_reduce_t<float, kAdd, 8, false>(shard, rows, cols, bt, nb, stride, K, slot, rowflag, ctrl, tail_cut, ada, st, nblocks_out, ev);
+                default: return DML_R(float, kAdd);
+            }
+        }
         if (mode == kAdaGrad) return DML_R(float, kAdaGrad);
-        if (mode == kPreReduce) return DML_R(float, kPreReduce);
+        if (mode == kPreReduce) {
+            if (prereduce_variant() == 1)
+                return launch_reduce_t<float, kPreReduce, 8, true>(shard, rows, cols, bt, nb, stride, K, slot, rowflag, ctrl, tail_cut, ada, st, nblocks_out, ev);
+            return DML_R(float, kPreReduce);
+        }
     } else if (vtype == kI32) {
         if (mode == kAdd) return DML_R(int32_t, kAdd);
         if (mode == kAddCheckI32) return DML_R(int32_t, kAddCheckI32);
@@ -372,10 +477,10 @@ hipError_t launch_reduce(int vtype, int mode, void* shard, int64_t rows, int32_t
 }
 
 hipError_t launch_rollback_i32(int32_t* shard, int64_t rows, int32_t cols, const Batch& bt, int nb,
-                               int64_t stride, int K, const int32_t* slot, Ctrl* ctrl, uint64_t tail_cut,
-                               hipStream_t st) {
+                               int64_t stride, int K, const int32_t* slot, const uint32_t* rowflag, Ctrl* ctrl,
+                               uint64_t tail_cut, hipStream_t st) {
     AdaArgs none{};
-    return launch_reduce_t<int32_t, kRollbackI32>(shard, rows, cols, bt, nb, stride, K, slot, ctrl,
+    return launch_reduce_t<int32_t, kRollbackI32>(shard, rows, cols, bt, nb, stride, K, slot, rowflag, ctrl,
                                                   tail_cut, none, st, nullptr);
 }
 
@@ -428,9 +533,11 @@ hipError_t launch_maxdelta_finalize(const DeltaCand* cand, int64_t n, MaxDelta* 
 // ---------------------------------------------------------------------------
 // Array stores. Records [key][value] at stride K+VS.
 __global__ __launch_bounds__(256) void k_array_validate(const Batch bt, int64_t stride, int K,
-                                                        int64_t first, int64_t rows, Ctrl* __restrict__ ctrl) {
+                                                        int64_t first, int64_t rows, Ctrl* __restrict__ ctrl,
+                                                        uint64_t tail_cut) {
     const int b = blockIdx.y;
     const int64_t r = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (r == 0 && b == 0 && tail_cut != kNoPos) atomicMin(&ctrl->cutoff, (unsigned long long)tail_cut);
     if (r >= bt.nrec[b]) return;
     const int64_t off = r * stride;
     if (row_index(ld_key(bt.base[b] + off, K), first, rows) < 0)
@@ -438,10 +545,10 @@ __global__ __launch_bounds__(256) void k_array_validate(const Batch bt, int64_t 
 }
 
 hipError_t launch_array_validate(const Batch& bt, int nb, int64_t max_nrec, int64_t stride, int K,
-                                 int64_t first, int64_t rows, Ctrl* ctrl, hipStream_t st) {
-    if (max_nrec <= 0 || nb <= 0) return hipSuccess;
-    dim3 grid((unsigned)((max_nrec + 255) / 256), (unsigned)nb);
-    hipLaunchKernelGGL(k_array_validate, grid, dim3(256), 0, st, bt, stride, K, first, rows, ctrl);
+                                 int64_t first, int64_t rows, Ctrl* ctrl, uint64_t tail_cut, hipStream_t st) {
+    if (nb <= 0) return hipSuccess;
+    dim3 grid((unsigned)std::max<int64_t>(1, (max_nrec + 255) / 256), (unsigned)nb);
+    hipLaunchKernelGGL(k_array_validate, grid, dim3(256), 0, st, bt, stride, K, first, rows, ctrl, tail_cut);
     return hipGetLastError();
 }
 
@@ -452,9 +559,11 @@ hipError_t launch_array_validate(const Batch& bt, int nb, int64_t max_nrec, int6
 template <typename T, bool CHECK>
 __global__ __launch_bounds__(256) void k_array_apply(T* __restrict__ shard, int64_t rows, const uint8_t* __restrict__ base,
                                                      int64_t nrec, int b_global, int64_t stride, int K,
-                                                     int64_t first, Ctrl* __restrict__ ctrl, uint64_t tail_cut) {
+                                                     int64_t first, Ctrl* __restrict__ ctrl, uint64_t tail_cut,
+                                                     const Ctrl* __restrict__ prev) {
     const int64_t r = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (r >= nrec) return;
+    if (prev && ctrl_abnormal(prev)) return;
     uint64_t cut = ctrl->cutoff;
     if (tail_cut < cut) cut = tail_cut;
     const int64_t off = r * stride;
@@ -472,18 +581,19 @@ __global__ __launch_bounds__(256) void k_array_apply(T* __restrict__ shard, int6
 }
 
 hipError_t launch_array_apply(int vtype, void* shard, int64_t rows, const uint8_t* base, int64_t nrec, int b_global,
-                              int64_t stride, int K, int64_t first, Ctrl* ctrl, uint64_t tail_cut, hipStream_t st) {
+                              int64_t stride, int K, int64_t first, Ctrl* ctrl, uint64_t tail_cut, const Ctrl* prev,
+                              hipStream_t st, LaunchEv ev) {
     if (nrec <= 0) return hipSuccess;
     const dim3 grid((unsigned)((nrec + 255) / 256));
     if (vtype == kF32)
-        hipLaunchKernelGGL((k_array_apply<float, false>), grid, dim3(256), 0, st, (float*)shard, rows, base, nrec,
-                           b_global, stride, K, first, ctrl, tail_cut);
+        hipExtLaunchKernelGGL((k_array_apply<float, false>), grid, dim3(256), 0, st, ev.start, ev.stop, 0,
+                              (float*)shard, rows, base, nrec, b_global, stride, K, first, ctrl, tail_cut, prev);
     else if (vtype == kI32)
-        hipLaunchKernelGGL((k_array_apply<int32_t, true>), grid, dim3(256), 0, st, (int32_t*)shard, rows, base, nrec,
-                           b_global, stride, K, first, ctrl, tail_cut);
+        hipExtLaunchKernelGGL((k_array_apply<int32_t, true>), grid, dim3(256), 0, st, ev.start, ev.stop, 0,
+                              (int32_t*)shard, rows, base, nrec, b_global, stride, K, first, ctrl, tail_cut, prev);
     else
-        hipLaunchKernelGGL((k_array_apply<double, false>), grid, dim3(256), 0, st, (double*)shard, rows, base, nrec,
-                           b_global, stride, K, first, ctrl, tail_cut);
+        hipExtLaunchKernelGGL((k_array_apply<double, false>), grid, dim3(256), 0, st, ev.start, ev.stop, 0,
+                              (double*)shard, rows, base, nrec, b_global, stride, K, first, ctrl, tail_cut, prev);
     return hipGetLastError();
 }
 

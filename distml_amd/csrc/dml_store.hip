@@ -19,6 +19,7 @@
 #include <algorithm>
 #include <cstdio>
 #include <cstring>
+#include <deque>
 #include <mutex>
 #include <string>
 #include <unordered_map>
@@ -58,17 +59,40 @@ struct Chunk {
     int nb = 0;
     int64_t max_nrec = 0;
     uint64_t tail_cut = kNoPos;
-    uint64_t tail_cut_keyok = kNoPos;  // tail errors whose record key is complete (key readable)
 };
 
 int vtype_of(const dml_desc& d) { return d.value_type; }
 
 }  // namespace
 
+// One workspace of the pipeline: [Ctrl | slot rows x kMaxW | rowflag rows].
+// Ring of kRing, at most kRing-1 chunks pending: chunk j's index reuses chunk
+// j-3's workspace, whose Ctrl chunk j-2 read as `prev` — and chunk j-2 has been
+// retired before chunk j launches.
+constexpr int kRing = 3;
+struct Workspace {
+    uint8_t* base = nullptr;
+    Ctrl* ctrl = nullptr;
+    int32_t* slot = nullptr;
+    uint32_t* rowflag = nullptr;
+    Ctrl* hctrl = nullptr;            // pinned copy of ctrl, written by the chunk's last DMA
+    hipEvent_t idx_done = nullptr;    // side stream: index of the chunk built
+    hipEvent_t kstart = nullptr;      // main stream: reduce dispatch start (in-packet timestamp)
+    hipEvent_t applied = nullptr;     // main stream: chunk applied (in-packet stop of its last kernel)
+    hipEvent_t done = nullptr;        // copy stream: ctrl copied out (chunk retired-able)
+};
+
+struct Pending {
+    Chunk c;
+    int w = 0;  // workspace index
+};
+
 struct dml_store {
     std::mutex mu;
     int device = 0;
-    hipStream_t stream = nullptr;
+    hipStream_t stream = nullptr;     // applies (reduce / scatter-add), in push order
+    hipStream_t istream = nullptr;    // key index of the next chunk, overlapping the current apply
+    hipStream_t cstream = nullptr;    // ctrl read-back, off the apply stream
     dml_desc desc{};
     uint32_t flags = 0;
     bool is_matrix = false, adagrad = false;
@@ -84,19 +108,14 @@ struct dml_store {
     int64_t cand_n = 0;
     MaxDelta* md = nullptr;
     float initial_alpha = 0.f, min_alpha = 0.f, factor = 1.5f;  // :22, :26
-    uint8_t* ws = nullptr;      // Ctrl + slot table
-    size_t ws_bytes = 0;
-    Ctrl* ctrl = nullptr;
-    int32_t* slot = nullptr;
-    Ctrl* hctrl = nullptr;      // pinned mirror
+    Workspace ws[kRing];
+    size_t slot_bytes = 0, ws_bytes = 0;
+    int next_ws = 0;
+    std::deque<Pending> pend;   // launched, not yet retired (oldest first), at most kRing-1
     // staging for host-memory pushes
     uint8_t* hstage = nullptr;
     uint8_t* dstage = nullptr;
     size_t stage_cap = 0;
-    hipEvent_t h2d_done = nullptr;
-    // pending (un-retired) chunk
-    bool pending = false;
-    Chunk pend;
     // sticky error (first failure)
     int err = 0;
     int64_t err_key = 0;
@@ -124,17 +143,23 @@ std::pair<hipEvent_t, hipEvent_t> ev_pair(dml_store* s) {
     return p;
 }
 
-// Collect elapsed times of recorded event pairs (stream must be synced).
+// Collect elapsed times of the completed event pairs (recorded in stream order:
+// stop at the first pair still in flight).
 void ev_collect(dml_store* s) {
-    for (auto& p : s->ev_used) {
+    size_t i = 0;
+    for (; i < s->ev_used.size(); ++i) {
+        auto& p = s->ev_used[i];
+        if (hipEventQuery(p.second) != hipSuccess) break;
         float ms = 0.f;
         if (hipEventElapsedTime(&ms, p.first, p.second) == hipSuccess) {
             s->timed_ms += ms;
             s->timed_n += 1;
         }
-        s->ev_free.push_back(p);
+        bool ring = false;
+        for (const Workspace& W : s->ws) ring |= p.first == W.kstart;
+        if (!ring) s->ev_free.push_back(p);
     }
-    s->ev_used.clear();
+    s->ev_used.erase(s->ev_used.begin(), s->ev_used.begin() + (std::ptrdiff_t)i);
 }
 
 int ensure_stage(dml_store* s, size_t bytes) {
@@ -153,29 +178,24 @@ int ensure_stage(dml_store* s, size_t bytes) {
 
 // Per-push record accounting: records with a complete key, and the position of
 // the first truncated access of a ragged tail (DataDesc.readInt past data.length).
-void plan_bucket(const dml_store* s, int64_t len, int gb, int64_t* nrec, uint64_t* tail_cut, bool* key_ok) {
+void plan_bucket(const dml_store* s, int64_t len, int gb, int64_t* nrec, uint64_t* tail_cut) {
     const int64_t nfull = len / s->stride, tail = len % s->stride;
     *nrec = nfull;
     *tail_cut = kNoPos;
-    *key_ok = false;
     if (tail == 0) return;
     const int64_t t0 = nfull * s->stride;
     if (s->is_matrix) {
         if (tail < s->K) {
             *tail_cut = pos_of((uint64_t)gb, (uint64_t)t0);
         } else {
-            *nrec = nfull + 1;  // key complete: the index sees it (out-of-shard key reported first)
+            *nrec = nfull + 1;  // key complete: the index sees it (an out-of-shard key is reported first)
             const int64_t nvals = (tail - s->K) / s->V;
             *tail_cut = pos_of((uint64_t)gb, (uint64_t)(t0 + s->K + nvals * s->V));
-            *key_ok = true;
         }
+    } else if (tail >= s->K + value_read_bytes(s)) {
+        *nrec = nfull + 1;  // readable record (FloatArrayStore 8-byte stride, short last slot)
     } else {
-        if (tail >= s->K + value_read_bytes(s)) {
-            *nrec = nfull + 1;  // readable record (FloatArrayStore 8-byte stride, short last slot)
-        } else {
-            *tail_cut = pos_of((uint64_t)gb, (uint64_t)t0);
-            *key_ok = tail >= s->K;
-        }
+        *tail_cut = pos_of((uint64_t)gb, (uint64_t)t0);
     }
 }
 
@@ -185,58 +205,75 @@ int reduce_mode(const dml_store* s) {
     return kAdd;
 }
 
-int launch_chunk(dml_store* s, const Chunk& c) {
-    const size_t clear = s->is_matrix ? s->ws_bytes : sizeof(Ctrl);
-    HIPCHK(hipMemsetAsync(s->ws, 0xFF, clear, s->stream));
+AdaArgs ada_args(dml_store* s) { return AdaArgs{s->alpha, s->delta, s->cand, s->initial_alpha, s->min_alpha, s->factor}; }
+
+// Apply part of a chunk on the main stream (after its index is ready), then
+// copy its Ctrl out and record `done`. `prev` = Ctrl of the chunk enqueued before.
+int launch_apply(dml_store* s, Chunk& c, Workspace& W, const Ctrl* prev) {
+    c.bt.prev = prev;
     if (s->is_matrix) {
-        HIPCHK(launch_index(c.bt, c.nb, c.max_nrec, s->stride, s->K, s->first, s->rows, s->slot, s->ctrl, s->stream));
-        std::pair<hipEvent_t, hipEvent_t> ev{};
-        if (s->timing) {
-            ev = ev_pair(s);
-            HIPCHK(hipEventRecord(ev.first, s->stream));
-        }
-        AdaArgs ada{s->alpha, s->delta, s->cand, s->initial_alpha, s->min_alpha, s->factor};
+        // start/stop timestamps ride in the dispatch packet (no marker packets between
+        // back-to-back reduces); `applied` doubles as the ctrl read-back dependency
+        LaunchEv ev{W.kstart, s->adagrad ? nullptr : W.applied};
         int64_t nblk = 0;
         HIPCHK(launch_reduce(vtype_of(s->desc), reduce_mode(s), s->data, s->rows, s->cols, c.bt, c.nb, s->stride,
-                             s->K, s->slot, s->ctrl, c.tail_cut, ada, s->stream, &nblk));
-        if (s->timing) {
-            HIPCHK(hipEventRecord(ev.second, s->stream));
-            s->ev_used.push_back(ev);
-        }
-        if (s->adagrad)
+                             s->K, W.slot, W.rowflag, W.ctrl, c.tail_cut, ada_args(s), s->stream, &nblk, ev));
+        if (s->adagrad) {
             HIPCHK(launch_maxdelta_finalize(s->cand, nblk, s->md, c.bt, c.nb, s->stride, s->K, s->V, s->stream));
+            HIPCHK(hipEventRecord(W.applied, s->stream));
+        }
+        if (s->timing) s->ev_used.emplace_back(W.kstart, W.applied);
     } else {
-        HIPCHK(launch_array_validate(c.bt, c.nb, c.max_nrec, s->stride, s->K, s->first, s->rows, s->ctrl, s->stream));
         for (int b = 0; b < c.nb; ++b) {
-            std::pair<hipEvent_t, hipEvent_t> ev{};
+            LaunchEv ev{};
             if (s->timing) {
-                ev = ev_pair(s);
-                HIPCHK(hipEventRecord(ev.first, s->stream));
+                auto p = ev_pair(s);
+                ev = {p.first, p.second};
+                s->ev_used.push_back(p);
             }
             HIPCHK(launch_array_apply(vtype_of(s->desc), s->data, s->rows, c.bt.base[b], c.bt.nrec[b], c.bt.bidx[b],
-                                      s->stride, s->K, s->first, s->ctrl, c.tail_cut, s->stream));
-            if (s->timing) {
-                HIPCHK(hipEventRecord(ev.second, s->stream));
-                s->ev_used.push_back(ev);
-            }
+                                      s->stride, s->K, s->first, W.ctrl, c.tail_cut, prev, s->stream, ev));
         }
+        HIPCHK(hipEventRecord(W.applied, s->stream));
     }
+    // ctrl read-back on its own stream, so the next chunk's apply follows this one directly
+    HIPCHK(hipStreamWaitEvent(s->cstream, W.applied, 0));
+    HIPCHK(hipMemcpyAsync(W.hctrl, W.ctrl, sizeof(Ctrl), hipMemcpyDeviceToHost, s->cstream));
+    HIPCHK(hipEventRecord(W.done, s->cstream));
     return DML_OK;
 }
 
-int read_ctrl(dml_store* s, Ctrl* out) {
-    HIPCHK(hipMemcpyAsync(s->hctrl, s->ctrl, sizeof(Ctrl), hipMemcpyDeviceToHost, s->stream));
+// Index on the side stream (overlaps the previous chunk's apply), then apply.
+int launch_chunk(dml_store* s, Chunk& c, Workspace& W, const Ctrl* prev) {
+    HIPCHK(hipMemsetAsync(W.base, 0xFF, sizeof(Ctrl) + s->slot_bytes, s->istream));
+    if (s->is_matrix) {
+        HIPCHK(hipMemsetAsync(W.rowflag, 0, (size_t)s->rows * sizeof(uint32_t), s->istream));
+        HIPCHK(launch_index(c.bt, c.nb, c.max_nrec, s->stride, s->K, s->first, s->rows, W.slot, W.rowflag, W.ctrl,
+                            c.tail_cut, s->istream));
+    } else {
+        HIPCHK(launch_array_validate(c.bt, c.nb, c.max_nrec, s->stride, s->K, s->first, s->rows, W.ctrl, c.tail_cut,
+                                     s->istream));
+    }
+    HIPCHK(hipEventRecord(W.idx_done, s->istream));
+    HIPCHK(hipStreamWaitEvent(s->stream, W.idx_done, 0));
+    return launch_apply(s, c, W, prev);
+}
+
+int read_ctrl(dml_store* s, Workspace& W, Ctrl* out) {
+    HIPCHK(hipMemcpyAsync(W.hctrl, W.ctrl, sizeof(Ctrl), hipMemcpyDeviceToHost, s->stream));
     HIPCHK(hipStreamSynchronize(s->stream));
-    *out = *s->hctrl;
+    *out = *W.hctrl;
     return DML_OK;
 }
 
-// Exact replay of a chunk in which some push lists a row twice: split each push
-// into layers (k-th occurrence of each row), apply layers in (push, layer)
-// order. Per element the adds keep their reference order.
-int replay_layers(dml_store* s, const Chunk& c, Ctrl* ctl) {
-    std::vector<Chunk> vchunks(1);
-    std::vector<std::vector<int32_t>> vslots;  // per virtual column: (row, record) pairs flattened
+// Exact replay of the rows some push lists twice (rowflag set; the reduce left
+// them untouched): split each push into layers (k-th occurrence of each flagged
+// row) and apply layers in (push, layer) order, so per element the adds keep
+// their reference order. Other rows are final already (rows are independent).
+int replay_rows(dml_store* s, const Chunk& c, Workspace& W, Ctrl* ctl) {
+    std::vector<uint32_t> flag((size_t)s->rows);
+    HIPCHK(hipMemcpyAsync(flag.data(), W.rowflag, flag.size() * sizeof(uint32_t), hipMemcpyDeviceToHost, s->stream));
+    HIPCHK(hipStreamSynchronize(s->stream));
     struct VCol { int src_b; std::vector<std::pair<int32_t, int32_t>> rr; };
     std::vector<VCol> cols;
     int32_t* drows = nullptr;
@@ -255,7 +292,7 @@ int replay_layers(dml_store* s, const Chunk& c, Ctrl* ctl) {
         std::vector<VCol> layers;
         for (int64_t r = 0; r < n; ++r) {
             const int32_t row = hrows[(size_t)r];
-            if (row < 0) continue;  // out of shard: cutoff already covers it
+            if (row < 0 || !flag[(size_t)row]) continue;  // out of shard (cutoff covers it) or already applied
             const int32_t l = occ[row]++;
             if ((int)layers.size() <= l) layers.push_back(VCol{b, {}});
             layers[(size_t)l].rr.emplace_back(row, (int32_t)r);
@@ -263,18 +300,11 @@ int replay_layers(dml_store* s, const Chunk& c, Ctrl* ctl) {
         for (auto& L : layers) cols.push_back(std::move(L));
     }
     (void)hipFree(drows);
-    // ctrl keeps the key-error cutoff of the first pass; clear neg/no_dup.
-    Ctrl init = *ctl;
-    init.neg_pos = kNoPos;
-    init.no_dup = 0xFFFFFFFFu;
-    HIPCHK(hipMemcpy(s->ctrl, &init, sizeof(Ctrl), hipMemcpyHostToDevice));
     std::vector<int32_t> hslot((size_t)s->rows * kMaxW);
-    AdaArgs ada{s->alpha, s->delta, s->cand, s->initial_alpha, s->min_alpha, s->factor};
-    std::vector<Chunk> done;
-    for (size_t v0 = 0; v0 < cols.size(); v0 += kMaxW) {
-        Chunk vc;
+    auto upload = [&](size_t v0, Chunk& vc) -> int {
         vc.nb = (int)std::min<size_t>(kMaxW, cols.size() - v0);
         vc.tail_cut = c.tail_cut;
+        vc.bt.prev = nullptr;
         std::fill(hslot.begin(), hslot.end(), -1);
         for (int j = 0; j < vc.nb; ++j) {
             const VCol& col = cols[v0 + (size_t)j];
@@ -284,29 +314,38 @@ int replay_layers(dml_store* s, const Chunk& c, Ctrl* ctl) {
             vc.bt.bidx[j] = c.bt.bidx[col.src_b];
             for (auto& pr : col.rr) hslot[(size_t)pr.first * kMaxW + (size_t)j] = pr.second;
         }
-        HIPCHK(hipMemcpy(s->slot, hslot.data(), hslot.size() * sizeof(int32_t), hipMemcpyHostToDevice));
+        HIPCHK(hipMemcpy(W.slot, hslot.data(), hslot.size() * sizeof(int32_t), hipMemcpyHostToDevice));
+        return DML_OK;
+    };
+    for (size_t v0 = 0; v0 < cols.size(); v0 += kMaxW) {
+        Chunk vc;
+        if (int rc = upload(v0, vc)) return rc;
         int64_t nblk = 0;
         HIPCHK(launch_reduce(vtype_of(s->desc), reduce_mode(s), s->data, s->rows, s->cols, vc.bt, vc.nb, s->stride,
-                             s->K, s->slot, s->ctrl, vc.tail_cut, ada, s->stream, &nblk));
+                             s->K, W.slot, nullptr, W.ctrl, vc.tail_cut, ada_args(s), s->stream, &nblk));
         if (s->adagrad)
             HIPCHK(launch_maxdelta_finalize(s->cand, nblk, s->md, vc.bt, vc.nb, s->stride, s->K, s->V, s->stream));
         HIPCHK(hipStreamSynchronize(s->stream));
-        done.push_back(vc);
     }
-    int rc = read_ctrl(s, ctl);
-    if (rc) return rc;
+    if (int rc = read_ctrl(s, W, ctl)) return rc;
     if (ctl->neg_pos != kNoPos) {
-        // undo every add after the first negative, across all layers
-        for (auto& vc : done) {
-            std::fill(hslot.begin(), hslot.end(), -1);
-            size_t v0 = (size_t)(&vc - &done[0]) * kMaxW;
-            for (int j = 0; j < vc.nb; ++j)
-                for (auto& pr : cols[v0 + (size_t)j].rr) hslot[(size_t)pr.first * kMaxW + (size_t)j] = pr.second;
-            HIPCHK(hipMemcpy(s->slot, hslot.data(), hslot.size() * sizeof(int32_t), hipMemcpyHostToDevice));
-            HIPCHK(launch_rollback_i32((int32_t*)s->data, s->rows, s->cols, vc.bt, vc.nb, s->stride, s->K, s->slot,
-                                       s->ctrl, vc.tail_cut, s->stream));
+        // undo every add after the first negative: the unflagged rows (rebuilt slot
+        // table of the chunk) and every layer of the replayed rows
+        Chunk mc = c;
+        mc.bt.prev = nullptr;
+        HIPCHK(hipMemsetAsync(W.slot, 0xFF, s->slot_bytes, s->stream));
+        HIPCHK(launch_index(mc.bt, mc.nb, mc.max_nrec, s->stride, s->K, s->first, s->rows, W.slot, W.rowflag, W.ctrl,
+                            kNoPos, s->stream));
+        HIPCHK(launch_rollback_i32((int32_t*)s->data, s->rows, s->cols, mc.bt, mc.nb, s->stride, s->K, W.slot,
+                                   W.rowflag, W.ctrl, mc.tail_cut, s->stream));
+        for (size_t v0 = 0; v0 < cols.size(); v0 += kMaxW) {
+            Chunk vc;
             HIPCHK(hipStreamSynchronize(s->stream));
+            if (int rc = upload(v0, vc)) return rc;
+            HIPCHK(launch_rollback_i32((int32_t*)s->data, s->rows, s->cols, vc.bt, vc.nb, s->stride, s->K, W.slot,
+                                       nullptr, W.ctrl, vc.tail_cut, s->stream));
         }
+        HIPCHK(hipStreamSynchronize(s->stream));
     }
     return DML_OK;
 }
@@ -343,26 +382,33 @@ int record_error(dml_store* s, int code, int64_t key, int32_t col) {
     return set_err(code, buf);
 }
 
-// Retire the pending chunk: see file header.
-int retire(dml_store* s) {
-    if (!s->pending) return DML_OK;
-    s->pending = false;
-    const Chunk& c = s->pend;
-    Ctrl ctl;
-    int rc = read_ctrl(s, &ctl);
-    if (rc) return rc;
+// Turn the oldest pending chunk's Ctrl into final state + status: replay rows a
+// push repeats, undo int32 adds past the first negative counter, map the first
+// failing position to (code, key, col). If it ended abnormally, the chunk queued
+// after it ran as a no-op: relaunch it (replay only) or drop it (error: the
+// reference's PS loop has ended, PSAgent.java:188-191).
+int retire_front(dml_store* s) {
+    if (s->pend.empty()) return DML_OK;
+    Pending p = s->pend.front();
+    s->pend.pop_front();
+    Workspace& W = s->ws[p.w];
+    const Chunk& c = p.c;
+    HIPCHK(hipEventSynchronize(W.done));
+    Ctrl ctl = *W.hctrl;
     if (s->timing) ev_collect(s);
+    const bool abnormal = ctrl_abnormal(&ctl);
+    int rc = DML_OK;
     if (s->is_matrix && ctl.no_dup == 0u) {
-        rc = replay_layers(s, c, &ctl);
+        rc = replay_rows(s, c, W, &ctl);
         if (rc) return rc;
     } else if (ctl.neg_pos != kNoPos) {
         if (s->is_matrix) {
-            HIPCHK(launch_rollback_i32((int32_t*)s->data, s->rows, s->cols, c.bt, c.nb, s->stride, s->K, s->slot,
-                                       s->ctrl, c.tail_cut, s->stream));
+            HIPCHK(launch_rollback_i32((int32_t*)s->data, s->rows, s->cols, c.bt, c.nb, s->stride, s->K, W.slot,
+                                       W.rowflag, W.ctrl, c.tail_cut, s->stream));
         } else {
             for (int b = 0; b < c.nb; ++b)
                 HIPCHK(launch_array_rollback_i32((int32_t*)s->data, s->rows, c.bt.base[b], c.bt.nrec[b], c.bt.bidx[b],
-                                                 s->stride, s->K, s->first, s->ctrl, c.tail_cut, s->stream));
+                                                 s->stride, s->K, s->first, W.ctrl, c.tail_cut, s->stream));
         }
         HIPCHK(hipStreamSynchronize(s->stream));
     }
@@ -372,42 +418,60 @@ int retire(dml_store* s) {
         const int64_t off = (int64_t)(ctl.neg_pos & kOffMask);
         const int64_t r = off / s->stride;
         const int32_t col = s->is_matrix ? (int32_t)((off - r * s->stride - s->K) / s->V) : -1;
-        return record_error(s, DML_E_NEGATIVE_COUNTER, read_key_at(s, base_of(c, gb) + r * s->stride), col);
-    }
-    if (cut != kNoPos) {
+        rc = record_error(s, DML_E_NEGATIVE_COUNTER, read_key_at(s, base_of(c, gb) + r * s->stride), col);
+    } else if (cut != kNoPos) {
         const int gb = (int)(cut >> 40);
         const int64_t off = (int64_t)(cut & kOffMask);
         const int64_t r = off / s->stride;
         const uint8_t* rec = base_of(c, gb) + r * s->stride;
-        if (ctl.cutoff <= c.tail_cut) return record_error(s, DML_E_KEY_OUT_OF_SHARD, read_key_at(s, rec), -1);
-        // truncated: the key is known when the record's key bytes were complete
-        int64_t len = 0;
-        for (int b = 0; b < c.nb; ++b)
-            if (c.bt.bidx[b] == gb) len = c.bt.len[b];
-        const bool key_ok = len - r * s->stride >= s->K;
-        int32_t col = -1;
-        if (s->is_matrix && key_ok) col = (int32_t)((off - r * s->stride - s->K) / s->V);
-        return record_error(s, DML_E_TRUNCATED, key_ok ? read_key_at(s, rec) : 0, col);
+        if (ctl.cutoff < c.tail_cut) {
+            rc = record_error(s, DML_E_KEY_OUT_OF_SHARD, read_key_at(s, rec), -1);
+        } else {
+            // truncated: the key is known when the record's key bytes were complete
+            int64_t len = 0;
+            for (int b = 0; b < c.nb; ++b)
+                if (c.bt.bidx[b] == gb) len = c.bt.len[b];
+            const bool key_ok = len - r * s->stride >= s->K;
+            int32_t col = -1;
+            if (s->is_matrix && key_ok) col = (int32_t)((off - r * s->stride - s->K) / s->V);
+            rc = record_error(s, DML_E_TRUNCATED, key_ok ? read_key_at(s, rec) : 0, col);
+        }
+    }
+    if (abnormal && !s->pend.empty()) {
+        if (rc != DML_OK) {
+            for (auto& q : s->pend) (void)hipEventSynchronize(s->ws[q.w].done);
+            s->pend.clear();  // their kernels were no-ops; the store stops here like the reference
+        } else {
+            Pending& q = s->pend.front();  // relaunch its apply; its index is still valid
+            HIPCHK(hipEventSynchronize(s->ws[q.w].done));
+            if (int r2 = launch_apply(s, q.c, s->ws[q.w], nullptr)) return r2;
+        }
+    }
+    return rc;
+}
+
+int retire_all(dml_store* s) {
+    while (!s->pend.empty()) {
+        int rc = retire_front(s);
+        if (rc) {
+            s->pend.clear();
+            return rc;
+        }
     }
     return DML_OK;
 }
 
-// Run `n` device-resident pushes (global indices b0..b0+n-1) as ordered chunks.
-// The last chunk stays pending (retired by the caller or a later call).
+// Run `n` device-resident pushes (global indices 0..n-1) as ordered chunks of
+// <= kMaxW; up to two chunks stay in flight (retired later, in order).
 int run_batch(dml_store* s, const uint8_t* const* dptr, const int64_t* lens, int n) {
     for (int c0 = 0; c0 < n; c0 += kMaxW) {
-        if (s->pending) {
-            int rc = retire(s);
-            if (rc) return rc;
-        }
         Chunk c;
         c.nb = std::min(kMaxW, n - c0);
         for (int j = 0; j < c.nb; ++j) {
             const int gb = c0 + j;
             int64_t nrec;
             uint64_t tcut;
-            bool key_ok;
-            plan_bucket(s, lens[gb], gb, &nrec, &tcut, &key_ok);
+            plan_bucket(s, lens[gb], gb, &nrec, &tcut);
             c.bt.base[j] = dptr[gb];
             c.bt.len[j] = lens[gb];
             c.bt.nrec[j] = nrec;
@@ -416,10 +480,19 @@ int run_batch(dml_store* s, const uint8_t* const* dptr, const int64_t* lens, int
             c.tail_cut = std::min(c.tail_cut, tcut);
         }
         if (c.max_nrec == 0 && c.tail_cut == kNoPos) continue;  // empty pushes: nothing to apply
-        int rc = launch_chunk(s, c);
+        while ((int)s->pend.size() >= kRing - 1) {  // see Workspace
+            int rc = retire_front(s);
+            if (rc) { s->pend.clear(); return rc; }
+        }
+        if (s->err) return set_err(s->err, "store is in a failed state (see dml_store_error_state)");
+        const Ctrl* prev = s->pend.empty() ? nullptr : s->ws[s->pend.back().w].ctrl;
+        Pending p;
+        p.c = c;
+        p.w = s->next_ws;
+        s->next_ws = (s->next_ws + 1) % kRing;
+        int rc = launch_chunk(s, p.c, s->ws[p.w], prev);
         if (rc) return rc;
-        s->pend = c;
-        s->pending = true;
+        s->pend.push_back(p);
     }
     return DML_OK;
 }
@@ -429,14 +502,9 @@ int check_store(dml_store* s) {
     return DML_OK;
 }
 
-// Entry check shared by every mutating/reading call: retire pending work and
-// refuse to run once the store has failed (the reference's PSAgent loop ends
-// with the exception, PSAgent.java:188-191).
-int begin_call(dml_store* s) {
-    int rc = retire(s);
-    if (rc) return rc;
-    return DML_OK;
-}
+// Entry of every reading / non-push call: all accepted pushes applied and
+// checked (read-your-writes).
+int begin_call(dml_store* s) { return retire_all(s); }
 
 }  // namespace
 
@@ -520,12 +588,21 @@ int dml_store_create_range(const dml_desc* desc, int64_t first_key, int64_t last
         if ((e = hipMalloc((void**)&s->md, sizeof(MaxDelta))) != hipSuccess) return fail(e, "md alloc");
         if ((e = hipMemsetAsync(s->md, 0, sizeof(MaxDelta), s->stream)) != hipSuccess) return fail(e, "md zero");
     }
-    s->ws_bytes = sizeof(Ctrl) + (s->is_matrix ? (size_t)rows * kMaxW * sizeof(int32_t) : 0);
-    if ((e = hipMalloc((void**)&s->ws, s->ws_bytes)) != hipSuccess) return fail(e, "workspace alloc");
-    s->ctrl = (Ctrl*)s->ws;
-    s->slot = (int32_t*)(s->ws + sizeof(Ctrl));
-    if ((e = hipHostMalloc((void**)&s->hctrl, sizeof(Ctrl), hipHostMallocDefault)) != hipSuccess) return fail(e, "ctrl");
-    if ((e = hipEventCreateWithFlags(&s->h2d_done, hipEventDisableTiming)) != hipSuccess) return fail(e, "event");
+    s->slot_bytes = s->is_matrix ? (size_t)rows * kMaxW * sizeof(int32_t) : 0;
+    s->ws_bytes = sizeof(Ctrl) + s->slot_bytes + (s->is_matrix ? (size_t)rows * sizeof(uint32_t) : 0);
+    if ((e = hipStreamCreateWithFlags(&s->istream, hipStreamNonBlocking)) != hipSuccess) return fail(e, "index stream");
+    if ((e = hipStreamCreateWithFlags(&s->cstream, hipStreamNonBlocking)) != hipSuccess) return fail(e, "copy stream");
+    for (Workspace& W : s->ws) {
+        if ((e = hipMalloc((void**)&W.base, s->ws_bytes)) != hipSuccess) return fail(e, "workspace alloc");
+        W.ctrl = (Ctrl*)W.base;
+        W.slot = (int32_t*)(W.base + sizeof(Ctrl));
+        W.rowflag = (uint32_t*)(W.base + sizeof(Ctrl) + s->slot_bytes);
+        if ((e = hipHostMalloc((void**)&W.hctrl, sizeof(Ctrl), hipHostMallocDefault)) != hipSuccess) return fail(e, "ctrl");
+        if ((e = hipEventCreateWithFlags(&W.idx_done, hipEventDisableTiming)) != hipSuccess) return fail(e, "event");
+        if ((e = hipEventCreateWithFlags(&W.done, hipEventDisableTiming)) != hipSuccess) return fail(e, "event");
+        if ((e = hipEventCreate(&W.applied)) != hipSuccess) return fail(e, "event");
+        if ((e = hipEventCreate(&W.kstart)) != hipSuccess) return fail(e, "event");
+    }
     if ((e = hipStreamSynchronize(s->stream)) != hipSuccess) return fail(e, "init sync");
     *out = s;
     return DML_OK;
@@ -537,19 +614,32 @@ void dml_store_destroy(dml_store* s) {
         std::lock_guard<std::mutex> lk(s->mu);
         DeviceGuard g(s->device);
         if (s->stream) (void)hipStreamSynchronize(s->stream);
-        for (auto& p : s->ev_used) { (void)hipEventDestroy(p.first); (void)hipEventDestroy(p.second); }
+        if (s->istream) (void)hipStreamSynchronize(s->istream);
+        if (s->cstream) (void)hipStreamSynchronize(s->cstream);
+        for (auto& p : s->ev_used) {
+            bool ring = false;
+            for (const Workspace& W : s->ws) ring |= p.first == W.kstart;
+            if (!ring) { (void)hipEventDestroy(p.first); (void)hipEventDestroy(p.second); }
+        }
         for (auto& p : s->ev_free) { (void)hipEventDestroy(p.first); (void)hipEventDestroy(p.second); }
-        if (s->h2d_done) (void)hipEventDestroy(s->h2d_done);
+        for (Workspace& W : s->ws) {
+            (void)hipFree(W.base);
+            if (W.hctrl) (void)hipHostFree(W.hctrl);
+            if (W.idx_done) (void)hipEventDestroy(W.idx_done);
+            if (W.done) (void)hipEventDestroy(W.done);
+            if (W.applied) (void)hipEventDestroy(W.applied);
+            if (W.kstart) (void)hipEventDestroy(W.kstart);
+        }
         (void)hipFree(s->data);
         (void)hipFree(s->alpha);
         (void)hipFree(s->delta);
         (void)hipFree(s->cand);
         (void)hipFree(s->md);
-        (void)hipFree(s->ws);
         (void)hipFree(s->dstage);
         if (s->hstage) (void)hipHostFree(s->hstage);
-        if (s->hctrl) (void)hipHostFree(s->hctrl);
         if (s->stream) (void)hipStreamDestroy(s->stream);
+        if (s->istream) (void)hipStreamDestroy(s->istream);
+        if (s->cstream) (void)hipStreamDestroy(s->cstream);
     }
     delete s;
 }
@@ -571,12 +661,13 @@ static int push_host(dml_store* s, const uint8_t* const* bufs, const int64_t* le
     // Stage: pageable -> pinned (CPU copy) -> HBM (one async DMA).
     for (int32_t i = 0; i < n; ++i)
         if (lens[i] > 0) std::memcpy(s->hstage + offs[(size_t)i], bufs[i], (size_t)lens[i]);
-    if (total > 0) HIPCHK(hipMemcpyAsync(s->dstage, s->hstage, total, hipMemcpyHostToDevice, s->stream));
+    // on the index stream: the index reads the staged bytes first, the apply waits for the index
+    if (total > 0) HIPCHK(hipMemcpyAsync(s->dstage, s->hstage, total, hipMemcpyHostToDevice, s->istream));
     std::vector<const uint8_t*> dptr((size_t)n);
     for (int32_t i = 0; i < n; ++i) dptr[(size_t)i] = s->dstage + offs[(size_t)i];
     rc = run_batch(s, dptr.data(), lens, n);
     if (rc) return rc;
-    if (!(s->flags & DML_FLAG_ASYNC)) return retire(s);
+    if (!(s->flags & DML_FLAG_ASYNC)) return retire_all(s);
     // async: the caller's bytes are already copied into pinned staging.
     return DML_OK;
 }
@@ -601,8 +692,7 @@ int dml_store_push_batch_device(dml_store* s, const void* const* dev_bufs, const
     std::lock_guard<std::mutex> lk(s->mu);
     DeviceGuard g(s->device);
     if (n < 0 || (n > 0 && (!dev_bufs || !lens))) return set_err(DML_E_INVALID_ARG, "bad push arguments");
-    int rc = begin_call(s);
-    if (rc) return rc;
+    // no retire-all here: run_batch keeps up to kRing-1 chunks in flight
     if (s->err) return set_err(s->err, "store is in a failed state (see dml_store_error_state)");
     for (int32_t i = 0; i < n; ++i)
         if (lens[i] < 0 || (lens[i] > 0 && !dev_bufs[i])) return set_err(DML_E_INVALID_ARG, "bad push buffer");
@@ -613,7 +703,7 @@ int dml_store_flush(dml_store* s) {
     if (int rc = check_store(s)) return rc;
     std::lock_guard<std::mutex> lk(s->mu);
     DeviceGuard g(s->device);
-    int rc = retire(s);
+    int rc = retire_all(s);
     if (rc) return rc;
     HIPCHK(hipStreamSynchronize(s->stream));
     return DML_OK;
@@ -880,11 +970,28 @@ int dml_reduce_buckets_dense(const dml_desc* desc, int64_t first_key, int64_t ro
     const int K = desc->key_type == 0 ? 4 : 8, V = vt == 3 ? 8 : 4;
     const int64_t stride = K + (int64_t)V * cols;
     hipStream_t st = (hipStream_t)stream;
-    uint8_t* ws = nullptr;
-    const size_t wsb = sizeof(Ctrl) + (size_t)rows * kMaxW * sizeof(int32_t);
-    HIPCHK(hipMallocAsync((void**)&ws, wsb, st));
+    const size_t sb = (size_t)rows * kMaxW * sizeof(int32_t);
+    const size_t wsb = sizeof(Ctrl) + sb + (size_t)rows * sizeof(uint32_t);
+    // per-device cached workspace (grown on demand; calls on one device serialize on it)
+    static std::mutex ws_mu;
+    static std::unordered_map<int, std::pair<uint8_t*, size_t>> ws_cache;
+    int dev = 0;
+    HIPCHK(hipGetDevice(&dev));
+    std::lock_guard<std::mutex> wlk(ws_mu);
+    auto& slot_ws = ws_cache[dev];
+    if (slot_ws.second < wsb) {
+        if (slot_ws.first) {
+            HIPCHK(hipDeviceSynchronize());
+            (void)hipFree(slot_ws.first);
+        }
+        slot_ws = {nullptr, 0};
+        HIPCHK(hipMalloc((void**)&slot_ws.first, wsb));
+        slot_ws.second = wsb;
+    }
+    uint8_t* ws = slot_ws.first;
     Ctrl* ctrl = (Ctrl*)ws;
     int32_t* slot = (int32_t*)(ws + sizeof(Ctrl));
+    uint32_t* rflag = (uint32_t*)(ws + sizeof(Ctrl) + sb);
     AdaArgs none{};
     int rc = DML_OK;
     for (int c0 = 0; c0 < std::max(n, 1) && rc == DML_OK; c0 += kMaxW) {
@@ -900,11 +1007,12 @@ int dml_reduce_buckets_dense(const dml_desc* desc, int64_t first_key, int64_t ro
             max_nrec = std::max(max_nrec, bt.nrec[j]);
         }
         if (rc) break;
-        hipError_t e = hipMemsetAsync(ws, 0xFF, wsb, st);
-        if (e == hipSuccess) e = launch_index(bt, nb, max_nrec, stride, K, first_key, rows, slot, ctrl, st);
+        hipError_t e = hipMemsetAsync(ws, 0xFF, sizeof(Ctrl) + sb, st);
+        if (e == hipSuccess) e = hipMemsetAsync(rflag, 0, (size_t)rows * sizeof(uint32_t), st);
+        if (e == hipSuccess) e = launch_index(bt, nb, max_nrec, stride, K, first_key, rows, slot, rflag, ctrl, kNoPos, st);
         if (e == hipSuccess)
-            e = launch_reduce(vt, c0 == 0 ? kPreReduce : kAdd, dev_out, rows, cols, bt, nb, stride, K, slot, ctrl,
-                              kNoPos, none, st, nullptr);
+            e = launch_reduce(vt, c0 == 0 ? kPreReduce : kAdd, dev_out, rows, cols, bt, nb, stride, K, slot, nullptr,
+                              ctrl, kNoPos, none, st, nullptr);
         Ctrl h;
         if (e == hipSuccess) e = hipMemcpyAsync(&h, ctrl, sizeof h, hipMemcpyDeviceToHost, st);
         if (e == hipSuccess) e = hipStreamSynchronize(st);
@@ -913,7 +1021,6 @@ int dml_reduce_buckets_dense(const dml_desc* desc, int64_t first_key, int64_t ro
         else if (h.no_dup == 0u) rc = set_err(DML_E_UNSUPPORTED, "pre-reduce: a bucket repeats a row");
         if (n == 0) break;
     }
-    (void)hipFreeAsync(ws, st);
     return rc;
 }
 

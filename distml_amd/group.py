@@ -1,0 +1,90 @@
+"""Multi-GPU shard group: one process per GPU, RCCL over xGMI via torch.distributed.
+
+The matrix's rows are split by KeyRange.linearSplit (KeyRange.java:68-80,
+DMatrix.partition DMatrix.java:53-64); rank r owns shard r in HBM.
+
+Path for device-resident FULL-RANGE pushes (every push covers all rows — the
+data-parallel gradient case):
+  1. pre-reduce: the rank's W local pushes, in push order, into one partial
+     buffer of the whole matrix (dml_reduce_buckets_dense, HBM-bound);
+  2. reduce-scatter (sum) of the partials: rank r receives the sum of every
+     rank's partial for its shard (RCCL ncclReduceScatter over xGMI);
+  3. owner apply: shard += received (dml_store_apply_dense_device).
+fp32 results differ from the single-shard ordered sum only by summation order
+(bound stated in tests/test_group_gloo.py); int32 is exact.
+
+Pushes that are already split per shard (SparseMatrix.push splits by partition,
+SparseMatrix.java:124-138) need no exchange: push_local() applies them on the
+owner with the exact ordered reduce.
+"""
+from __future__ import annotations
+
+import ctypes as C
+from typing import List, Optional, Sequence
+
+from . import _lib
+from .datadesc import DataDesc, KeyRange
+from .store import DataStore, check
+
+
+class HipOps:
+    """Product kernels (libdistml_ps). Tests may inject CPU stand-ins with the same methods."""
+
+    def prereduce(self, fmt: DataDesc, first: int, rows: int, cols: int, dev_ptrs: Sequence[int],
+                  lens: Sequence[int], out_ptr: int, stream: int) -> None:
+        n = len(dev_ptrs)
+        ptrs = (C.c_void_p * max(n, 1))(*dev_ptrs)
+        ls = (C.c_int64 * max(n, 1))(*lens)
+        rc = _lib.load().dml_reduce_buckets_dense(C.byref(fmt.to_c()), first, rows, cols, ptrs, ls, n,
+                                                   C.c_void_p(out_ptr), C.c_void_p(stream))
+        check(rc)
+
+    def apply(self, store: DataStore, src_ptr: int, elems: int) -> None:
+        check(_lib.load().dml_store_apply_dense_device(store._h, C.c_void_p(src_ptr), elems), store)
+
+
+class ShardGroup:
+    def __init__(self, fmt: DataDesc, total_rows: int, cols: int, rank: int, world: int,
+                 device: Optional[int] = None, ops=None, store_factory=None):
+        import torch
+        import torch.distributed as dist
+        self.torch, self.dist = torch, dist
+        self.fmt, self.cols, self.rank, self.world = fmt, cols, rank, world
+        self.parts: List[KeyRange] = KeyRange(0, total_rows - 1).linearSplit(world)
+        self.shard = self.parts[rank]
+        self.step_rows = self.parts[0].size()  # linearSplit step: equal padded chunk per rank
+        self.total_rows = total_rows
+        self.device = device
+        self.ops = ops or HipOps()
+        self.store = (store_factory or (lambda: DataStore(fmt, self.shard, cols, device=device)))()
+        self.dtype = {0: torch.int32, 1: torch.float32, 3: torch.float64}[fmt.valueType]
+        dev = torch.device("cuda", device) if device is not None else torch.device("cpu")
+        self.partial = torch.empty(world * self.step_rows * cols, dtype=self.dtype, device=dev)
+        self.recv = torch.empty(self.step_rows * cols, dtype=self.dtype, device=dev)
+
+    def push_full_range(self, dev_ptrs: Sequence[int], lens: Sequence[int], stream: int = 0) -> None:
+        """Ordered local pre-reduce -> reduce-scatter -> owner apply (see module doc)."""
+        torch, dist = self.torch, self.dist
+        # rows past the matrix end (linearSplit's last shard may be short) stay zero
+        self.ops.prereduce(self.fmt, 0, self.total_rows, self.cols, dev_ptrs, lens,
+                           self.partial.data_ptr(), stream)
+        if self.world > 1:
+            if dist.get_backend() == "gloo":
+                dist.all_reduce(self.partial)  # gloo: no reduce_scatter for CPU tensors
+                lo = self.rank * self.step_rows * self.cols
+                self.recv.copy_(self.partial[lo:lo + self.step_rows * self.cols])
+            else:
+                dist.reduce_scatter_tensor(self.recv, self.partial)
+        else:
+            self.recv.copy_(self.partial[: self.step_rows * self.cols])
+        if self.recv.is_cuda:
+            torch.cuda.current_stream().synchronize()
+        n = self.shard.size() * self.cols
+        self.ops.apply(self.store, self.recv.data_ptr(), n)
+
+    def push_local(self, dev_ptrs: Sequence[int], lens: Sequence[int]) -> None:
+        """Pushes already split to this shard: exact ordered apply, no exchange."""
+        self.store.pushDevice(dev_ptrs, lens)
+
+    def flush(self):
+        self.store.flush()

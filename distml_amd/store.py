@@ -144,12 +144,12 @@ class DataStore:
         lens = (C.c_int64 * n)(*[len(b) for b in bufs])
         check(_lib.load().dml_store_push_batch(self._h, ptrs, lens, n), self)
 
-    def pushDevice(self, dev_ptrs: Sequence[int], lens: Sequence[int]):
-        """Device-resident pushes (pointers on this store's device), applied in order."""
-        n = len(dev_ptrs)
-        ptrs = (C.c_void_p * n)(*dev_ptrs)
-        ls = (C.c_int64 * n)(*lens)
-        check(_lib.load().dml_store_push_batch_device(self._h, ptrs, ls, n), self)
+    def pushDevice(self, dev_ptrs, lens=None):
+        """Device-resident pushes (pointers on this store's device), applied in order,
+        asynchronously: a deferred error surfaces at a later call or flush().
+        `dev_ptrs` may be a DeviceBatch (prebuilt argument arrays)."""
+        b = dev_ptrs if isinstance(dev_ptrs, DeviceBatch) else DeviceBatch(dev_ptrs, lens)
+        check(_lib.load().dml_store_push_batch_device(self._h, b.ptrs, b.lens, b.n), self)
 
     def flush(self):
         check(_lib.load().dml_store_flush(self._h), self)
@@ -287,6 +287,15 @@ class DataStore:
     @staticmethod
     def createStores(model, serverIndex: int, device: Optional[int] = None):
         return {name: DataStore.createStore(serverIndex, m, device) for name, m in model.dataMap.items()}
+
+
+class DeviceBatch:
+    """ctypes argument arrays for a list of device-resident pushes (built once, reusable)."""
+
+    def __init__(self, dev_ptrs: Sequence[int], lens: Sequence[int]):
+        self.n = len(dev_ptrs)
+        self.ptrs = (C.c_void_p * max(self.n, 1))(*dev_ptrs)
+        self.lens = (C.c_int64 * max(self.n, 1))(*lens)
 
 
 class DMatrix:

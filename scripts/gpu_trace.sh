@@ -1,0 +1,8 @@
+set -e
+R=$GRAFT_REPO_ROOT
+export TMPDIR=/tmp
+cd $R
+timeout -k 10 600 python -m pytest tests -m gpu -x -q -p no:cacheprovider > gpurun_out/gpu_tests.log 2>&1 || { tail -40 gpurun_out/gpu_tests.log; exit 1; }
+tail -2 gpurun_out/gpu_tests.log
+timeout -k 10 300 rocprofv3 --kernel-trace -d $R/gpurun_out/trace_async -o run --output-format csv -- python3 bench.py --steps 10 --warmup 2 --no-cpu > gpurun_out/trace_async.log 2>&1
+timeout -k 10 300 python bench.py --no-cpu

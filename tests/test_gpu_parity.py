@@ -199,6 +199,56 @@ def test_batch_error_state_matches_sequential(oracle, kind):
         s.close()
 
 
+@pytest.mark.parametrize("middle", ["normal", "dup", "key", "neg"])
+def test_pipelined_batches(oracle, middle):
+    """Several device batches in flight (no flush between them): a repeated row in
+    the middle batch is replayed and the next batch relaunched; an error stops the
+    store there (later batches never applied), surfacing at a later call."""
+    from distml_amd import DataDesc, DistMLException, encode_matrix_push
+    rng = np.random.default_rng({"normal": 1, "dup": 2, "key": 3, "neg": 4}[middle])
+    rows, cols = 257, 40
+    vt = 0 if middle == "neg" else 1
+    fmt = DataDesc(1, 0, vt)
+    batches = [rand_matrix_pushes(rng, 0, rows, cols, 0, vt, 5, 0.7) for _ in range(5)]
+    if middle == "dup":
+        batches[2] = rand_matrix_pushes(rng, 0, rows, cols, 0, vt, 5, 0.7, dup=True)
+    elif middle == "key":
+        batches[2][1] = batches[2][1] + encode_matrix_push([rows + 5], np.ones((1, cols), np.float32), 0, 1)
+    elif middle == "neg":
+        bad = np.zeros((1, cols), np.int32)
+        bad[0, 3] = -10_000
+        batches[2][3] = batches[2][3] + encode_matrix_push([7], bad, 0, 0)
+    init = (rng.integers(10, 20, size=(rows, cols)).astype(np.int32) if vt == 0
+            else rng.standard_normal((rows, cols)).astype(np.float32))
+    o = oracle_store(oracle, fmt, 0, rows - 1, cols)
+    o.data[:] = init
+    rc = 0
+    for bt in batches:
+        for p in bt:
+            rc = o.push(p)
+            if rc:
+                break
+        if rc:
+            break
+    s, _ = mk_store(fmt, 0, rows - 1, cols)
+    s.load_values(init)
+    dev = [[torch.frombuffer(bytearray(p), dtype=torch.uint8).cuda() for p in bt] for bt in batches]
+    torch.cuda.synchronize()
+    err = None
+    try:
+        for bt in dev:
+            s.pushDevice([b.data_ptr() for b in bt], [b.numel() for b in bt])
+        s.flush()
+    except DistMLException as e:
+        err = e
+    if rc:
+        assert err is not None and (err.code, err.key, err.col) == o.error()
+    else:
+        assert err is None
+    assert kat.bits_equal(s.values(), o.data)
+    s.close()
+
+
 def test_async_push_defers_error_to_flush(oracle):
     from distml_amd import DataDesc, IllegalStateException, encode_matrix_push
     fmt = DataDesc(1, 0, 0)
