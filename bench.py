@@ -78,6 +78,49 @@ def cpu_baseline(budget_s: float = 12.0):
                       f"{el:.1f} s, oracle/dml_oracle.c single thread"}
 
 
+def sparse_leg(L, torch, steps: int):
+    """Config 3 (reported beside the headline): 1e9-dim fp32 FloatArrayStore shard
+    (4 GB), 32 device-resident pushes x 1e6 unique keys ([int64 key][f32] = 12 B),
+    ordered per-push scatter-add. Algorithmic bytes per step = 32 x 12e6 + 2 x 4 x 32e6."""
+    from distml_amd import DataDesc, DataStore, KeyRange
+    from distml_amd.store import DeviceBatch
+    dim, nnz, w = 10**9, 10**6, 32
+    fmt = DataDesc(DataDesc.DATA_TYPE_ARRAY, DataDesc.KEY_TYPE_LONG, DataDesc.ELEMENT_TYPE_FLOAT)
+    store = DataStore(fmt, KeyRange(0, dim - 1))
+    bufs = []
+    st = torch.cuda.current_stream().cuda_stream
+    for b in range(w):
+        pa = (2 * b + 3) * 999_999_937 % dim
+        while pa % 2 == 0 or pa % 5 == 0:
+            pa += 1
+        t = torch.empty(nnz * 12, dtype=torch.uint8, device="cuda")
+        assert L.dml_synth_sparse_bucket(t.data_ptr(), C.byref(fmt.to_c()), 0, dim, nnz, 2000 + b, pa,
+                                         (b * 12_345_701) % dim, C.c_void_p(st)) == 0
+        bufs.append(t)
+    torch.cuda.synchronize()
+    batch = DeviceBatch([b.data_ptr() for b in bufs], [b.numel() for b in bufs])
+    store.pushDevice(batch)
+    store.flush()
+    store.set_timing(True)
+    store.kernel_time(reset=True)
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(steps):
+        store.pushDevice(batch)
+    store.flush()
+    torch.cuda.synchronize()
+    el = time.perf_counter() - t0
+    k_ms, k_n = store.kernel_time(reset=True)
+    algo = w * nnz * 12 + 2 * 4 * w * nnz
+    out = {"workload": "config3: 1e9-dim fp32 array shard, 32 pushes x 1e6 unique int64 keys, ordered scatter-add",
+           "value": round(steps * algo / el / 2**30, 2), "unit": "GiB/s (algorithmic)", "steps": steps,
+           "ms_per_step": round(el / steps * 1e3, 3), "algorithmic_bytes_per_step": algo,
+           "apply_kernel_us_avg": round(k_ms / max(k_n, 1) * 1e3, 2), "apply_launches": k_n}
+    store.close()
+    del bufs
+    return out
+
+
 def load_traffic():
     p = os.path.join(ROOT, "profiles", "pmc_traffic.json")
     if not os.path.exists(p):
@@ -95,6 +138,9 @@ def main():
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--no-cpu", action="store_true", help="skip the CPU baseline leg")
+    ap.add_argument("--sparse-steps", type=int, default=5, help="config-3 sparse leg steps (0 = skip)")
+    ap.add_argument("--group", action="store_true",
+                    help="use the sharded pre-reduce/reduce-scatter path even at N=1 (path check)")
     args = ap.parse_args()
 
     import torch
@@ -110,6 +156,10 @@ def main():
     torch.cuda.set_device(local)
     if world > 1:
         dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+    elif args.group:
+        os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+        os.environ.setdefault("MASTER_PORT", "29533")
+        dist.init_process_group("nccl", rank=0, world_size=1, device_id=torch.device("cuda", local))
     L = _lib.load()
     fmt = DataDesc(DataDesc.DATA_TYPE_MATRIX, DataDesc.KEY_TYPE_INT, DataDesc.ELEMENT_TYPE_FLOAT)
 
@@ -118,7 +168,7 @@ def main():
             dist.barrier()
         torch.cuda.synchronize()
 
-    if world == 1:
+    if world == 1 and not args.group:
         store = DataStore(fmt, KeyRange(0, ROWS - 1), COLS, device=local)
         store.rand(7)
         bufs = make_buckets(L, torch, fmt, W, ROWS)
@@ -176,11 +226,12 @@ def main():
         "config": {"workload": "config2: dense fp32 reduce, 32 device-resident pushes x 64 MiB "
                                "([int32 key][1024 x f32] x 16384) -> 16384x1024 fp32 shard per model",
                    "pushes_per_gpu": W, "push_bytes": BUCKET, "model_rows": ROWS, "cols": COLS,
-                   "parallelism": "single shard" if world == 1 else f"linearSplit({world}) + RCCL reduce-scatter",
+                   "parallelism": ("single shard" if world == 1 and not args.group
+                                   else f"linearSplit({world}) + RCCL reduce-scatter"),
                    "algorithmic_bytes_per_step_per_gpu": algo_per_rank},
     }
     if rank == 0:
-        if world == 1 and k_n > 0:
+        if world == 1 and k_n > 0 and not args.group:
             avg_s = k_ms / k_n / 1e3
             achieved = algo_per_rank / avg_s / 1e9
             traffic = load_traffic()
@@ -191,10 +242,13 @@ def main():
         elif k_n > 0:
             line["roofline"] = {"bound": "hbm", "achieved": None, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                                 "frac": None, "traffic": None, "note": "apply kernel only timed at N>1"}
-        if world == 1 and not args.no_cpu:
+        if world == 1 and not args.group and args.sparse_steps > 0:
+            del bufs
+            line["sparse"] = sparse_leg(L, torch, args.sparse_steps)
+        if world == 1 and not args.no_cpu and not args.group:
             line["cpu_baseline"] = cpu_baseline()
         print(json.dumps(line), flush=True)
-    if world > 1:
+    if dist.is_initialized():
         dist.destroy_process_group()
 
 

@@ -1,0 +1,112 @@
+// dml_jni.cc — JNI shim: com.intel.distml.util.store.GpuDataStore -> include/distml_ps.h.
+// Build (where a JDK provides jni.h):
+//   g++ -O2 -fPIC -shared -I$JAVA_HOME/include -I$JAVA_HOME/include/linux -I../../include \
+//       dml_jni.cc -L../../distml_amd -ldistml_ps -Wl,-rpath,'$ORIGIN' -o libdistml_jni.so
+// Status codes become the exceptions the reference throws (DataStore.java:91,
+// IntMatrixStore.java:175, array bounds): see include/distml_ps.h.
+#include <jni.h>
+
+#include <vector>
+
+#include "distml_ps.h"
+
+static void throw_for(JNIEnv* env, int rc) {
+    const char* cls = "java/lang/RuntimeException";
+    switch (rc) {
+        case DML_E_BAD_DESC: cls = "java/lang/IllegalArgumentException"; break;
+        case DML_E_KEY_OUT_OF_SHARD:
+        case DML_E_TRUNCATED: cls = "java/lang/ArrayIndexOutOfBoundsException"; break;
+        case DML_E_NEGATIVE_COUNTER: cls = "java/lang/IllegalStateException"; break;
+        default: break;
+    }
+    env->ThrowNew(env->FindClass(cls), dml_last_error());
+}
+
+#define FN(name) Java_com_intel_distml_util_store_GpuDataStore_##name
+static dml_store* H(jlong h) { return reinterpret_cast<dml_store*>(h); }
+
+extern "C" {
+
+JNIEXPORT jlong JNICALL FN(nativeCreate)(JNIEnv* env, jclass, jint dt, jint kt, jint vt, jint dr, jint dc, jint ada,
+                                         jlong first, jlong last, jint cols, jint device, jint flags) {
+    dml_desc d{dt, kt, vt, dr, dc, ada};
+    dml_store* s = nullptr;
+    int rc = dml_store_create_range(&d, first, last, cols, device, (uint32_t)flags, &s);
+    if (rc) throw_for(env, rc);
+    return reinterpret_cast<jlong>(s);
+}
+
+// The byte[] is borrowed for the call only: GetPrimitiveArrayCritical pins it,
+// dml_store_push copies it into pinned staging / HBM, JNI_ABORT releases
+// without copy-back. Nothing retains the pointer after return.
+JNIEXPORT void JNICALL FN(nativePush)(JNIEnv* env, jclass, jlong h, jbyteArray a) {
+    const jsize n = env->GetArrayLength(a);
+    void* p = env->GetPrimitiveArrayCritical(a, nullptr);
+    int rc = dml_store_push(H(h), static_cast<const uint8_t*>(p), n);
+    env->ReleasePrimitiveArrayCritical(a, p, JNI_ABORT);
+    if (rc) throw_for(env, rc);
+}
+
+static jbyteArray fetch_common(JNIEnv* env, dml_store* s, const int64_t* keys, int64_t n, bool range, int64_t f,
+                               int64_t l) {
+    int64_t rows = 0;
+    int32_t cols = 0;
+    dml_store_shape(s, &rows, &cols);
+    const int64_t cap = (range ? (l - f + 1) : n) * (8 + 16 * (int64_t)cols);
+    std::vector<uint8_t> out((size_t)(cap > 0 ? cap : 1));
+    int64_t len = 0;
+    int rc = range ? dml_store_fetch_range(s, f, l, out.data(), cap, &len)
+                   : dml_store_fetch(s, keys, n, out.data(), cap, &len);
+    if (rc) { throw_for(env, rc); return nullptr; }
+    jbyteArray r = env->NewByteArray((jsize)len);
+    env->SetByteArrayRegion(r, 0, (jsize)len, reinterpret_cast<const jbyte*>(out.data()));
+    return r;
+}
+
+JNIEXPORT jbyteArray JNICALL FN(nativeFetch)(JNIEnv* env, jclass, jlong h, jlongArray ks) {
+    const jsize n = env->GetArrayLength(ks);
+    std::vector<int64_t> keys((size_t)n);
+    env->GetLongArrayRegion(ks, 0, n, reinterpret_cast<jlong*>(keys.data()));
+    return fetch_common(env, H(h), keys.data(), n, false, 0, 0);
+}
+
+JNIEXPORT jbyteArray JNICALL FN(nativeFetchRange)(JNIEnv* env, jclass, jlong h, jlong f, jlong l) {
+    return fetch_common(env, H(h), nullptr, 0, true, f, l);
+}
+
+JNIEXPORT jlong JNICALL FN(nativeShardBytes)(JNIEnv*, jclass, jlong h) {
+    int64_t len = 0;
+    dml_store_write_all(H(h), nullptr, 0, &len);  // size query (returns DML_E_CAPACITY)
+    return len;
+}
+
+JNIEXPORT jbyteArray JNICALL FN(nativeWriteAll)(JNIEnv* env, jclass, jlong h) {
+    int64_t len = 0;
+    dml_store_write_all(H(h), nullptr, 0, &len);
+    std::vector<uint8_t> out((size_t)(len > 0 ? len : 1));
+    int rc = dml_store_write_all(H(h), out.data(), len, &len);
+    if (rc) { throw_for(env, rc); return nullptr; }
+    jbyteArray r = env->NewByteArray((jsize)len);
+    env->SetByteArrayRegion(r, 0, (jsize)len, reinterpret_cast<const jbyte*>(out.data()));
+    return r;
+}
+
+JNIEXPORT void JNICALL FN(nativeReadAll)(JNIEnv* env, jclass, jlong h, jbyteArray a) {
+    const jsize n = env->GetArrayLength(a);
+    void* p = env->GetPrimitiveArrayCritical(a, nullptr);
+    int rc = dml_store_read_all(H(h), static_cast<const uint8_t*>(p), n);
+    env->ReleasePrimitiveArrayCritical(a, p, JNI_ABORT);
+    if (rc) throw_for(env, rc);
+}
+
+JNIEXPORT void JNICALL FN(nativeFill)(JNIEnv* env, jclass, jlong h, jdouble v) {
+    if (int rc = dml_store_fill(H(h), v)) throw_for(env, rc);
+}
+
+JNIEXPORT void JNICALL FN(nativeSetAlpha)(JNIEnv* env, jclass, jlong h, jfloat a, jfloat m, jfloat f) {
+    if (int rc = dml_store_set_alpha(H(h), a, m, f)) throw_for(env, rc);
+}
+
+JNIEXPORT void JNICALL FN(nativeDestroy)(JNIEnv*, jclass, jlong h) { dml_store_destroy(H(h)); }
+
+}  // extern "C"

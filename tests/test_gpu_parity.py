@@ -435,3 +435,45 @@ def test_config4_adagrad_rows_bit_exact(oracle):
     assert kat.bits_equal(a, o.alpha)
     assert kat.bits_equal(d, o.delta)
     assert s.maxDelta() == o.max_delta()
+
+
+def test_shard_group_rccl_world1(oracle):
+    """The multi-GPU full-range path (HIP pre-reduce -> RCCL reduce-scatter -> HIP owner
+    apply) at world_size 1 on one MI355X; fp32 within the bound of tests/test_group_gloo.py."""
+    import os
+    import socket
+    import torch.distributed as dist
+    from distml_amd import DataDesc
+    from distml_amd.group import ShardGroup
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    dist.init_process_group("nccl", init_method=f"tcp://127.0.0.1:{port}", rank=0, world_size=1,
+                            device_id=torch.device("cuda", 0))
+    try:
+        rows, cols, W = 1000, 256, 6
+        fmt = DataDesc(1, 0, 1)
+        g = ShardGroup(fmt, rows, cols, 0, 1, device=0)
+        g.store.rand(3)
+        pas = [1, 3, 7, 9, 11, 13]  # coprime with 1000: each push lists every row once
+        host = [oracle.synth_dense_bucket(0, 1, 0, rows, rows, cols, 50 + b, pas[b], b) for b in range(W)]
+        dev = [torch.from_numpy(h).cuda() for h in host]
+        torch.cuda.synchronize()
+        g.push_full_range([d.data_ptr() for d in dev], [d.numel() for d in dev],
+                          torch.cuda.current_stream().cuda_stream)
+        g.flush()
+        o = oracle_store(oracle, fmt, 0, rows - 1, cols)
+        o.synth_fill(3)
+        init = o.data.copy()
+        for h in host:
+            assert o.push(h.tobytes()) == 0
+        got = g.store.values().astype(np.float64)
+        terms = np.abs(init.astype(np.float64))
+        for h in host:
+            rec = h.reshape(rows, 4 + 4 * cols)
+            terms[rec[:, :4].copy().view("<i4").ravel()] += np.abs(rec[:, 4:].copy().view("<f4"))
+        diff = np.abs(got - o.data.astype(np.float64))
+        assert np.all(diff <= 2 * W * 2.0 ** -24 * terms)
+    finally:
+        dist.destroy_process_group()
