@@ -138,6 +138,7 @@ def main():
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--no-cpu", action="store_true", help="skip the CPU baseline leg")
+    ap.add_argument("--no-timing", action="store_true", help="no kernel timing events in the timed region")
     ap.add_argument("--sparse-steps", type=int, default=5, help="config-3 sparse leg steps (0 = skip)")
     ap.add_argument("--group", action="store_true",
                     help="use the sharded pre-reduce/reduce-scatter path even at N=1 (path check)")
@@ -200,7 +201,7 @@ def main():
     for _ in range(args.warmup):
         step()
     finish()
-    timed_store.set_timing(True)
+    timed_store.set_timing(not args.no_timing)
     timed_store.kernel_time(reset=True)
     barrier()
     t0 = time.perf_counter()

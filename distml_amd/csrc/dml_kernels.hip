@@ -180,23 +180,28 @@ hipError_t launch_index(const Batch& bt, int nb, int64_t max_nrec, int64_t strid
 }
 
 // ---------------------------------------------------------------------------
-// k_reduce: one wave per (shard row, 64*VEC-column chunk); a 256-thread block =
-// 4 waves. The wave reads the row's slots (wave-uniform scalar loads), keeps
-// the row chunk in registers, adds every push's values in push order (loads of
-// up to 8 pushes in flight per lane, 16 B each), then writes the row once.
+// k_reduce: one wave per (shard row, CPW consecutive 64*VEC-column chunks); a
+// block = WPB waves. The wave reads the row's slots (wave-uniform scalar loads),
+// keeps its row chunks in registers, adds every push's values in push order
+// (G pushes x CPW chunks of 16-B loads in flight per lane), then writes the row
+// chunks once. With CPW > 1 one wave walks neighbouring 1-KiB chunks of a record
+// in consecutive load instructions, so the line two chunks share is requested
+// back to back (merged) instead of by two waves (fetched twice under nt loads).
 // Elements at or past the batch cutoff (first key/truncation error) are not
 // applied — the state the reference leaves when its exception escapes.
-template <typename T, int MODE, int G, bool NT, int WPB, bool SNT = false>
-__global__ __launch_bounds__(64 * WPB) void k_reduce(T* __restrict__ shard, int64_t rows, int32_t cols, int32_t nchunks,
+template <typename T, int MODE, int G, bool NT, int WPB, bool SNT, int CPW>
+__global__ __launch_bounds__(64 * WPB) void k_reduce(T* __restrict__ shard, int64_t rows, int32_t cols, int32_t ngroups,
                                                 const Batch bt, int nb, int64_t stride, int K,
                                                 const int32_t* __restrict__ slot, const uint32_t* __restrict__ rowflag,
                                                 Ctrl* __restrict__ ctrl, uint64_t tail_cut, AdaArgs ada) {
     constexpr int VEC = Elem<T>::VEC;
-    static_assert(G == 8 || G == 16, "slot groups are loaded 8 at a time");
+    constexpr int SG = G < 8 ? 8 : G;  // slots fetched per scalar round (multiple of 8)
+    static_assert(G == 2 || G == 4 || G == 8 || G == 16, "push groups of 2, 4, 8 or 16");
+    static_assert(CPW == 1 || CPW == 2 || CPW == 4, "1, 2 or 4 chunks per wave");
     const int lane = threadIdx.x & 63;
     const int wid = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     const int64_t task = (int64_t)blockIdx.x * WPB + wid;
-    const int64_t ntask = rows * (int64_t)nchunks;
+    const int64_t ntask = rows * (int64_t)ngroups;
 
     // AdaGrad maxDelta candidate of this lane.
     float cand_v = 0.f;
@@ -205,11 +210,25 @@ __global__ __launch_bounds__(64 * WPB) void k_reduce(T* __restrict__ shard, int6
 
     if (task < ntask) do {
         if (bt.prev && ctrl_abnormal(bt.prev)) break;  // predecessor needs the host first
-        const int64_t row = task / nchunks;
+        const int64_t row = task / ngroups;
         if (rowflag && rowflag[row]) break;  // a push repeats this row: the host replays it exactly
-        const int chunk = (int)(task - row * nchunks);
-        const int32_t c0 = (chunk * 64 + lane) * VEC;
-        const int nv = c0 < cols ? (cols - c0 < VEC ? cols - c0 : VEC) : 0;
+        const int cg = (int)(task - row * ngroups);
+        T* const rowp = shard + row * (int64_t)cols;
+
+        int32_t c0[CPW];
+        int nv[CPW], sh[CPW];
+        int64_t voff[CPW], shb[CPW];
+#pragma unroll
+        for (int c = 0; c < CPW; ++c) {
+            c0[c] = ((cg * CPW + c) * 64 + lane) * VEC;
+            nv[c] = c0[c] < cols ? (cols - c0[c] < VEC ? cols - c0[c] : VEC) : 0;
+            // a ragged row's last lane loads the 16 B that END at its last element
+            // (in bounds: c0 >= VEC - nv) and shifts them down by sh elements
+            sh[c] = nv[c] > 0 ? VEC - nv[c] : 0;
+            shb[c] = (int64_t)sh[c] * (int64_t)sizeof(T);
+            voff[c] = (int64_t)K + (int64_t)c0[c] * (int64_t)sizeof(T);  // value offset inside a record
+        }
+        if (nv[0] == 0) break;  // lanes past the row's last column idle
 
         uint64_t cut = ctrl->cutoff;
         if (tail_cut < cut) cut = tail_cut;
@@ -220,81 +239,76 @@ __global__ __launch_bounds__(64 * WPB) void k_reduce(T* __restrict__ shard, int6
             negcut = ctrl->neg_pos;
             if (negcut == kNoPos) break;
         }
-
         const int32_t* srow = slot + row * kMaxW;
-        T* prow = shard + row * (int64_t)cols + c0;
-        const int64_t voff = (int64_t)K + (int64_t)c0 * (int64_t)sizeof(T);  // value offset inside a record
 
-        T acc[VEC];
-        float dl[VEC], al[VEC];
+        T acc[CPW][VEC];
+        float dl[CPW][VEC], al[CPW][VEC];
         bool touched = false;
         bool negf = false;
         uint64_t negpos = kNoPos;
 
         auto load_row = [&]() {
-            if (MODE == kPreReduce) {
 #pragma unroll
-                for (int e = 0; e < VEC; ++e) acc[e] = T(0);
-            } else if (nv == VEC) {
-                const u32x4 t = SNT ? ldg16_nt((const uint8_t*)prow) : ldg16((const uint8_t*)prow);
-                unpack<T>(t, acc);
-            } else {
+            for (int c = 0; c < CPW; ++c) {
+                T* prow = rowp + c0[c];
+                if (MODE == kPreReduce) {
 #pragma unroll
-                for (int e = 0; e < VEC; ++e) acc[e] = e < nv ? prow[e] : T(0);
-            }
-            if constexpr (MODE == kAdaGrad) {
-                const int64_t ei = row * (int64_t)cols + c0;
+                    for (int e = 0; e < VEC; ++e) acc[c][e] = T(0);
+                } else if (nv[c] == VEC) {
+                    const u32x4 t = SNT ? ldg16_nt((const uint8_t*)prow) : ldg16((const uint8_t*)prow);
+                    unpack<T>(t, acc[c]);
+                } else {
 #pragma unroll
-                for (int e = 0; e < VEC; ++e) {
-                    dl[e] = e < nv ? ada.delta[ei + e] : 0.f;
-                    al[e] = e < nv ? ada.alpha[ei + e] : 0.f;
+                    for (int e = 0; e < VEC; ++e) acc[c][e] = e < nv[c] ? prow[e] : T(0);
+                }
+                if constexpr (MODE == kAdaGrad) {
+                    const int64_t ei = row * (int64_t)cols + c0[c];
+#pragma unroll
+                    for (int e = 0; e < VEC; ++e) {
+                        dl[c][e] = e < nv[c] ? ada.delta[ei + e] : 0.f;
+                        al[c][e] = e < nv[c] ? ada.alpha[ei + e] : 0.f;
+                    }
                 }
             }
         };
 
-        // One contribution u to element e at batch position p.
-        auto apply = [&](int e, T u, uint64_t p) {
+        // One contribution u to element (c, e) at batch position p.
+        auto apply = [&](int c, int e, T u, uint64_t p) {
             if constexpr (MODE == kRollbackI32) {
-                if (p > negcut) acc[e] = (T)((uint32_t)acc[e] - (uint32_t)u);
+                if (p > negcut) acc[c][e] = (T)((uint32_t)acc[c][e] - (uint32_t)u);
             } else {
-                acc[e] = Elem<T>::add(acc[e], u);
+                acc[c][e] = Elem<T>::add(acc[c][e], u);
                 if constexpr (MODE == kAddCheckI32) {
-                    if (!negf && acc[e] < 0) { negf = true; negpos = p; }
+                    if (!negf && acc[c][e] < 0) { negf = true; negpos = p; }
                 }
                 if constexpr (MODE == kAdaGrad) {
                     // FloatMatrixStoreAdaGrad.java:265-277
                     const float uu = __fmul_rn((float)u, (float)u);
-                    const float nd = __fadd_rn(dl[e], uu);
-                    if (nd > dl[e]) {  // delta rose: candidate for maxDelta (NaN never rises)
+                    const float nd = __fadd_rn(dl[c][e], uu);
+                    if (nd > dl[c][e]) {  // delta rose: candidate for maxDelta (NaN never rises)
                         if (!cand_ok || nd > cand_v || (nd == cand_v && p < cand_p)) {
                             cand_ok = true; cand_v = nd; cand_p = p;
                         }
                     }
-                    dl[e] = nd;
+                    dl[c][e] = nd;
                     if ((double)nd > 1.0) {
                         float a = (float)((double)ada.initial_alpha / ((double)ada.factor * sqrt((double)nd)));
                         if (a < ada.min_alpha) a = ada.min_alpha;
-                        al[e] = a;
+                        al[c][e] = a;
                     }
                 }
             }
         };
 
-        const bool vec_ok = cols >= VEC;   // wave-uniform: vector loads for every active lane
-        if (nv == 0) break;                 // lanes past the row's last column idle
-        // A ragged row's last lane (nv < VEC) loads the 16 B that END at its last
-        // element (in bounds: c0 >= VEC - nv) and shifts them down by `sh` elements.
-        const int sh = VEC - nv;
-        const int64_t shb = (int64_t)sh * (int64_t)sizeof(T);
-
-        for (int b0 = 0; b0 < nb; b0 += G) {
+        const bool vec_ok = cols >= VEC;  // wave-uniform: vector loads for every active lane
+        for (int b0 = 0; b0 < nb; b0 += SG) {
             // Wave-uniform scalar loads of 8 slots / push indices / bases at once;
             // every index < kMaxW is in bounds of the slot row and the kernarg table.
-            int32_t rr[G];
-            int gbv[G];
-            const uint8_t* bp[G];
+            int32_t rr[SG];
+            int gbv[SG];
+            const uint8_t* bp[SG];
 #pragma unroll
-            for (int h = 0; h < G; h += 8) {
+            for (int h = 0; h < SG; h += 8) {
                 const i32x8 sv = *(const i32x8*)(srow + b0 + h);
                 const i32x8 gv = *(const i32x8*)(&bt.bidx[b0 + h]);
                 const u64x8 pv = *(const u64x8*)(&bt.base[b0 + h]);
@@ -308,45 +322,67 @@ __global__ __launch_bounds__(64 * WPB) void k_reduce(T* __restrict__ shard, int6
             }
             bool any = false;
 #pragma unroll
-            for (int g = 0; g < G; ++g) any |= rr[g] >= 0;
+            for (int g = 0; g < SG; ++g) any |= rr[g] >= 0;
             if (!any) continue;
             if (!touched) { load_row(); touched = true; }
-            const int glast = (nb - b0 < G ? nb - b0 : G) - 1;
 
-            if (vec_ok && gbv[glast] < cut_b) {
-                // Fast path: G independent 16-B loads in flight, no branches between
-                // them; an absent slot re-reads this lane's own row chunk (cache hit).
-                u32x4 raw[G];
 #pragma unroll
-                for (int g = 0; g < G; ++g) {
-                    const uint8_t* src = (rr[g] >= 0 ? bp[g] + (int64_t)rr[g] * stride + voff : (const uint8_t*)prow) - shb;
-                    raw[g] = NT ? ldg16_nt(src) : ldg16(src);
-                }
+            for (int s0 = 0; s0 < SG; s0 += G) {
+                bool sub = false;
 #pragma unroll
-                for (int g = 0; g < G; ++g) {
-                    if (rr[g] < 0) continue;  // wave-uniform
-                    T t[VEC], u[VEC];
-                    unpack<T>(raw[g], t);
+                for (int g = 0; g < G; ++g) sub |= rr[s0 + g] >= 0;
+                if (!sub) continue;
+                int glast = s0;  // last live push of this sub-group (absent ones carry INT_MAX)
 #pragma unroll
-                    for (int e = 0; e < VEC; ++e) {  // u[e] = t[e + sh] without runtime register indexing
-                        u[e] = t[e];
+                for (int g = 0; g < G; ++g) glast = b0 + s0 + g < nb ? s0 + g : glast;
+                if (vec_ok && gbv[glast] < cut_b) {
+                    // Fast path: G x CPW independent 16-B loads in flight, no branches
+                    // between them; an absent slot / empty chunk re-reads the row start.
+                    u32x4 raw[G][CPW];
 #pragma unroll
-                        for (int k = 1; k < VEC - e; ++k) u[e] = sh == k ? t[e + k] : u[e];
+                    for (int g = 0; g < G; ++g) {
+#pragma unroll
+                        for (int c = 0; c < CPW; ++c) {
+                            const bool live = rr[s0 + g] >= 0 && nv[c] > 0;
+                            const uint8_t* src =
+                                live ? bp[s0 + g] + (int64_t)rr[s0 + g] * stride + voff[c] - shb[c] : (const uint8_t*)rowp;
+                            raw[g][c] = NT ? ldg16_nt(src) : ldg16(src);
+                        }
                     }
-                    const uint64_t pb = pos_of((uint64_t)gbv[g], (uint64_t)((int64_t)rr[g] * stride + voff));
 #pragma unroll
-                    for (int e = 0; e < VEC; ++e)
-                        if (e < nv) apply(e, u[e], pb + (uint64_t)(e * (int)sizeof(T)));
-                }
-            } else {
-                // Generic path: rows narrower than one vector, or the group holding the cutoff push.
-                for (int g = 0; g < G; ++g) {
-                    if (rr[g] < 0) continue;
-                    const int64_t roff = (int64_t)rr[g] * stride + voff;
-                    for (int e = 0; e < nv; ++e) {
-                        const uint64_t off = (uint64_t)(roff + e * (int64_t)sizeof(T));
-                        if (gbv[g] == cut_b && off >= cut_off) break;
-                        apply(e, Elem<T>::load(bp[g] + off), pos_of((uint64_t)gbv[g], off));
+                    for (int g = 0; g < G; ++g) {
+                        if (rr[s0 + g] < 0) continue;  // wave-uniform
+#pragma unroll
+                        for (int c = 0; c < CPW; ++c) {
+                            T t[VEC], u[VEC];
+                            unpack<T>(raw[g][c], t);
+#pragma unroll
+                            for (int e = 0; e < VEC; ++e) {  // u[e] = t[e + sh] without runtime register indexing
+                                u[e] = t[e];
+#pragma unroll
+                                for (int k = 1; k < VEC - e; ++k) u[e] = sh[c] == k ? t[e + k] : u[e];
+                            }
+                            const uint64_t pb =
+                                pos_of((uint64_t)gbv[s0 + g], (uint64_t)((int64_t)rr[s0 + g] * stride + voff[c]));
+#pragma unroll
+                            for (int e = 0; e < VEC; ++e)
+                                if (e < nv[c]) apply(c, e, u[e], pb + (uint64_t)(e * (int)sizeof(T)));
+                        }
+                    }
+                } else {
+                    // Generic path: rows narrower than one vector, or the group holding the cutoff push.
+                    for (int g = 0; g < G; ++g) {
+                        if (rr[s0 + g] < 0) continue;
+                        const int gb = gbv[s0 + g];
+#pragma unroll
+                        for (int c = 0; c < CPW; ++c) {
+                            const int64_t roff = (int64_t)rr[s0 + g] * stride + voff[c];
+                            for (int e = 0; e < nv[c]; ++e) {
+                                const uint64_t off = (uint64_t)(roff + e * (int64_t)sizeof(T));
+                                if (gb == cut_b && off >= cut_off) break;
+                                apply(c, e, Elem<T>::load(bp[s0 + g] + off), pos_of((uint64_t)gb, off));
+                            }
+                        }
                     }
                 }
             }
@@ -354,19 +390,25 @@ __global__ __launch_bounds__(64 * WPB) void k_reduce(T* __restrict__ shard, int6
 
         if (MODE == kPreReduce && !touched) {
 #pragma unroll
-            for (int e = 0; e < VEC; ++e) acc[e] = T(0);
+            for (int c = 0; c < CPW; ++c)
+#pragma unroll
+                for (int e = 0; e < VEC; ++e) acc[c][e] = T(0);
             touched = true;
         }
-        if (touched && nv > 0) {
-            if (nv == VEC) {
-                if (SNT) stg16_nt(prow, pack<T>(acc));
-                else stg16(prow, pack<T>(acc));
-            } else {
-                for (int e = 0; e < nv; ++e) prow[e] = acc[e];
-            }
-            if constexpr (MODE == kAdaGrad) {
-                const int64_t ei = row * (int64_t)cols + c0;
-                for (int e = 0; e < nv; ++e) { ada.delta[ei + e] = dl[e]; ada.alpha[ei + e] = al[e]; }
+        if (touched) {
+#pragma unroll
+            for (int c = 0; c < CPW; ++c) {
+                T* prow = rowp + c0[c];
+                if (nv[c] == VEC) {
+                    if (SNT) stg16_nt(prow, pack<T>(acc[c]));
+                    else stg16(prow, pack<T>(acc[c]));
+                } else {
+                    for (int e = 0; e < nv[c]; ++e) prow[e] = acc[c][e];
+                }
+                if constexpr (MODE == kAdaGrad) {
+                    const int64_t ei = row * (int64_t)cols + c0[c];
+                    for (int e = 0; e < nv[c]; ++e) { ada.delta[ei + e] = dl[c][e]; ada.alpha[ei + e] = al[c][e]; }
+                }
             }
         }
         if (MODE == kAddCheckI32 && negf) atomicMin(&ctrl->neg_pos, (unsigned long long)negpos);
@@ -398,41 +440,56 @@ __global__ __launch_bounds__(64 * WPB) void k_reduce(T* __restrict__ shard, int6
     }
 }
 
-template <typename T, int MODE, int G = 8, bool NT = false, int WPB = 4, bool SNT = false>
+template <typename T, int MODE, int G = 8, bool NT = false, int WPB = 4, bool SNT = false, int CPW = 1>
 static hipError_t launch_reduce_t(void* shard, int64_t rows, int32_t cols, const Batch& bt, int nb,
                                   int64_t stride, int K, const int32_t* slot, const uint32_t* rowflag, Ctrl* ctrl,
                                   uint64_t tail_cut,
                                   const AdaArgs& ada, hipStream_t st, int64_t* nblocks_out, LaunchEv ev = {}) {
     constexpr int VEC = Elem<T>::VEC;
     const int32_t nchunks = (cols + 64 * VEC - 1) / (64 * VEC);
-    const int64_t ntask = rows * nchunks;
+    const int32_t ngroups = (nchunks + CPW - 1) / CPW;
+    const int64_t ntask = rows * ngroups;
     const int64_t nblocks = (ntask + WPB - 1) / WPB;
     if (nblocks_out) *nblocks_out = nblocks;
     if (nblocks <= 0) return hipSuccess;
     if (ev.start || ev.stop)
-        hipExtLaunchKernelGGL((k_reduce<T, MODE, G, NT, WPB, SNT>), dim3((unsigned)nblocks), dim3(64 * WPB), 0, st,
-                              ev.start, ev.stop, 0, (T*)shard, rows, cols, nchunks, bt, nb, stride, K, slot, rowflag,
-                              ctrl, tail_cut, ada);
+        hipExtLaunchKernelGGL((k_reduce<T, MODE, G, NT, WPB, SNT, CPW>), dim3((unsigned)nblocks), dim3(64 * WPB), 0,
+                              st, ev.start, ev.stop, 0, (T*)shard, rows, cols, ngroups, bt, nb, stride, K, slot,
+                              rowflag, ctrl, tail_cut, ada);
     else
-        hipLaunchKernelGGL((k_reduce<T, MODE, G, NT, WPB, SNT>), dim3((unsigned)nblocks), dim3(64 * WPB), 0, st, (T*)shard,
-                           rows, cols, nchunks, bt, nb, stride, K, slot, rowflag, ctrl, tail_cut, ada);
+        hipLaunchKernelGGL((k_reduce<T, MODE, G, NT, WPB, SNT, CPW>), dim3((unsigned)nblocks), dim3(64 * WPB), 0, st,
+                           (T*)shard, rows, cols, ngroups, bt, nb, stride, K, slot, rowflag, ctrl, tail_cut, ada);
     return hipGetLastError();
 }
 
-// f32 kAdd variants (env DML_REDUCE_VARIANT, read per launch; default 3 = measured best):
-// 0: G=8 plain, 1: G=8 nt, 2: G=16 plain, 3: G=16 nt, 4-6: 1/8-wave blocks
+// Tuning variants of the f32 plain reduce (env DML_REDUCE_VARIANT, read per launch;
+// 0 = auto = the shape rule below). Kept for A/B runs (scripts/tune.py):
+// 1: G8/CPW1 nt, 3: G16/CPW1 nt, 9: G8/CPW2, 10: G4/CPW4, 11: G8/CPW4, 12: G4/CPW4 2-wave blocks,
+// 13: G4/CPW4 plain loads, 14: G2/CPW4, 15: G4/CPW4 8-wave blocks.
 int reduce_variant() {
     const char* v = getenv("DML_REDUCE_VARIANT");
-    return v ? atoi(v) : 3;
+    return v ? atoi(v) : 0;
 }
 
-// pre-reduce variants (DML_PREREDUCE_VARIANT): 0 G=8 plain, 1 G=8 nt
-static int prereduce_variant() {
-    const char* v = getenv("DML_PREREDUCE_VARIANT");
-    return v ? atoi(v) : 1;
+// Shape rule (measured, scripts/tune.py): one wave walks up to 4 neighbouring
+// 1-KiB chunks of a row (CPW) with G pushes x CPW 16-B nt loads in flight.
+template <typename T, int MODE>
+static hipError_t launch_auto(void* shard, int64_t rows, int32_t cols, const Batch& bt, int nb, int64_t stride, int K,
+                              const int32_t* slot, const uint32_t* rowflag, Ctrl* ctrl, uint64_t tail_cut,
+                              const AdaArgs& ada, hipStream_t st, int64_t* nblocks_out, LaunchEv ev) {
+    constexpr int VEC = Elem<T>::VEC;
+    const int32_t nchunks = (cols + 64 * VEC - 1) / (64 * VEC);
+#define DML_L(G, CPW) launch_reduce_t<T, MODE, G, true, 4, false, CPW>(shard, rows, cols, bt, nb, stride, K, slot, \
+                                                                     rowflag, ctrl, tail_cut, ada, st, nblocks_out, ev)
+    if (MODE == kAdaGrad || MODE == kRollbackI32) return DML_L(8, 1);
+    if (nchunks >= 4) return DML_L(4, 4);
+    if (nchunks >= 2) return DML_L(8, 2);
+    return DML_L(16, 1);
+#undef DML_L
 }
 
 int64_t reduce_blocks(int vtype, int64_t rows, int32_t cols) {
+    // AdaGrad (the only caller that needs it) always runs one chunk per wave, 4 waves per block
     const int VEC = vtype == kF64 ? 2 : 4;
     const int64_t nchunks = (cols + 64 * VEC - 1) / (64 * VEC);
     return (rows * nchunks + 3) / 4;
@@ -441,38 +498,36 @@ int64_t reduce_blocks(int vtype, int64_t rows, int32_t cols) {
 hipError_t launch_reduce(int vtype, int mode, void* shard, int64_t rows, int32_t cols, const Batch& bt, int nb,
                          int64_t stride, int K, const int32_t* slot, const uint32_t* rowflag, Ctrl* ctrl,
                          uint64_t tail_cut, const AdaArgs& ada, hipStream_t st, int64_t* nblocks_out, LaunchEv ev) {
-#define DML_R(T, M) launch_reduce_t<T, M, 8, true>(shard, rows, cols, bt, nb, stride, K, slot, rowflag, ctrl, tail_cut, ada, st, nblocks_out, ev)
+#define DML_A(T, M) launch_auto<T, M>(shard, rows, cols, bt, nb, stride, K, slot, rowflag, ctrl, tail_cut, ada, st, nblocks_out, ev)
+#define DML_V(G, NT, WPB, SNT, CPW) launch_reduce_t<float, kAdd, G, NT, WPB, SNT, CPW>(shard, rows, cols, bt, nb, stride, K, slot, rowflag, ctrl, tail_cut, ada, st, nblocks_out, ev)
     if (vtype == kF32) {
         if (mode == kAdd) {
-            // tuning variants (DML_REDUCE_VARIANT=<g>,<nt>), default from measurement
             switch (reduce_variant()) {
-                case 1: return launch_reduce_t<float, kAdd, 8, true>(shard, rows, cols, bt, nb, stride, K, slot, rowflag, ctrl, tail_cut, ada, st, nblocks_out, ev);
-                case 2: return launch_reduce_t<float, kAdd, 16, false>(shard, rows, cols, bt, nb, stride, K, slot, rowflag, ctrl, tail_cut, ada, st, nblocks_out, ev);
-                case 3: return launch_reduce_t<float, kAdd, 16, true>(shard, rows, cols, bt, nb, stride, K, slot, rowflag, ctrl, tail_cut, ada, st, nblocks_out, ev);
-                case 4: return launch_reduce_t<float, kAdd, 8, true, 1>(shard, rows, cols, bt, nb, stride, K, slot, rowflag, ctrl, tail_cut, ada, st, nblocks_out, ev);
-                case 5: return launch_reduce_t<float, kAdd, 8, true, 8>(shard, rows, cols, bt, nb, stride, K, slot, rowflag, ctrl, tail_cut, ada, st, nblocks_out, ev);
-                case 6: return launch_reduce_t<float, kAdd, 16, true, 8>(shard, rows, cols, bt, nb, stride, K, slot, rowflag, ctrl, tail_cut, ada, st, nblocks_out, ev);
-                case 7: return launch_reduce_t<float, kAdd, 16, true, 4, true>(shard, rows, cols, bt, nb, stride, K, slot, rowflag, ctrl, tail_cut, ada, st, nblocks_out, ev);
-                case 8: return launch_reduce_t<float, kAdd, 8, true, 4, true>(shard, rows, cols, bt, nb, stride, K, slot, rowflag, ctrl, tail_cut, ada, st, nblocks_out, ev);
-                case 0: return launch_reduce_t<float, kAdd, 8, false>(shard, rows, cols, bt, nb, stride, K, slot, rowflag, ctrl, tail_cut, ada, st, nblocks_out, ev);
-                default: return DML_R(float, kAdd);
+                case 1: return DML_V(8, true, 4, false, 1);
+                case 3: return DML_V(16, true, 4, false, 1);
+                case 9: return DML_V(8, true, 4, false, 2);
+                case 10: return DML_V(4, true, 4, false, 4);
+                case 11: return DML_V(8, true, 4, false, 4);
+                case 12: return DML_V(4, true, 2, false, 4);
+                case 13: return DML_V(4, false, 4, false, 4);
+                case 14: return DML_V(2, true, 4, false, 4);
+                case 15: return DML_V(4, true, 8, false, 4);
+                case 16: return DML_V(4, true, 4, true, 4);
+                default: return DML_A(float, kAdd);
             }
         }
-        if (mode == kAdaGrad) return DML_R(float, kAdaGrad);
-        if (mode == kPreReduce) {
-            if (prereduce_variant() == 1)
-                return launch_reduce_t<float, kPreReduce, 8, true>(shard, rows, cols, bt, nb, stride, K, slot, rowflag, ctrl, tail_cut, ada, st, nblocks_out, ev);
-            return DML_R(float, kPreReduce);
-        }
+        if (mode == kAdaGrad) return DML_A(float, kAdaGrad);
+        if (mode == kPreReduce) return DML_A(float, kPreReduce);
     } else if (vtype == kI32) {
-        if (mode == kAdd) return DML_R(int32_t, kAdd);
-        if (mode == kAddCheckI32) return DML_R(int32_t, kAddCheckI32);
-        if (mode == kPreReduce) return DML_R(int32_t, kPreReduce);
+        if (mode == kAdd) return DML_A(int32_t, kAdd);
+        if (mode == kAddCheckI32) return DML_A(int32_t, kAddCheckI32);
+        if (mode == kPreReduce) return DML_A(int32_t, kPreReduce);
     } else if (vtype == kF64) {
-        if (mode == kAdd) return DML_R(double, kAdd);
-        if (mode == kPreReduce) return DML_R(double, kPreReduce);
+        if (mode == kAdd) return DML_A(double, kAdd);
+        if (mode == kPreReduce) return DML_A(double, kPreReduce);
     }
-#undef DML_R
+#undef DML_A
+#undef DML_V
     return hipErrorInvalidValue;
 }
 

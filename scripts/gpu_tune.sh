@@ -3,6 +3,6 @@ R=$GRAFT_REPO_ROOT
 export TMPDIR=/tmp
 cd $R
 timeout -k 10 600 python -m pytest tests -m gpu -x -q -p no:cacheprovider > gpurun_out/gpu_tests.log 2>&1 || { tail -40 gpurun_out/gpu_tests.log; exit 1; }
-tail -3 gpurun_out/gpu_tests.log
-timeout -k 10 400 python scripts/tune.py 5 > gpurun_out/tune.log 2>&1
+tail -2 gpurun_out/gpu_tests.log
+timeout -k 10 400 python scripts/tune.py ${ROUNDS:-4} > gpurun_out/tune.log 2>&1
 cat gpurun_out/tune.log

@@ -22,7 +22,7 @@ from distml_amd import DataDesc, DataStore, KeyRange, _lib  # noqa: E402
 
 def main():
     rounds = int(sys.argv[1]) if len(sys.argv) > 1 else 5
-    variants = [(r, 0) for r in (1, 3, 7, 8)]
+    variants = [(r, 0) for r in (3, 10, 13, 14, 15)]
     L = _lib.load()
     fmt = DataDesc(1, 0, 1)
     store = DataStore(fmt, KeyRange(0, bench.ROWS - 1), bench.COLS)
