@@ -59,6 +59,16 @@ struct DeltaCand {
     unsigned long long pos;
 };
 
+// Optional row map of a reduce launch (multi-GPU pre-reduce pieces): task row t
+// reduces shard row  (t / block) * stride + off + t % block  (block == 0: row = t)
+// and writes it to out + t*cols (out == null: in place). Rows >= rows_total are
+// padding of linearSplit's short last shard: written as zeros.
+struct RowMap {
+    int64_t block = 0, stride = 0, off = 0;
+    int64_t rows_total = 0;
+    void* out = nullptr;
+};
+
 struct AdaArgs {
     float* alpha;
     float* delta;
@@ -90,7 +100,7 @@ hipError_t launch_index(const Batch& bt, int nb, int64_t max_nrec, int64_t strid
 hipError_t launch_reduce(int vtype, int mode, void* shard, int64_t rows, int32_t cols, const Batch& bt,
                          int nb, int64_t stride, int K, const int32_t* slot, const uint32_t* rowflag, Ctrl* ctrl,
                          uint64_t tail_cut, const AdaArgs& ada, hipStream_t st, int64_t* nblocks_out,
-                         LaunchEv ev = {});
+                         LaunchEv ev = {}, RowMap rm = {});
 hipError_t launch_rollback_i32(int32_t* shard, int64_t rows, int32_t cols, const Batch& bt, int nb,
                                int64_t stride, int K, const int32_t* slot, const uint32_t* rowflag, Ctrl* ctrl,
                                uint64_t tail_cut, hipStream_t st);

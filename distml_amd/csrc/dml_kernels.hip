@@ -193,7 +193,7 @@ template <typename T, int MODE, int G, bool NT, int WPB, bool SNT, int CPW>
 __global__ __launch_bounds__(64 * WPB) void k_reduce(T* __restrict__ shard, int64_t rows, int32_t cols, int32_t ngroups,
                                                 const Batch bt, int nb, int64_t stride, int K,
                                                 const int32_t* __restrict__ slot, const uint32_t* __restrict__ rowflag,
-                                                Ctrl* __restrict__ ctrl, uint64_t tail_cut, AdaArgs ada) {
+                                                Ctrl* __restrict__ ctrl, uint64_t tail_cut, AdaArgs ada, RowMap rm) {
     constexpr int VEC = Elem<T>::VEC;
     constexpr int SG = G < 8 ? 8 : G;  // slots fetched per scalar round (multiple of 8)
     static_assert(G == 2 || G == 4 || G == 8 || G == 16, "push groups of 2, 4, 8 or 16");
@@ -210,10 +210,20 @@ __global__ __launch_bounds__(64 * WPB) void k_reduce(T* __restrict__ shard, int6
 
     if (task < ntask) do {
         if (bt.prev && ctrl_abnormal(bt.prev)) break;  // predecessor needs the host first
-        const int64_t row = task / ngroups;
+        const int64_t trow = task / ngroups;
+        const int cg = (int)(task - trow * ngroups);
+        const int64_t row = rm.block ? (trow / rm.block) * rm.stride + rm.off + trow % rm.block : trow;
+        T* const rowp = rm.out ? (T*)rm.out + trow * (int64_t)cols : shard + row * (int64_t)cols;
+        if (rm.block && row >= rm.rows_total) {  // padding row of a short last shard
+#pragma unroll
+            for (int c = 0; c < CPW; ++c) {
+                const int32_t cc = ((cg * CPW + c) * 64 + lane) * VEC;
+                for (int e = 0; e < VEC; ++e)
+                    if (cc + e < cols) rowp[cc + e] = T(0);
+            }
+            break;
+        }
         if (rowflag && rowflag[row]) break;  // a push repeats this row: the host replays it exactly
-        const int cg = (int)(task - row * ngroups);
-        T* const rowp = shard + row * (int64_t)cols;
 
         int32_t c0[CPW];
         int nv[CPW], sh[CPW];
@@ -444,7 +454,8 @@ template <typename T, int MODE, int G = 8, bool NT = false, int WPB = 4, bool SN
 static hipError_t launch_reduce_t(void* shard, int64_t rows, int32_t cols, const Batch& bt, int nb,
                                   int64_t stride, int K, const int32_t* slot, const uint32_t* rowflag, Ctrl* ctrl,
                                   uint64_t tail_cut,
-                                  const AdaArgs& ada, hipStream_t st, int64_t* nblocks_out, LaunchEv ev = {}) {
+                                  const AdaArgs& ada, hipStream_t st, int64_t* nblocks_out, LaunchEv ev = {},
+                                  RowMap rm = {}) {
     constexpr int VEC = Elem<T>::VEC;
     const int32_t nchunks = (cols + 64 * VEC - 1) / (64 * VEC);
     const int32_t ngroups = (nchunks + CPW - 1) / CPW;
@@ -455,10 +466,10 @@ static hipError_t launch_reduce_t(void* shard, int64_t rows, int32_t cols, const
     if (ev.start || ev.stop)
         hipExtLaunchKernelGGL((k_reduce<T, MODE, G, NT, WPB, SNT, CPW>), dim3((unsigned)nblocks), dim3(64 * WPB), 0,
                               st, ev.start, ev.stop, 0, (T*)shard, rows, cols, ngroups, bt, nb, stride, K, slot,
-                              rowflag, ctrl, tail_cut, ada);
+                              rowflag, ctrl, tail_cut, ada, rm);
     else
         hipLaunchKernelGGL((k_reduce<T, MODE, G, NT, WPB, SNT, CPW>), dim3((unsigned)nblocks), dim3(64 * WPB), 0, st,
-                           (T*)shard, rows, cols, ngroups, bt, nb, stride, K, slot, rowflag, ctrl, tail_cut, ada);
+                           (T*)shard, rows, cols, ngroups, bt, nb, stride, K, slot, rowflag, ctrl, tail_cut, ada, rm);
     return hipGetLastError();
 }
 
@@ -476,11 +487,11 @@ int reduce_variant() {
 template <typename T, int MODE>
 static hipError_t launch_auto(void* shard, int64_t rows, int32_t cols, const Batch& bt, int nb, int64_t stride, int K,
                               const int32_t* slot, const uint32_t* rowflag, Ctrl* ctrl, uint64_t tail_cut,
-                              const AdaArgs& ada, hipStream_t st, int64_t* nblocks_out, LaunchEv ev) {
+                              const AdaArgs& ada, hipStream_t st, int64_t* nblocks_out, LaunchEv ev, RowMap rm) {
     constexpr int VEC = Elem<T>::VEC;
     const int32_t nchunks = (cols + 64 * VEC - 1) / (64 * VEC);
 #define DML_L(G, CPW) launch_reduce_t<T, MODE, G, true, 4, false, CPW>(shard, rows, cols, bt, nb, stride, K, slot, \
-                                                                     rowflag, ctrl, tail_cut, ada, st, nblocks_out, ev)
+                                                                     rowflag, ctrl, tail_cut, ada, st, nblocks_out, ev, rm)
     if (MODE == kAdaGrad || MODE == kRollbackI32) return DML_L(8, 1);
     if (nchunks >= 4) return DML_L(4, 4);
     if (nchunks >= 2) return DML_L(8, 2);
@@ -497,8 +508,9 @@ int64_t reduce_blocks(int vtype, int64_t rows, int32_t cols) {
 
 hipError_t launch_reduce(int vtype, int mode, void* shard, int64_t rows, int32_t cols, const Batch& bt, int nb,
                          int64_t stride, int K, const int32_t* slot, const uint32_t* rowflag, Ctrl* ctrl,
-                         uint64_t tail_cut, const AdaArgs& ada, hipStream_t st, int64_t* nblocks_out, LaunchEv ev) {
-#define DML_A(T, M) launch_auto<T, M>(shard, rows, cols, bt, nb, stride, K, slot, rowflag, ctrl, tail_cut, ada, st, nblocks_out, ev)
+                         uint64_t tail_cut, const AdaArgs& ada, hipStream_t st, int64_t* nblocks_out, LaunchEv ev,
+                         RowMap rm) {
+#define DML_A(T, M) launch_auto<T, M>(shard, rows, cols, bt, nb, stride, K, slot, rowflag, ctrl, tail_cut, ada, st, nblocks_out, ev, rm)
 #define DML_V(G, NT, WPB, SNT, CPW) launch_reduce_t<float, kAdd, G, NT, WPB, SNT, CPW>(shard, rows, cols, bt, nb, stride, K, slot, rowflag, ctrl, tail_cut, ada, st, nblocks_out, ev)
     if (vtype == kF32) {
         if (mode == kAdd) {

@@ -42,10 +42,27 @@ class HipOps:
     def apply(self, store: DataStore, src_ptr: int, elems: int) -> None:
         check(_lib.load().dml_store_apply_dense_device(store._h, C.c_void_p(src_ptr), elems), store)
 
+    # piecewise pre-reduce (pipelined with the reduce-scatter)
+    def begin(self, fmt: DataDesc, first: int, rows: int, cols: int, dev_ptrs, lens, stream: int):
+        n = len(dev_ptrs)
+        ptrs = (C.c_void_p * max(n, 1))(*dev_ptrs)
+        ls = (C.c_int64 * max(n, 1))(*lens)
+        h = C.c_void_p()
+        check(_lib.load().dml_prereduce_begin(C.byref(fmt.to_c()), first, rows, cols, ptrs, ls, n,
+                                              C.c_void_p(stream), C.byref(h)))
+        return h.value
+
+    def piece(self, h, block: int, stride: int, off: int, ntask_rows: int, out_ptr: int, stream: int) -> None:
+        check(_lib.load().dml_prereduce_piece(C.c_void_p(h), block, stride, off, ntask_rows, C.c_void_p(out_ptr),
+                                              C.c_void_p(stream)))
+
+    def end(self, h) -> None:
+        check(_lib.load().dml_prereduce_end(C.c_void_p(h)))
+
 
 class ShardGroup:
     def __init__(self, fmt: DataDesc, total_rows: int, cols: int, rank: int, world: int,
-                 device: Optional[int] = None, ops=None, store_factory=None):
+                 device: Optional[int] = None, ops=None, store_factory=None, pieces: int = 4):
         import torch
         import torch.distributed as dist
         self.torch, self.dist = torch, dist
@@ -61,10 +78,18 @@ class ShardGroup:
         dev = torch.device("cuda", device) if device is not None else torch.device("cpu")
         self.partial = torch.empty(world * self.step_rows * cols, dtype=self.dtype, device=dev)
         self.recv = torch.empty(self.step_rows * cols, dtype=self.dtype, device=dev)
+        # pipelining of the full-range path: P row slices, reduce-scattered on a comm stream
+        self.pieces = pieces
+        if self.partial.is_cuda:
+            self.comm = torch.cuda.Stream(device=dev)
+            self._ev = [torch.cuda.Event() for _ in range(pieces)]
 
     def push_full_range(self, dev_ptrs: Sequence[int], lens: Sequence[int], stream: int = 0) -> None:
         """Ordered local pre-reduce -> reduce-scatter -> owner apply (see module doc)."""
         torch, dist = self.torch, self.dist
+        if (self.partial.is_cuda and hasattr(self.ops, "begin") and len(dev_ptrs) <= 64
+                and self.step_rows % self.pieces == 0):
+            return self._push_pipelined(dev_ptrs, lens)
         # rows past the matrix end (linearSplit's last shard may be short) stay zero
         self.ops.prereduce(self.fmt, 0, self.total_rows, self.cols, dev_ptrs, lens,
                            self.partial.data_ptr(), stream)
@@ -81,6 +106,29 @@ class ShardGroup:
             torch.cuda.current_stream().synchronize()
         n = self.shard.size() * self.cols
         self.ops.apply(self.store, self.recv.data_ptr(), n)
+
+    def _push_pipelined(self, dev_ptrs, lens) -> None:
+        """Pre-reduce in `pieces` row slices; slice j holds rows [q*S + j*S/P, q*S + (j+1)*S/P)
+        of every rank q, laid out [rank][row], so its reduce-scatter (comm stream) runs
+        while slice j+1 is pre-reduced (compute stream)."""
+        torch, dist = self.torch, self.dist
+        S, P, cols, world = self.step_rows, self.pieces, self.cols, self.world
+        blk = S // P
+        cur = torch.cuda.current_stream()
+        st = cur.cuda_stream
+        h = self.ops.begin(self.fmt, 0, self.total_rows, cols, dev_ptrs, lens, st)
+        try:
+            for j in range(P):
+                piece = self.partial[j * world * blk * cols:(j + 1) * world * blk * cols]
+                self.ops.piece(h, blk, S, j * blk, world * blk, piece.data_ptr(), st)
+                self._ev[j].record(cur)
+                with torch.cuda.stream(self.comm):
+                    self.comm.wait_event(self._ev[j])
+                    dist.reduce_scatter_tensor(self.recv[j * blk * cols:(j + 1) * blk * cols], piece)
+        finally:
+            self.ops.end(h)  # waits for the pre-reduce; key / repeated-row errors
+        self.comm.synchronize()
+        self.ops.apply(self.store, self.recv.data_ptr(), self.shard.size() * cols)
 
     def push_local(self, dev_ptrs: Sequence[int], lens: Sequence[int]) -> None:
         """Pushes already split to this shard: exact ordered apply, no exchange."""

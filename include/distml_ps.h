@@ -182,6 +182,20 @@ int dml_reduce_buckets_dense(const dml_desc* desc, int64_t first_key, int64_t ro
                              const void* const* dev_bufs, const int64_t* lens, int32_t n,
                              void* dev_out, void* stream);
 
+/* Piecewise pre-reduce for pipelining with the reduce-scatter: _begin enqueues
+ * the key index of the n (<= 64) full-range pushes on `stream`; each _piece
+ * writes the ordered sum of rows r(t) = (t / row_block) * row_stride + row_off
+ * + t % row_block, t < ntask_rows, to dev_out + t*cols (rows >= `rows`, the
+ * padding of linearSplit's short last shard, are zeros); _end waits for the
+ * stream and reports key-out-of-matrix / repeated-row errors. Opaque handle. */
+typedef struct dml_prereduce dml_prereduce;
+int dml_prereduce_begin(const dml_desc* desc, int64_t first_key, int64_t rows, int32_t cols,
+                        const void* const* dev_bufs, const int64_t* lens, int32_t n, void* stream,
+                        dml_prereduce** out);
+int dml_prereduce_piece(dml_prereduce* p, int64_t row_block, int64_t row_stride, int64_t row_off,
+                        int64_t ntask_rows, void* dev_out, void* stream);
+int dml_prereduce_end(dml_prereduce* p);
+
 /* --- synthetic workload generators (bench/test support) ----------------- *
  * Counter-based (SplitMix64) so the CPU oracle regenerates the same bytes.
  * Spec in DESIGN.md §Synthetic data. Run on `stream` (void* hipStream_t). */

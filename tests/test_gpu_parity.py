@@ -477,3 +477,36 @@ def test_shard_group_rccl_world1(oracle):
         assert np.all(diff <= 2 * W * 2.0 ** -24 * terms)
     finally:
         dist.destroy_process_group()
+
+
+def test_prereduce_pieces_row_map(oracle):
+    """dml_prereduce_{begin,piece,end}: slices laid out [rank][row] for a 3-way
+    linearSplit of 1000 rows (step 334, last shard 332 rows + 2 padding rows),
+    bit-exact vs an oracle store that starts at zero (0 + g0 + g1 + ...)."""
+    import ctypes as C
+    from distml_amd import DataDesc
+    from distml_amd.group import HipOps
+    rows, cols, W, world, P = 1000, 300, 5, 3, 2
+    S = (rows - 1 + world) // world
+    blk = S // P
+    fmt = DataDesc(1, 0, 1)
+    pas = [1, 3, 7, 9, 11]
+    host = [oracle.synth_dense_bucket(0, 1, 0, rows, rows, cols, 70 + b, pas[b], b) for b in range(W)]
+    dev = [torch.from_numpy(h).cuda() for h in host]
+    torch.cuda.synchronize()
+    ops = HipOps()
+    st = torch.cuda.current_stream().cuda_stream
+    out = torch.full((P, world * blk, cols), float("nan"), dtype=torch.float32, device="cuda")
+    h = ops.begin(fmt, 0, rows, cols, [d.data_ptr() for d in dev], [d.numel() for d in dev], st)
+    for j in range(P):
+        ops.piece(h, blk, S, j * blk, world * blk, out[j].data_ptr(), st)
+    ops.end(h)
+    o = oracle_store(oracle, fmt, 0, rows - 1, cols)
+    for hb in host:
+        assert o.push(hb.tobytes()) == 0
+    got = out.cpu().numpy()
+    for j in range(P):
+        for t in range(world * blk):
+            r = (t // blk) * S + j * blk + t % blk
+            want = o.data[r] if r < rows else np.zeros(cols, np.float32)
+            assert got[j, t].tobytes() == want.tobytes(), (j, t, r)
