@@ -64,6 +64,7 @@ SIGNATURES = {
     "dml_synth_dense_bucket": (C.c_int, [_vp, _P(dml_desc), _i64, _i64, _i64, _i32, _u64, _u64, _u64, _vp]),
     "dml_synth_sparse_bucket": (C.c_int, [_vp, _P(dml_desc), _i64, _i64, _i64, _u64, _u64, _u64, _vp]),
     "dml_synth_fill_store": (C.c_int, [_vp, _u64]),
+    "dml_diag_stream": (C.c_int, [_i32, _vp, _vp, _i64, _vp, _P(C.c_float)]),
     "dml_last_error": (C.c_char_p, []),
     "dml_version": (C.c_char_p, []),
 }

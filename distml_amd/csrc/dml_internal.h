@@ -126,6 +126,7 @@ hipError_t launch_synth_dense(uint8_t* out, int K, int vtype, int64_t first, int
 hipError_t launch_synth_sparse(uint8_t* out, int K, int vtype, int value_stride, int64_t first,
                                int64_t key_space, int64_t nrec, uint64_t s0, uint64_t pa, uint64_t pc,
                                hipStream_t st);
+hipError_t launch_stream(bool copy, void* dst, const void* src, int64_t n16, hipStream_t st, LaunchEv ev);
 hipError_t launch_synth_fill(int vtype, void* p, int64_t n, uint64_t s0, hipStream_t st);
 hipError_t launch_key_rows(const uint8_t* base, int64_t nrec, int64_t stride, int K, int64_t first, int64_t rows,
                            int32_t* out, hipStream_t st);

@@ -1217,6 +1217,24 @@ int dml_synth_sparse_bucket(void* dev_out, const dml_desc* desc, int64_t first_k
     return DML_OK;
 }
 
+int dml_diag_stream(int32_t copy, void* dev_dst, const void* dev_src, int64_t bytes, void* stream, float* ms) {
+    if (!dev_dst || !dev_src || bytes < 0 || bytes % 16 || ((uintptr_t)dev_dst | (uintptr_t)dev_src) % 16)
+        return set_err(DML_E_INVALID_ARG, "stream copy needs 16-B aligned buffers and a multiple of 16 bytes");
+    hipStream_t st = (hipStream_t)stream;
+    hipEvent_t e0 = nullptr, e1 = nullptr;
+    HIPCHK(hipEventCreate(&e0));
+    hipError_t e = hipEventCreate(&e1);
+    if (e == hipSuccess) e = launch_stream(copy != 0, dev_dst, dev_src, bytes / 16, st, LaunchEv{e0, e1});
+    if (e == hipSuccess) e = hipEventSynchronize(e1);
+    float t = 0.f;
+    if (e == hipSuccess) e = hipEventElapsedTime(&t, e0, e1);
+    (void)hipEventDestroy(e0);
+    if (e1) (void)hipEventDestroy(e1);
+    if (e != hipSuccess) return set_err(DML_E_HIP, hipGetErrorString(e));
+    if (ms) *ms = t;
+    return DML_OK;
+}
+
 int dml_synth_fill_store(dml_store* s, uint64_t seed) {
     if (int rc = check_store(s)) return rc;
     std::lock_guard<std::mutex> lk(s->mu);

@@ -62,7 +62,8 @@ class HipOps:
 
 class ShardGroup:
     def __init__(self, fmt: DataDesc, total_rows: int, cols: int, rank: int, world: int,
-                 device: Optional[int] = None, ops=None, store_factory=None, pieces: int = 4):
+                 device: Optional[int] = None, ops=None, store_factory=None, pieces: int = 4,
+                 reduce_scatter=None):
         import torch
         import torch.distributed as dist
         self.torch, self.dist = torch, dist
@@ -73,6 +74,10 @@ class ShardGroup:
         self.total_rows = total_rows
         self.device = device
         self.ops = ops or HipOps()
+        # reduce_scatter(out, inp): out = this rank's chunk of sum-over-ranks(inp); runs on the
+        # current stream context. Default: RCCL ncclReduceScatter (backend "nccl"), or a
+        # host all_reduce + slice under gloo (no reduce_scatter there).
+        self._rs = reduce_scatter or self._default_reduce_scatter
         self.store = (store_factory or (lambda: DataStore(fmt, self.shard, cols, device=device)))()
         self.dtype = {0: torch.int32, 1: torch.float32, 3: torch.float64}[fmt.valueType]
         dev = torch.device("cuda", device) if device is not None else torch.device("cpu")
@@ -84,24 +89,28 @@ class ShardGroup:
             self.comm = torch.cuda.Stream(device=dev)
             self._ev = [torch.cuda.Event() for _ in range(pieces)]
 
+    def _default_reduce_scatter(self, out, inp) -> None:
+        dist = self.dist
+        if self.world == 1:
+            out.copy_(inp)
+        elif dist.get_backend() == "gloo":
+            host = inp.cpu() if inp.is_cuda else inp.clone()
+            dist.all_reduce(host)
+            n = out.numel()
+            out.copy_(host[self.rank * n:(self.rank + 1) * n])
+        else:
+            dist.reduce_scatter_tensor(out, inp)
+
     def push_full_range(self, dev_ptrs: Sequence[int], lens: Sequence[int], stream: int = 0) -> None:
         """Ordered local pre-reduce -> reduce-scatter -> owner apply (see module doc)."""
-        torch, dist = self.torch, self.dist
+        torch = self.torch
         if (self.partial.is_cuda and hasattr(self.ops, "begin") and len(dev_ptrs) <= 64
                 and self.step_rows % self.pieces == 0):
             return self._push_pipelined(dev_ptrs, lens)
         # rows past the matrix end (linearSplit's last shard may be short) stay zero
         self.ops.prereduce(self.fmt, 0, self.total_rows, self.cols, dev_ptrs, lens,
                            self.partial.data_ptr(), stream)
-        if self.world > 1:
-            if dist.get_backend() == "gloo":
-                dist.all_reduce(self.partial)  # gloo: no reduce_scatter for CPU tensors
-                lo = self.rank * self.step_rows * self.cols
-                self.recv.copy_(self.partial[lo:lo + self.step_rows * self.cols])
-            else:
-                dist.reduce_scatter_tensor(self.recv, self.partial)
-        else:
-            self.recv.copy_(self.partial[: self.step_rows * self.cols])
+        self._rs(self.recv, self.partial)
         if self.recv.is_cuda:
             torch.cuda.current_stream().synchronize()
         n = self.shard.size() * self.cols
@@ -111,7 +120,7 @@ class ShardGroup:
         """Pre-reduce in `pieces` row slices; slice j holds rows [q*S + j*S/P, q*S + (j+1)*S/P)
         of every rank q, laid out [rank][row], so its reduce-scatter (comm stream) runs
         while slice j+1 is pre-reduced (compute stream)."""
-        torch, dist = self.torch, self.dist
+        torch = self.torch
         S, P, cols, world = self.step_rows, self.pieces, self.cols, self.world
         blk = S // P
         cur = torch.cuda.current_stream()
@@ -124,7 +133,7 @@ class ShardGroup:
                 self._ev[j].record(cur)
                 with torch.cuda.stream(self.comm):
                     self.comm.wait_event(self._ev[j])
-                    dist.reduce_scatter_tensor(self.recv[j * blk * cols:(j + 1) * blk * cols], piece)
+                    self._rs(self.recv[j * blk * cols:(j + 1) * blk * cols], piece)
         finally:
             self.ops.end(h)  # waits for the pre-reduce; key / repeated-row errors
         self.comm.synchronize()

@@ -207,6 +207,13 @@ int dml_synth_sparse_bucket(void* dev_out, const dml_desc* desc, int64_t first_k
                             uint64_t perm_a, uint64_t perm_c, void* stream);
 int dml_synth_fill_store(dml_store* s, uint64_t seed);
 
+/* Diagnostic: stream `bytes` (multiple of 16, 16-B aligned) from dev_src with
+ * 16-B non-temporal loads, copying them to dev_dst (copy != 0) or only reading
+ * them (copy == 0; dev_dst receives at most one word); timed by HIP events on
+ * `stream`, *ms = kernel time. bench.py reports the reduce's fraction of these
+ * measured HBM ceilings. */
+int dml_diag_stream(int32_t copy, void* dev_dst, const void* dev_src, int64_t bytes, void* stream, float* ms);
+
 /* --- misc --------------------------------------------------------------- */
 const char* dml_last_error(void);   /* thread-local message for the last failure */
 const char* dml_version(void);

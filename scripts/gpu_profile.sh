@@ -9,4 +9,6 @@ cat gpurun_out/bench_prof.json
 timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $R/gpurun_out/prof_stats -o run --output-format csv -- python3 bench.py --steps 20 --warmup 3 --no-cpu --sparse-steps 0 > gpurun_out/prof_stats.log 2>&1
 timeout -k 10 300 rocprofv3 --pmc FETCH_SIZE -d $R/gpurun_out/prof_fetch -o run --output-format csv -- python3 bench.py --steps 4 --warmup 1 --no-cpu --sparse-steps 0 > gpurun_out/prof_fetch.log 2>&1
 timeout -k 10 300 rocprofv3 --pmc WRITE_SIZE -d $R/gpurun_out/prof_write -o run --output-format csv -- python3 bench.py --steps 4 --warmup 1 --no-cpu --sparse-steps 0 > gpurun_out/prof_write.log 2>&1
-echo profile-done
+
+timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $R/gpurun_out/prof_sparse -o run --output-format csv -- python3 bench.py --steps 2 --warmup 1 --no-cpu --sparse-steps 5 > gpurun_out/prof_sparse.log 2>&1
+echo sparse-profile-done

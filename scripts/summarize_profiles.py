@@ -62,6 +62,15 @@ def main(tag):
                 f"{ALGO/avg_ns:.1f} GB/s algorithmic, {traffic/avg_ns:.1f} GB/s measured traffic\n")
         if bench:
             f.write(f"\n## bench.py line of the same box\n\n```\n{bench}\n```\n")
+    sp = os.path.join(OUT, "prof_sparse", "run_kernel_stats.csv")
+    if os.path.exists(sp):
+        shutil.copy(sp, os.path.join(PROF, f"{tag}_sparse_kernel_stats.csv"))
+        with open(os.path.join(PROF, f"{tag}_summary.md"), "a") as f:
+            f.write("\n## Sparse leg (config 3), `rocprofv3 --kernel-trace --stats -- python3 bench.py --steps 2 "
+                    "--warmup 1 --no-cpu --sparse-steps 5`\n\n| kernel | calls | avg µs | % time |\n|---|---|---|---|\n")
+            for r in csv.DictReader(open(sp)):
+                f.write(f"| `{r['Name'][:90]}` | {r['Calls']} | {float(r['AverageNs'])/1e3:.1f} | "
+                        f"{float(r['Percentage']):.1f} |\n")
     print(open(os.path.join(PROF, f"{tag}_summary.md")).read())
 
 

@@ -1,0 +1,179 @@
+// Microbenchmark: scatter-add access patterns into a 1e9-float array (config 3 shape).
+// Not part of the product; informs the sparse kernel design.
+//   hipcc --offload-arch=gfx950 -O3 scripts/ubench_scatter.hip -o gpurun_out/ubench_scatter
+#include <hip/hip_runtime.h>
+#include <hipcub/hipcub.hpp>
+
+#include <algorithm>
+#include <cstdio>
+#include <cstdlib>
+#include <vector>
+
+#define CK(x)                                                                         \
+    do {                                                                              \
+        hipError_t e_ = (x);                                                          \
+        if (e_ != hipSuccess) {                                                       \
+            fprintf(stderr, "%s:%d %s\n", __FILE__, __LINE__, hipGetErrorString(e_)); \
+            exit(1);                                                                  \
+        }                                                                             \
+    } while (0)
+
+__global__ void k_atomic(float* a, const uint32_t* keys, const float* v, int64_t n) {
+    int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i < n) atomicAdd(&a[keys[i]], v[i]);
+}
+__global__ void k_plain(float* a, const uint32_t* keys, const float* v, int64_t n) {
+    int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i < n) {
+        uint32_t k = keys[i];
+        a[k] = a[k] + v[i];
+    }
+}
+// 4 independent RMWs per thread (more memory-level parallelism)
+__global__ void k_plain4(float* a, const uint32_t* keys, const float* v, int64_t n) {
+    int64_t i0 = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x);
+    int64_t stride = (int64_t)gridDim.x * blockDim.x;
+    uint32_t k[4];
+    float x[4], u[4];
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+        int64_t i = i0 + j * stride;
+        k[j] = i < n ? keys[i] : 0;
+        u[j] = i < n ? v[i] : 0.f;
+    }
+#pragma unroll
+    for (int j = 0; j < 4; ++j) x[j] = a[k[j]];
+#pragma unroll
+    for (int j = 0; j < 4; ++j)
+        if (i0 + j * stride < n) a[k[j]] = x[j] + u[j];
+}
+__global__ void k_read(const float4* p, int64_t n, float* out) {
+    float s = 0;
+    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
+        float4 q = p[i];
+        s += q.x + q.y + q.z + q.w;
+    }
+    if (s == 1234.5f) *out = s;
+}
+
+static uint64_t sm(uint64_t x) {
+    x += 0x9e3779b97f4a7c15ull;
+    x = (x ^ (x >> 30)) * 0xbf58476d1ce4e5b9ull;
+    x = (x ^ (x >> 27)) * 0x94d049bb133111ebull;
+    return x ^ (x >> 31);
+}
+
+int main() {
+    const int64_t rows = 1000000000, per = 1000000;
+    const int W = 32;
+    const int64_t N = per * W;
+    float* a;
+    CK(hipMalloc(&a, rows * 4));
+    CK(hipMemset(a, 0, rows * 4));
+    std::vector<uint32_t> hk(N), hs(N);
+    std::vector<float> hv(N, 1e-3f);
+    for (int b = 0; b < W; ++b) {
+        uint64_t pa = (sm(2000 + b) % (rows - 1)) | 1, pc = sm(3000 + b) % rows;
+        while (pa % 2 == 0 || pa % 5 == 0) pa += 2;  // coprime with 1e9
+        for (int64_t r = 0; r < per; ++r) hk[b * per + r] = (uint32_t)((pa * (uint64_t)r + pc) % rows);
+    }
+    // per-push sorted copy and globally sorted copy
+    hs = hk;
+    for (int b = 0; b < W; ++b) std::sort(hs.begin() + b * per, hs.begin() + (b + 1) * per);
+    std::vector<uint32_t> hg = hk;
+    std::sort(hg.begin(), hg.end());
+    uint32_t *dk, *ds, *dg;
+    float *dv, *dout;
+    CK(hipMalloc(&dk, N * 4));
+    CK(hipMalloc(&ds, N * 4));
+    CK(hipMalloc(&dg, N * 4));
+    CK(hipMalloc(&dv, N * 4));
+    CK(hipMalloc(&dout, 4));
+    CK(hipMemcpy(dk, hk.data(), N * 4, hipMemcpyHostToDevice));
+    CK(hipMemcpy(ds, hs.data(), N * 4, hipMemcpyHostToDevice));
+    CK(hipMemcpy(dg, hg.data(), N * 4, hipMemcpyHostToDevice));
+    CK(hipMemcpy(dv, hv.data(), N * 4, hipMemcpyHostToDevice));
+    hipEvent_t e0, e1;
+    CK(hipEventCreate(&e0));
+    CK(hipEventCreate(&e1));
+    auto timeit = [&](const char* name, auto fn) {
+        fn();
+        CK(hipDeviceSynchronize());
+        float best = 1e30f;
+        for (int rep = 0; rep < 5; ++rep) {
+            CK(hipEventRecord(e0));
+            fn();
+            CK(hipEventRecord(e1));
+            CK(hipEventSynchronize(e1));
+            float ms;
+            CK(hipEventElapsedTime(&ms, e0, e1));
+            best = std::min(best, ms);
+        }
+        printf("%-44s %8.3f ms  %7.2f Gupd/s\n", name, best, N / (best * 1e6));
+    };
+    const unsigned g1 = (unsigned)((per + 255) / 256);
+    const unsigned gN = (unsigned)((N + 255) / 256);
+    timeit("atomic, 32 launches x 1e6 random", [&] {
+        for (int b = 0; b < W; ++b) k_atomic<<<g1, 256>>>(a, dk + b * per, dv + b * per, per);
+    });
+    timeit("plain RMW, 32 launches x 1e6 random", [&] {
+        for (int b = 0; b < W; ++b) k_plain<<<g1, 256>>>(a, dk + b * per, dv + b * per, per);
+    });
+    timeit("plain RMW x4 ILP, 32 launches random", [&] {
+        for (int b = 0; b < W; ++b) k_plain4<<<(g1 + 3) / 4, 256>>>(a, dk + b * per, dv + b * per, per);
+    });
+    timeit("plain RMW, 32 launches, per-push sorted", [&] {
+        for (int b = 0; b < W; ++b) k_plain<<<g1, 256>>>(a, ds + b * per, dv + b * per, per);
+    });
+    timeit("atomic, 1 launch x 32e6 random", [&] { k_atomic<<<gN, 256>>>(a, dk, dv, N); });
+    timeit("plain RMW, 1 launch, globally sorted 32e6", [&] { k_plain<<<gN, 256>>>(a, dg, dv, N); });
+    timeit("plain RMW x4, 1 launch, globally sorted", [&] { k_plain4<<<(gN + 3) / 4, 256>>>(a, dg, dv, N); });
+    timeit("atomic, 1 launch, globally sorted", [&] { k_atomic<<<gN, 256>>>(a, dg, dv, N); });
+    {
+        float ms_best = 1e30f;
+        for (int rep = 0; rep < 5; ++rep) {
+            CK(hipEventRecord(e0));
+            k_read<<<4096, 256>>>((const float4*)a, rows / 4, dout);
+            CK(hipEventRecord(e1));
+            CK(hipEventSynchronize(e1));
+            float ms;
+            CK(hipEventElapsedTime(&ms, e0, e1));
+            ms_best = std::min(ms_best, ms);
+        }
+        printf("%-44s %8.3f ms  %7.1f GB/s\n", "stream read 4 GB", ms_best, rows * 4 / (ms_best * 1e6));
+    }
+    // partition cost: radix sort of 32e6 (u32 key, u64 payload) pairs on 16 / 30 key bits
+    {
+        uint32_t *kin, *kout;
+        uint64_t *vin, *vout;
+        CK(hipMalloc(&kin, N * 4));
+        CK(hipMalloc(&kout, N * 4));
+        CK(hipMalloc(&vin, N * 8));
+        CK(hipMalloc(&vout, N * 8));
+        CK(hipMemcpy(kin, hk.data(), N * 4, hipMemcpyHostToDevice));
+        size_t tmp_bytes = 0;
+        CK(hipcub::DeviceRadixSort::SortPairs(nullptr, tmp_bytes, kin, kout, vin, vout, (int)N, 0, 30));
+        void* tmp;
+        CK(hipMalloc(&tmp, tmp_bytes));
+        for (int bits : {16, 30}) {
+            timeit(bits == 16 ? "hipcub SortPairs u32/u64, 16 bits (14..30)" : "hipcub SortPairs u32/u64, 30 bits",
+                   [&] {
+                       size_t tb = tmp_bytes;
+                       CK(hipcub::DeviceRadixSort::SortPairs(tmp, tb, kin, kout, vin, vout, (int)N, 30 - bits, 30));
+                   });
+        }
+        uint32_t* vin32;
+        uint32_t* vout32;
+        CK(hipMalloc(&vin32, N * 4));
+        CK(hipMalloc(&vout32, N * 4));
+        timeit("hipcub SortPairs u32/u32, 16 bits", [&] {
+            size_t tb = tmp_bytes;
+            CK(hipcub::DeviceRadixSort::SortPairs(tmp, tb, kin, kout, vin32, vout32, (int)N, 14, 30));
+        });
+        timeit("hipcub SortKeys u32, 16 bits", [&] {
+            size_t tb = tmp_bytes;
+            CK(hipcub::DeviceRadixSort::SortKeys(tmp, tb, kin, kout, (int)N, 14, 30));
+        });
+    }
+    return 0;
+}

@@ -1,0 +1,116 @@
+"""GPU, multi-process: ShardGroup's full-range push path on the real HIP kernels.
+
+World 2 and 3 ranks share cuda:0, and the reduce-scatter runs over gloo. The
+default ShardGroup reduce-scatter under gloo copies the partial to the host,
+all_reduces it and copies the rank's chunk back. This exercises everything
+except RCCL itself: the piecewise pre-reduce with its [rank][row] row map, the
+padding rows of linearSplit's short last shard, the comm-stream ordering and
+the owner apply. RCCL needs one GPU per rank, so its reduce-scatter is covered
+only at world 1 (tests/test_gpu_parity.py) and by bench.py at N>1.
+
+Tolerance as in tests/test_group_gloo.py: fp32 within 2(n-1)2^-24 sum|terms| of
+the sequential oracle, and within 1e-6 relative (to sum|terms|) of the exact sum;
+int32 exact.
+"""
+import os
+import socket
+import sys
+
+import numpy as np
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+pytestmark = pytest.mark.gpu
+
+
+def _buckets(pyoracle, vt, rank, W, rows, cols):
+    # multipliers coprime with 1000: every push lists each row once, in a permuted order
+    return [pyoracle.synth_dense_bucket(0, vt, 0, rows, rows, cols, 100 * rank + b, (1, 3, 7, 9, 11)[b % 5], 13 * b)
+            for b in range(W)]
+
+
+def _init(vt, rows, cols):
+    rng = np.random.default_rng(5)
+    dt = {0: np.int32, 1: np.float32}[vt]
+    return (rng.integers(50, 60, size=(rows, cols)) if vt == 0 else rng.standard_normal((rows, cols))).astype(dt)
+
+
+def _worker(rank, world, port, vt, rows, cols, W, pieces, out_dir):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    sys.path[:0] = [ROOT, os.path.join(ROOT, "oracle")]
+    import torch
+    import torch.distributed as dist
+
+    import pyoracle
+    from distml_amd.datadesc import DataDesc
+    from distml_amd.group import ShardGroup
+
+    torch.cuda.set_device(0)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    fmt = DataDesc(1, 0, vt)
+    g = ShardGroup(fmt, rows, cols, rank, world, device=0, pieces=pieces)
+    sh = g.shard
+    g.store.load_values(_init(vt, rows, cols)[sh.firstKey:sh.lastKey + 1])
+    bufs = [torch.from_numpy(b).cuda() for b in _buckets(pyoracle, vt, rank, W, rows, cols)]
+    torch.cuda.synchronize()
+    pipelined = g.step_rows % pieces == 0
+    for _ in range(2):  # twice: the second step reuses the pooled pre-reduce workspace
+        g.push_full_range([b.data_ptr() for b in bufs], [b.numel() for b in bufs],
+                          torch.cuda.current_stream().cuda_stream)
+    g.flush()
+    np.save(os.path.join(out_dir, f"shard{rank}.npy"), g.store.values())
+    with open(os.path.join(out_dir, f"path{rank}.txt"), "w") as f:
+        f.write("pipelined" if pipelined else "plain")
+    g.store.close()
+    dist.destroy_process_group()
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+# (world, vt, rows, pieces): step_rows = ceil-ish linearSplit step
+#   2, 1000 rows -> step 500, pieces 4: pipelined, no padding
+#   3, 1000 rows -> step 334, pieces 2: pipelined, last shard 332 rows (2 padding rows)
+#   3, 1000 rows -> step 334, pieces 4: 334 % 4 != 0 -> one-shot pre-reduce path
+#   2, 1000 rows int32, pieces 4: exact
+@pytest.mark.parametrize("world,vt,rows,pieces,path", [(2, 1, 1000, 4, "pipelined"), (3, 1, 1000, 2, "pipelined"),
+                                                       (3, 1, 1000, 4, "plain"), (2, 0, 1000, 4, "pipelined")])
+def test_shard_group_hip_multiprocess(tmp_path, oracle, world, vt, rows, pieces, path):
+    import torch.multiprocessing as mp
+    cols, W = 67, 5
+    mp.spawn(_worker, args=(world, _free_port(), vt, rows, cols, W, pieces, str(tmp_path)), nprocs=world, join=True)
+    for r in range(world):
+        assert (tmp_path / f"path{r}.txt").read_text() == path
+    got = np.concatenate([np.load(tmp_path / f"shard{r}.npy") for r in range(world)]).reshape(rows, cols)
+    init = _init(vt, rows, cols)
+    o = oracle.OracleStore(1, 0, vt, 0, rows - 1, cols)
+    o.data[:] = init
+    all_b = [b for _ in range(2) for r in range(world) for b in _buckets(oracle, vt, r, W, rows, cols)]
+    for b in all_b:
+        assert o.push(b.tobytes()) == 0
+    if vt == 0:
+        assert np.array_equal(got, o.data)
+        return
+    terms = np.abs(init.astype(np.float64))
+    exact = init.astype(np.float64)
+    for b in all_b:
+        rec = b.reshape(rows, 4 + 4 * cols)
+        keys = rec[:, :4].copy().view("<i4").ravel()
+        g = rec[:, 4:].copy().view("<f4").astype(np.float64)
+        terms[keys] += np.abs(g)
+        exact[keys] += g
+    n = len(all_b) + 1
+    diff = np.abs(got.astype(np.float64) - o.data.astype(np.float64))
+    assert np.all(diff <= 2 * (n - 1) * 2.0 ** -24 * terms)
+    # north-star 1e-6 relative, against the exact sum: the sharded order rounds once at the
+    # shard value's magnitude, the sequential reference n-1 times, so the reference's own
+    # error dominates `diff` as n grows (at n = 31 it reaches ~1e-6 of sum|terms|)
+    err_ours = float(np.max(np.abs(got.astype(np.float64) - exact) / terms))
+    err_ref = float(np.max(np.abs(o.data.astype(np.float64) - exact) / terms))
+    assert err_ours <= 1e-6, (err_ours, err_ref)
+    assert err_ours <= err_ref + 2.0 ** -24, (err_ours, err_ref)

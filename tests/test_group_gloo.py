@@ -10,7 +10,11 @@ P_r is rank r's ordered partial, the reference as p0 + g_0 + g_1 + ... . For
 int32 the two are identical (exact, mod 2^32). For fp32 both orders are within
 Higham's recursive-summation bound of the exact sum, so
     |ours - oracle| <= 2 (n-1) 2^-24 sum|terms|,   n = number of terms,
-and the test also checks the north-star's 1e-6 relative bound against sum|terms|.
+and the test also checks the north-star's 1e-6 relative bound (to sum|terms|)
+against the exact sum. It does not check that bound against the oracle: with
+|init| >> |gradient| the sequential order rounds n-1 times at the shard value's
+magnitude and the sharded order once, so at n ~ 30 the reference's own error
+reaches 1e-6 of sum|terms| while ours stays near 2^-24.
 """
 import ctypes as C
 import os
@@ -132,11 +136,20 @@ def test_sharded_full_range_push_gloo(tmp_path, oracle, world, vt):
         assert np.array_equal(got, o.data)
         return
     terms = np.abs(init.astype(np.float64))
+    exact = init.astype(np.float64)
     for b in all_b:
         rec = b.reshape(rows, 4 + 4 * cols)
         keys = rec[:, :4].copy().view("<i4").ravel()
-        terms[keys] += np.abs(rec[:, 4:].copy().view("<f4").astype(np.float64))
+        g = rec[:, 4:].copy().view("<f4").astype(np.float64)
+        terms[keys] += np.abs(g)
+        exact[keys] += g
     n = len(all_b) + 1
     diff = np.abs(got.astype(np.float64) - o.data.astype(np.float64))
     assert np.all(diff <= 2 * (n - 1) * 2.0 ** -24 * terms)
-    assert float(np.max(diff / terms)) <= 1e-6
+    # north-star 1e-6 relative, against the exact sum: the sharded order rounds once at the
+    # shard value's magnitude, the sequential reference n-1 times, so the reference's own
+    # error dominates `diff` as n grows (at n = 31 it reaches ~1e-6 of sum|terms|)
+    err_ours = float(np.max(np.abs(got.astype(np.float64) - exact) / terms))
+    err_ref = float(np.max(np.abs(o.data.astype(np.float64) - exact) / terms))
+    assert err_ours <= 1e-6, (err_ours, err_ref)
+    assert err_ours <= err_ref + 2.0 ** -24, (err_ours, err_ref)
