@@ -8,6 +8,6 @@ from ._lib import NativeLibraryMissing, load as load_library  # noqa: F401
 from .datadesc import ALL, EMPTY, DataDesc, KeyCollection, KeyList, KeyRange  # noqa: F401
 from .store import (ArrayIndexOutOfBoundsException, DataStore, DistMLException, DMatrix,  # noqa: F401
                     IllegalArgumentException, IllegalStateException, Model, NativeError,
-                    encode_array_push, encode_matrix_push)
+                    encode_array_push, encode_matrix_push, pinned_empty)
 
 __version__ = "0.1.0"

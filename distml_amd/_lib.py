@@ -53,6 +53,10 @@ SIGNATURES = {
     "dml_store_fetch_range": (C.c_int, [_vp, _i64, _i64, _vp, _i64, _P(_i64)]),
     "dml_store_write_all": (C.c_int, [_vp, _vp, _i64, _P(_i64)]),
     "dml_store_read_all": (C.c_int, [_vp, _vp, _i64]),
+    "dml_store_sync_to": (C.c_int, [_vp, _i32, _i32, _vp, _i64, _P(_i64)]),
+    "dml_store_sync_from": (C.c_int, [_vp, _i32, _i32, _vp, _i64]),
+    "dml_host_alloc": (C.c_int, [_i64, _P(_vp)]),
+    "dml_host_free": (None, [_vp]),
     "dml_store_stream": (C.c_int, [_vp, _P(_vp)]),
     "dml_store_set_timing": (C.c_int, [_vp, _i32]),
     "dml_store_kernel_time": (C.c_int, [_vp, _P(C.c_double), _P(_i64), _i32]),

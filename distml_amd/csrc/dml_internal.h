@@ -118,7 +118,7 @@ hipError_t launch_fill(int vtype, void* p, int64_t n, double v, hipStream_t st);
 hipError_t launch_fill_f32(float* p, int64_t n, float v, hipStream_t st);
 hipError_t launch_apply_dense(int vtype, void* shard, const void* src, int64_t n, hipStream_t st);
 hipError_t launch_fetch(int vtype, const void* shard, const float* alpha, int32_t cols, const int64_t* keys,
-                        int64_t n, int64_t first, uint8_t* out, int64_t rec, int K, int value_slot,
+                        int64_t key_lo, int64_t n, int64_t first, uint8_t* out, int64_t rec, int K, int value_slot,
                         hipStream_t st);
 hipError_t launch_bswap(int V, const void* src, void* dst, int64_t n, hipStream_t st);
 hipError_t launch_synth_dense(uint8_t* out, int K, int vtype, int64_t first, int64_t shard_rows, int64_t nrec,
@@ -126,6 +126,35 @@ hipError_t launch_synth_dense(uint8_t* out, int K, int vtype, int64_t first, int
 hipError_t launch_synth_sparse(uint8_t* out, int K, int vtype, int value_stride, int64_t first,
                                int64_t key_space, int64_t nrec, uint64_t s0, uint64_t pa, uint64_t pc,
                                hipStream_t st);
+// ---- ordered sparse scatter-add (dml_sparse.hip), float / double array stores ----
+constexpr int kSpTile = 4096;      // records per partition tile (256 threads x 16)
+constexpr int kSpLeafCap = 2048;   // records one leaf sorts in LDS
+// Shape of one chunk's partition (host-computed, passed by value).
+struct SpPlan {
+    int64_t tile_base[kMaxW + 1];  // first level-1 tile of push b (prefix of ceil(nrec / kSpTile))
+    int64_t rec_base[kMaxW + 1];   // first sequence number of push b (prefix of nrec)
+    int64_t nrec, ntiles1, nleaves, max_tiles2;
+    int nb, SL, D2, nbins1;        // leaf = row >> SL; 2^D2 leaves per level-1 bin
+};
+// Device-side results of level 1 (bin bounds, level-2 tile table).
+struct SpMeta {
+    int64_t kept;                  // records before the cutoff
+    int64_t bin_start1[257];
+    int64_t tile_start2[257];
+};
+// Byte offsets of the partition buffers inside one workspace allocation.
+struct SpLayout {
+    size_t meta, comp1, val1, comp2, val2, cnt1, off1, cnt2, off2, leafflag, scan_tmp, scan_tmp_bytes, total;
+};
+SpPlan sparse_plan(const Batch& bt, int nb, int64_t rows);
+SpLayout sparse_layout(const SpPlan& pl, int vbytes);
+hipError_t launch_sparse_partition(int vtype, const Batch& bt, const SpPlan& pl, const SpLayout& l, uint8_t* ws,
+                                   int64_t stride, int K, int64_t first, int64_t rows, const Ctrl* ctrl,
+                                   uint64_t tail_cut, hipStream_t st);
+hipError_t launch_sparse_leaf(int vtype, void* shard, const SpPlan& pl, const SpLayout& l, uint8_t* ws, Ctrl* ctrl,
+                              const Ctrl* prev, hipStream_t st, LaunchEv ev);
+hipError_t sparse_replay(int vtype, void* shard, const SpPlan& pl, const SpLayout& l, uint8_t* ws, hipStream_t st);
+
 hipError_t launch_stream(bool copy, void* dst, const void* src, int64_t n16, hipStream_t st, LaunchEv ev);
 hipError_t launch_synth_fill(int vtype, void* p, int64_t n, uint64_t s0, hipStream_t st);
 hipError_t launch_key_rows(const uint8_t* base, int64_t nrec, int64_t stride, int K, int64_t first, int64_t rows,

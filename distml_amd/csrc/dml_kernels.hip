@@ -15,7 +15,7 @@
 //                   DoubleArrayStore.java:115-127), one launch per push
 //   k_fetch, k_bswap, k_fill, k_apply_dense, k_synth_*  — fetch / checkpoint /
 //                   init / owner-apply / synthetic data.
-#include "dml_internal.h"
+#include "dml_device.h"
 
 #include <hip/hip_ext.h>
 
@@ -25,24 +25,6 @@
 
 namespace dml {
 
-typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
-typedef u32x4 u32x4_u __attribute__((aligned(4)));  // records are 4-byte aligned only
-typedef int32_t i32x8 __attribute__((ext_vector_type(8)));
-typedef uint64_t u64x8 __attribute__((ext_vector_type(8)));
-
-// Loads through the global address space: bucket pointers come out of the
-// kernarg table as generic pointers, and flat loads would force vmcnt(0)+lgkmcnt(0)
-// waits (flat returns out of order).
-#define DML_GLOBAL __attribute__((address_space(1)))
-__device__ inline u32x4 ldg16(const uint8_t* p) { return *(const DML_GLOBAL u32x4_u*)(p); }
-__device__ inline uint32_t ldg32(const uint8_t* p) { return *(const DML_GLOBAL uint32_t*)(p); }
-// Streamed-once bucket bytes: non-temporal policy (no L2 retention).
-__device__ inline u32x4 ldg16_nt(const uint8_t* p) {
-    return __builtin_nontemporal_load((const DML_GLOBAL u32x4_u*)(p));
-}
-__device__ inline void stg16_nt(void* p, u32x4 v) { __builtin_nontemporal_store(v, (DML_GLOBAL u32x4_u*)(p)); }
-__device__ inline void stg16(void* p, u32x4 v) { *(DML_GLOBAL u32x4_u*)(p) = v; }
-
 __host__ __device__ inline uint64_t splitmix64_dev(uint64_t x) {
     uint64_t z = x + 0x9E3779B97F4A7C15ull;
     z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
@@ -50,41 +32,6 @@ __host__ __device__ inline uint64_t splitmix64_dev(uint64_t x) {
     return z ^ (z >> 31);
 }
 uint64_t splitmix64(uint64_t x) { return splitmix64_dev(x); }
-
-__device__ inline uint32_t ld32(const uint8_t* p) { return ldg32(p); }
-__device__ inline int64_t ld_key(const uint8_t* p, int K) {
-    // DataDesc.readKey (DataDesc.java:131-138): LE int32 sign-extended, or LE int64.
-    if (K == 4) return (int64_t)(int32_t)ld32(p);
-    return (int64_t)((uint64_t)ld32(p) | ((uint64_t)ld32(p + 4) << 32));
-}
-// KeyRange indexOf: (int)(key - firstKey) (FloatMatrixStore.java:176-179); -1 if
-// localData[index] would throw ArrayIndexOutOfBoundsException.
-__device__ inline int64_t row_index(int64_t key, int64_t first, int64_t rows) {
-    int32_t idx = (int32_t)(uint32_t)((uint64_t)key - (uint64_t)first);
-    return (idx < 0 || (int64_t)idx >= rows) ? -1 : (int64_t)idx;
-}
-
-template <typename T> struct Elem;
-template <> struct Elem<float> {
-    static constexpr int VEC = 4;
-    __device__ static float from_bits(uint32_t lo, uint32_t) { return __uint_as_float(lo); }
-    __device__ static float load(const uint8_t* p) { return __uint_as_float(ld32(p)); }
-    __device__ static float add(float a, float b) { return __fadd_rn(a, b); }
-};
-template <> struct Elem<int32_t> {
-    static constexpr int VEC = 4;
-    __device__ static int32_t from_bits(uint32_t lo, uint32_t) { return (int32_t)lo; }
-    __device__ static int32_t load(const uint8_t* p) { return (int32_t)ld32(p); }
-    __device__ static int32_t add(int32_t a, int32_t b) { return (int32_t)((uint32_t)a + (uint32_t)b); }
-};
-template <> struct Elem<double> {
-    static constexpr int VEC = 2;
-    __device__ static double from_bits(uint32_t lo, uint32_t hi) {
-        return __longlong_as_double((long long)((uint64_t)lo | ((uint64_t)hi << 32)));
-    }
-    __device__ static double load(const uint8_t* p) { return from_bits(ld32(p), ld32(p + 4)); }
-    __device__ static double add(double a, double b) { return __dadd_rn(a, b); }
-};
 
 template <typename T>
 __device__ inline void unpack(const u32x4& r, T* o) {
@@ -762,13 +709,13 @@ __device__ inline void st32(uint8_t* p, uint32_t v) { *(uint32_t*)p = v; }
 
 template <typename T>
 __global__ void k_fetch(const T* __restrict__ shard, const float* __restrict__ alpha, int32_t cols,
-                        const int64_t* __restrict__ keys, int64_t n, int64_t first, uint8_t* __restrict__ out,
-                        int64_t rec, int K, int value_slot) {
+                        const int64_t* __restrict__ keys, int64_t key_lo, int64_t n, int64_t first,
+                        uint8_t* __restrict__ out, int64_t rec, int K, int value_slot) {
     const int64_t total = n * (int64_t)cols;
     for (int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; t < total; t += (int64_t)gridDim.x * blockDim.x) {
         const int64_t j = t / cols;
         const int32_t c = (int32_t)(t - j * cols);
-        const int64_t key = keys[j];
+        const int64_t key = keys ? keys[j] : key_lo + j;
         const int64_t idx = key - first;
         uint8_t* o = out + j * rec;
         if (c == 0) {
@@ -784,16 +731,18 @@ __global__ void k_fetch(const T* __restrict__ shard, const float* __restrict__ a
             st32(v, (uint32_t)u); st32(v + 4, (uint32_t)(u >> 32));
         }
         if (alpha) st32(v + 4, __float_as_uint(alpha[idx * cols + c]));
+        else if (sizeof(T) == 4 && value_slot == 8) st32(v + 4, 0u);  // FloatArrayStore's zero pad
     }
 }
-hipError_t launch_fetch(int vtype, const void* shard, const float* alpha, int32_t cols, const int64_t* keys, int64_t n,
-                        int64_t first, uint8_t* out, int64_t rec, int K, int value_slot, hipStream_t st) {
+hipError_t launch_fetch(int vtype, const void* shard, const float* alpha, int32_t cols, const int64_t* keys,
+                        int64_t key_lo, int64_t n, int64_t first, uint8_t* out, int64_t rec, int K, int value_slot,
+                        hipStream_t st) {
     const int64_t total = n * (int64_t)cols;
     if (total <= 0) return hipSuccess;
     const dim3 g(grid_for(total));
-    if (vtype == kF32) hipLaunchKernelGGL(k_fetch<float>, g, dim3(256), 0, st, (const float*)shard, alpha, cols, keys, n, first, out, rec, K, value_slot);
-    else if (vtype == kI32) hipLaunchKernelGGL(k_fetch<int32_t>, g, dim3(256), 0, st, (const int32_t*)shard, alpha, cols, keys, n, first, out, rec, K, value_slot);
-    else hipLaunchKernelGGL(k_fetch<double>, g, dim3(256), 0, st, (const double*)shard, alpha, cols, keys, n, first, out, rec, K, value_slot);
+    if (vtype == kF32) hipLaunchKernelGGL(k_fetch<float>, g, dim3(256), 0, st, (const float*)shard, alpha, cols, keys, key_lo, n, first, out, rec, K, value_slot);
+    else if (vtype == kI32) hipLaunchKernelGGL(k_fetch<int32_t>, g, dim3(256), 0, st, (const int32_t*)shard, alpha, cols, keys, key_lo, n, first, out, rec, K, value_slot);
+    else hipLaunchKernelGGL(k_fetch<double>, g, dim3(256), 0, st, (const double*)shard, alpha, cols, keys, key_lo, n, first, out, rec, K, value_slot);
     return hipGetLastError();
 }
 

@@ -1,0 +1,513 @@
+// dml_sparse.hip — ordered sparse scatter-add for the float / double array stores
+// (FloatArrayStore.java:380-392, DoubleArrayStore.java:115-127) over a chunk of
+// pushes, without atomics on the shard.
+//
+// The reference adds record after record: per shard element, the adds land in
+// (push, record) order. Here every kept record becomes (comp, value) with
+// comp = row << 32 | seq, seq = its (push, record) rank in the chunk. Records are
+// partitioned by "leaf" = row >> SL (a key range holding ~1 K records on
+// average) with two 256-way digit passes (count -> exclusive scan -> scatter,
+// like one radix pass each; no ordering needed, seq travels along). A leaf
+// kernel then groups its records by row in LDS hash chains and applies each
+// row once: v = shard[row]; v += u_1; v += u_2 ... in sequence order;
+// shard[row] = v. That is the reference's value bit for bit, also when one push
+// repeats a key. A leaf's shard accesses stay inside one small row range
+// (DRAM-page friendly), which is what makes this faster than per-push scattered
+// atomics over the whole shard (scripts/ubench_scatter.hip).
+//
+// Records at or past the chunk's cutoff (first key outside the shard / first
+// truncated access, found by k_array_validate) are dropped at partition time.
+// A leaf with more than kSpLeafCap records (skewed keys) is not applied by the
+// leaf kernel: it is flagged, Ctrl::no_dup is cleared, and the host replays the
+// flagged leaves from a full device sort of the chunk (sparse_replay).
+#include "dml_device.h"
+
+#include <hip/hip_ext.h>
+#include <hipcub/hipcub.hpp>
+
+#include <algorithm>
+
+namespace dml {
+
+namespace {
+
+// First partition tile of push b: scalar scan of the (<= 64) prefix entries.
+__device__ inline int push_of_tile(const SpPlan& pl, int64_t tile) {
+    int b = 0;
+    while (b + 1 < pl.nb && pl.tile_base[b + 1] <= tile) ++b;
+    return b;
+}
+
+// Records [lo, hi) of the chunk-wide first-level bin b: tile t of the bin, or
+// (-1) when this block has no tile. Second-level tiles enumerate bins in order.
+struct Tile2 {
+    int bin;
+    int64_t t, ntiles, lo, hi;
+};
+__device__ inline Tile2 tile2_of(const SpMeta* m, int nbins1, int64_t tile) {
+    Tile2 r{-1, 0, 0, 0, 0};
+    if (tile >= m->tile_start2[nbins1]) return r;
+    int lo = 0, hi = nbins1;  // largest b with tile_start2[b] <= tile
+    while (hi - lo > 1) {
+        const int mid = (lo + hi) >> 1;
+        if (m->tile_start2[mid] <= tile) lo = mid;
+        else hi = mid;
+    }
+    while (lo + 1 < nbins1 && m->tile_start2[lo + 1] <= tile) ++lo;  // skip empty bins
+    r.bin = lo;
+    r.t = tile - m->tile_start2[lo];
+    r.ntiles = m->tile_start2[lo + 1] - m->tile_start2[lo];
+    r.lo = m->bin_start1[lo] + r.t * kSpTile;
+    r.hi = min(r.lo + (int64_t)kSpTile, m->bin_start1[lo + 1]);
+    return r;
+}
+
+}  // namespace
+
+// ---- level 1: first digit of the leaf, straight from the wire records -------
+template <typename T, bool SCATTER>
+__global__ __launch_bounds__(256) void k_sp_level1(const Batch bt, const SpPlan pl, int64_t stride, int K,
+                                                   int64_t first, int64_t rows, const Ctrl* __restrict__ ctrl,
+                                                   uint64_t tail_cut, uint32_t* __restrict__ cnt1,
+                                                   const uint32_t* __restrict__ off1, uint64_t* __restrict__ comp,
+                                                   T* __restrict__ val) {
+    __shared__ uint32_t h[256];
+    const int tid = threadIdx.x;
+    const int64_t tile = blockIdx.x;
+    const int b = push_of_tile(pl, tile);
+    h[tid] = SCATTER ? (tid < pl.nbins1 ? off1[(int64_t)tid * pl.ntiles1 + tile] : 0u) : 0u;
+    __syncthreads();
+    uint64_t cut = ctrl->cutoff;
+    if (tail_cut < cut) cut = tail_cut;
+    const int64_t r0 = (tile - pl.tile_base[b]) * kSpTile + tid;
+    const int64_t n = bt.nrec[b];
+    const uint8_t* base = bt.base[b];
+    constexpr int kPer = kSpTile / 256;
+    int64_t key[kPer];
+#pragma unroll
+    for (int i = 0; i < kPer; ++i) {  // all key loads in flight first
+        const int64_t r = r0 + i * 256;
+        key[i] = r < n ? ld_key(base + r * stride, K) : first;
+    }
+    T u[kPer];
+    if constexpr (SCATTER) {
+#pragma unroll
+        for (int i = 0; i < kPer; ++i) {
+            const int64_t r = r0 + i * 256;
+            u[i] = r < n ? Elem<T>::load(base + r * stride + K) : T(0);
+        }
+    }
+#pragma unroll
+    for (int i = 0; i < kPer; ++i) {
+        const int64_t r = r0 + i * 256;
+        if (r >= n || pos_of((uint64_t)bt.bidx[b], (uint64_t)(r * stride)) >= cut) continue;
+        const int64_t row = row_index(key[i], first, rows);  // in range: positions before the cutoff are valid
+        const uint32_t bin = (uint32_t)((row >> pl.SL) >> pl.D2);
+        if constexpr (SCATTER) {
+            const uint32_t p = atomicAdd(&h[bin], 1u);
+            comp[p] = ((uint64_t)row << 32) | (uint64_t)(pl.rec_base[b] + r);
+            val[p] = u[i];
+        } else {
+            atomicAdd(&h[bin], 1u);
+        }
+    }
+    if constexpr (!SCATTER) {
+        __syncthreads();
+        if (tid < pl.nbins1) cnt1[(int64_t)tid * pl.ntiles1 + tile] = h[tid];
+    }
+}
+
+// ---- between the levels: bin bounds and the second-level tile table ---------
+__global__ __launch_bounds__(256) void k_sp_plan2(const SpPlan pl, const uint32_t* __restrict__ cnt1,
+                                                  const uint32_t* __restrict__ off1, SpMeta* __restrict__ m) {
+    const int64_t cells = (int64_t)pl.nbins1 * pl.ntiles1;
+    const int64_t kept = cells ? (int64_t)off1[cells - 1] + cnt1[cells - 1] : 0;
+    for (int b = threadIdx.x; b < pl.nbins1; b += blockDim.x) m->bin_start1[b] = off1[(int64_t)b * pl.ntiles1];
+    if (threadIdx.x == 0) {
+        m->bin_start1[pl.nbins1] = kept;
+        m->kept = kept;
+    }
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        int64_t acc = 0;
+        for (int b = 0; b < pl.nbins1; ++b) {
+            m->tile_start2[b] = acc;
+            acc += (m->bin_start1[b + 1] - m->bin_start1[b] + kSpTile - 1) / kSpTile;
+        }
+        m->tile_start2[pl.nbins1] = acc;
+    }
+}
+
+// ---- level 2: second digit, within each first-level bin ---------------------
+template <typename T, bool SCATTER>
+__global__ __launch_bounds__(256) void k_sp_level2(const SpPlan pl, const SpMeta* __restrict__ m,
+                                                   uint32_t* __restrict__ cnt2, const uint32_t* __restrict__ off2,
+                                                   const uint64_t* __restrict__ comp_in, const T* __restrict__ val_in,
+                                                   uint64_t* __restrict__ comp_out, T* __restrict__ val_out) {
+    __shared__ uint32_t h[256];
+    const int tid = threadIdx.x;
+    const Tile2 tl = tile2_of(m, pl.nbins1, blockIdx.x);
+    if (tl.bin < 0) return;  // uniform: spare block of the upper-bound grid
+    const int nd = 1 << pl.D2;
+    const int64_t cell0 = (m->tile_start2[tl.bin] << pl.D2) + tl.t;  // + d * ntiles
+    h[tid] = SCATTER ? (tid < nd ? off2[cell0 + (int64_t)tid * tl.ntiles] : 0u) : 0u;
+    __syncthreads();
+    const uint32_t mask = (uint32_t)nd - 1u;
+    constexpr int kPer = kSpTile / 256;
+    uint64_t c[kPer];
+#pragma unroll
+    for (int i = 0; i < kPer; ++i) {
+        const int64_t j = tl.lo + i * 256 + tid;
+        c[i] = j < tl.hi ? comp_in[j] : 0;
+    }
+    T u[kPer];
+    if constexpr (SCATTER) {
+#pragma unroll
+        for (int i = 0; i < kPer; ++i) {
+            const int64_t j = tl.lo + i * 256 + tid;
+            u[i] = j < tl.hi ? val_in[j] : T(0);
+        }
+    }
+#pragma unroll
+    for (int i = 0; i < kPer; ++i) {
+        const int64_t j = tl.lo + i * 256 + tid;
+        if (j >= tl.hi) continue;
+        const uint32_t d = (uint32_t)(c[i] >> (32 + pl.SL)) & mask;
+        if constexpr (SCATTER) {
+            const uint32_t p = atomicAdd(&h[d], 1u);
+            comp_out[p] = c[i];
+            val_out[p] = u[i];
+        } else {
+            atomicAdd(&h[d], 1u);
+        }
+    }
+    if constexpr (!SCATTER) {
+        __syncthreads();
+        if (tid < nd) cnt2[cell0 + (int64_t)tid * tl.ntiles] = h[tid];
+    }
+}
+
+// First record of leaf L in the leaf-ordered arrays (L == nleaves: records kept).
+__device__ inline int64_t leaf_start(const SpPlan& pl, const SpMeta* m, const uint32_t* off2, int64_t L) {
+    if (L >= pl.nleaves) return m->kept;
+    const int b = (int)(L >> pl.D2);
+    const int64_t d = L & ((1 << pl.D2) - 1);
+    const int64_t nt = m->tile_start2[b + 1] - m->tile_start2[b];
+    return nt ? (int64_t)off2[(m->tile_start2[b] << pl.D2) + d * nt] : m->bin_start1[b];
+}
+
+// ---- leaf: per-row ownership through LDS hash chains, ordered apply ----------
+// Records of the leaf go into kSpHash chains keyed by a hash of the row. A
+// record owns its row when no record of the same row has a smaller comp (=
+// earlier sequence). Owners of single-record rows (almost all) issue their
+// shard loads together and add once; owners of repeated rows walk their chain
+// in ascending comp order (the reference's record order) adding each value.
+// Chains longer than kSpChainMax (adversarial keys) send the whole leaf to the
+// exact replay instead, before any of its rows is written.
+constexpr int kSpHash = 4096;
+constexpr int kSpChainMax = 64;
+
+__device__ inline uint32_t sp_hash(uint64_t row) { return ((uint32_t)row * 0x9E3779B1u) >> (32 - 12); }
+static_assert(kSpHash == 1 << 12, "sp_hash yields 12 bits");
+
+template <typename T>
+__global__ __launch_bounds__(256) void k_sp_leaf(T* __restrict__ shard, const SpPlan pl, const SpMeta* __restrict__ m,
+                                                 const uint32_t* __restrict__ off2, const uint64_t* __restrict__ comp,
+                                                 const T* __restrict__ val, uint8_t* __restrict__ leafflag,
+                                                 Ctrl* __restrict__ ctrl, const Ctrl* __restrict__ prev) {
+    __shared__ uint32_t head[kSpHash];
+    __shared__ uint16_t nxt[kSpLeafCap];
+    __shared__ uint64_t sc[kSpLeafCap];
+    __shared__ T sv[kSpLeafCap];
+    __shared__ int s_over;
+    if (prev && ctrl_abnormal(prev)) return;  // predecessor needs the host first
+    const int tid = threadIdx.x;
+    const int64_t L = blockIdx.x;
+    const int64_t lo = leaf_start(pl, m, off2, L), hi = leaf_start(pl, m, off2, L + 1);
+    const int n = (int)(hi - lo);
+    if (hi - lo <= 0) return;
+    if (hi - lo > kSpLeafCap) {  // skewed leaf: exact replay on the host's request
+        if (tid == 0) {
+            leafflag[L] = 1;
+            atomicAnd(&ctrl->no_dup, 0u);
+        }
+        return;
+    }
+    constexpr int kPer = kSpLeafCap / 256;
+    for (int i = tid; i < kSpHash; i += 256) head[i] = 0xFFFFFFFFu;
+    if (tid == 0) s_over = 0;
+    uint64_t c[kPer];
+#pragma unroll
+    for (int k = 0; k < kPer; ++k) {
+        const int i = tid + k * 256;
+        c[k] = i < n ? comp[lo + i] : 0;
+        if (i < n) {
+            sc[i] = c[k];
+            sv[i] = val[lo + i];
+        }
+    }
+    __syncthreads();
+#pragma unroll
+    for (int k = 0; k < kPer; ++k) {
+        const int i = tid + k * 256;
+        if (i < n) nxt[i] = (uint16_t)atomicExch(&head[sp_hash(c[k] >> 32)], (uint32_t)i);
+    }
+    __syncthreads();
+    bool own[kPer], multi[kPer];
+#pragma unroll
+    for (int k = 0; k < kPer; ++k) {
+        const int i = tid + k * 256;
+        own[k] = multi[k] = false;
+        if (i >= n) continue;
+        const uint64_t row = c[k] >> 32;
+        int len = 0;
+        bool first = true, dup = false;
+        for (uint32_t j = head[sp_hash(row)]; j < (uint32_t)kSpLeafCap; j = nxt[j]) {
+            ++len;
+            if ((int)j != i && (sc[j] >> 32) == row) {
+                dup = true;
+                first &= sc[j] > c[k];
+            }
+        }
+        if (len > kSpChainMax) s_over = 1;
+        own[k] = first;
+        multi[k] = dup;
+    }
+    __syncthreads();
+    if (s_over) {  // uniform
+        if (tid == 0) {
+            leafflag[L] = 1;
+            atomicAnd(&ctrl->no_dup, 0u);
+        }
+        return;
+    }
+    T cur[kPer];
+#pragma unroll
+    for (int k = 0; k < kPer; ++k)  // every owner's shard load in flight together
+        if (own[k]) cur[k] = shard[c[k] >> 32];
+#pragma unroll
+    for (int k = 0; k < kPer; ++k) {
+        if (!own[k]) continue;
+        const int i = tid + k * 256;
+        const uint64_t row = c[k] >> 32;
+        T v = cur[k];
+        if (!multi[k]) {
+            v = Elem<T>::add(v, sv[i]);
+        } else {
+            // this row's records in ascending comp (= sequence) order
+            uint64_t last = 0;
+            bool started = false;
+            for (;;) {
+                uint64_t best = ~0ull;
+                int bj = -1;
+                for (uint32_t j = head[sp_hash(row)]; j < (uint32_t)kSpLeafCap; j = nxt[j]) {
+                    const uint64_t cj = sc[j];
+                    if ((cj >> 32) == row && (!started || cj > last) && cj < best) {
+                        best = cj;
+                        bj = (int)j;
+                    }
+                }
+                if (bj < 0) break;
+                v = Elem<T>::add(v, sv[bj]);
+                last = best;
+                started = true;
+            }
+        }
+        shard[row] = v;
+    }
+}
+
+// Replay of flagged leaves from the fully sorted chunk (comp ascending).
+template <typename T>
+__global__ __launch_bounds__(256) void k_sp_runs(T* __restrict__ shard, const uint64_t* __restrict__ comp,
+                                                 const T* __restrict__ val, int64_t n, int SL,
+                                                 const uint8_t* __restrict__ leafflag) {
+    const int64_t p = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (p >= n) return;
+    const uint64_t row = comp[p] >> 32;
+    if (!leafflag[row >> SL]) return;
+    if (p > 0 && (comp[p - 1] >> 32) == row) return;
+    T v = shard[row];
+    for (int64_t q = p; q < n && (comp[q] >> 32) == row; ++q) v = Elem<T>::add(v, val[q]);
+    shard[row] = v;
+}
+
+// ---- host side ----------------------------------------------------------------
+static int ceil_log2(int64_t x) {
+    int r = 0;
+    while ((int64_t)1 << r < x) ++r;
+    return r;
+}
+
+SpPlan sparse_plan(const Batch& bt, int nb, int64_t rows) {
+    SpPlan pl{};
+    pl.nb = nb;
+    int64_t nrec = 0, ntiles = 0;
+    for (int b = 0; b < nb; ++b) {
+        pl.tile_base[b] = ntiles;
+        pl.rec_base[b] = nrec;
+        ntiles += (bt.nrec[b] + kSpTile - 1) / kSpTile;
+        nrec += bt.nrec[b];
+    }
+    pl.tile_base[nb] = ntiles;
+    pl.rec_base[nb] = nrec;
+    pl.ntiles1 = ntiles;
+    pl.nrec = nrec;
+    // leaves of ~kSpLeafCap/2 records on average, at most 65536 (two 256-way digits)
+    const double span = (double)(kSpLeafCap / 2) * (double)rows / (double)std::max<int64_t>(nrec, 1);
+    int SL = 0;
+    while (SL < 31 && (double)((int64_t)1 << (SL + 1)) <= span) ++SL;
+    while (SL < 31 && ((rows + ((int64_t)1 << SL) - 1) >> SL) > 65536) ++SL;
+    pl.SL = SL;
+    pl.nleaves = (rows + ((int64_t)1 << SL) - 1) >> SL;
+    pl.D2 = std::min(8, ceil_log2(pl.nleaves));
+    pl.nbins1 = (int)((pl.nleaves + ((int64_t)1 << pl.D2) - 1) >> pl.D2);
+    pl.max_tiles2 = (nrec + kSpTile - 1) / kSpTile + pl.nbins1;
+    return pl;
+}
+
+SpLayout sparse_layout(const SpPlan& pl, int vbytes) {
+    SpLayout l{};
+    auto take = [&](size_t bytes) {
+        const size_t o = l.total;
+        l.total += (bytes + 255) & ~(size_t)255;
+        return o;
+    };
+    const size_t n = (size_t)std::max<int64_t>(pl.nrec, 1);
+    const size_t cells1 = (size_t)pl.nbins1 * (size_t)pl.ntiles1 + 1;
+    const size_t cells2 = ((size_t)pl.max_tiles2 << pl.D2) + 1;
+    l.meta = take(sizeof(SpMeta));
+    l.comp1 = take(n * 8);
+    l.val1 = take(n * (size_t)vbytes);
+    l.comp2 = take(n * 8);
+    l.val2 = take(n * (size_t)vbytes);
+    l.cnt1 = take(cells1 * 4);
+    l.off1 = take(cells1 * 4);
+    l.cnt2 = take(cells2 * 4);
+    l.off2 = take(cells2 * 4);
+    l.leafflag = take((size_t)pl.nleaves);
+    size_t t1 = 0, t2 = 0;
+    (void)hipcub::DeviceScan::ExclusiveSum(nullptr, t1, (uint32_t*)nullptr, (uint32_t*)nullptr, (int)cells1);
+    (void)hipcub::DeviceScan::ExclusiveSum(nullptr, t2, (uint32_t*)nullptr, (uint32_t*)nullptr, (int)cells2);
+    l.scan_tmp_bytes = std::max(t1, t2);
+    l.scan_tmp = take(l.scan_tmp_bytes);
+    return l;
+}
+
+template <typename T>
+static hipError_t partition_t(const Batch& bt, const SpPlan& pl, const SpLayout& l, uint8_t* ws, int64_t stride,
+                              int K, int64_t first, int64_t rows, const Ctrl* ctrl, uint64_t tail_cut,
+                              hipStream_t st) {
+    SpMeta* m = (SpMeta*)(ws + l.meta);
+    uint64_t* comp1 = (uint64_t*)(ws + l.comp1);
+    uint64_t* comp2 = (uint64_t*)(ws + l.comp2);
+    T* val1 = (T*)(ws + l.val1);
+    T* val2 = (T*)(ws + l.val2);
+    uint32_t* cnt1 = (uint32_t*)(ws + l.cnt1);
+    uint32_t* off1 = (uint32_t*)(ws + l.off1);
+    uint32_t* cnt2 = (uint32_t*)(ws + l.cnt2);
+    uint32_t* off2 = (uint32_t*)(ws + l.off2);
+    const int cells1 = (int)((int64_t)pl.nbins1 * pl.ntiles1 + 1);
+    const int cells2 = (int)((pl.max_tiles2 << pl.D2) + 1);
+    hipError_t e = hipMemsetAsync(ws + l.leafflag, 0, (size_t)pl.nleaves, st);
+    if (e == hipSuccess) e = hipMemsetAsync(cnt1, 0, (size_t)cells1 * 4, st);
+    if (e == hipSuccess) e = hipMemsetAsync(cnt2, 0, (size_t)cells2 * 4, st);
+    if (e != hipSuccess) return e;
+    if (pl.ntiles1 > 0) {
+        hipLaunchKernelGGL((k_sp_level1<T, false>), dim3((unsigned)pl.ntiles1), dim3(256), 0, st, bt, pl, stride, K,
+                           first, rows, ctrl, tail_cut, cnt1, (const uint32_t*)nullptr, (uint64_t*)nullptr, (T*)nullptr);
+        if ((e = hipGetLastError()) != hipSuccess) return e;
+    }
+    size_t tb = l.scan_tmp_bytes;
+    if ((e = hipcub::DeviceScan::ExclusiveSum(ws + l.scan_tmp, tb, cnt1, off1, cells1, st)) != hipSuccess) return e;
+    if (pl.ntiles1 > 0) {
+        hipLaunchKernelGGL((k_sp_level1<T, true>), dim3((unsigned)pl.ntiles1), dim3(256), 0, st, bt, pl, stride, K,
+                           first, rows, ctrl, tail_cut, (uint32_t*)nullptr, (const uint32_t*)off1, comp1, val1);
+        if ((e = hipGetLastError()) != hipSuccess) return e;
+    }
+    hipLaunchKernelGGL(k_sp_plan2, dim3(1), dim3(256), 0, st, pl, (const uint32_t*)cnt1, (const uint32_t*)off1, m);
+    if ((e = hipGetLastError()) != hipSuccess) return e;
+    if (pl.max_tiles2 > 0) {
+        hipLaunchKernelGGL((k_sp_level2<T, false>), dim3((unsigned)pl.max_tiles2), dim3(256), 0, st, pl,
+                           (const SpMeta*)m, cnt2, (const uint32_t*)nullptr, (const uint64_t*)comp1, (const T*)val1,
+                           (uint64_t*)nullptr, (T*)nullptr);
+        if ((e = hipGetLastError()) != hipSuccess) return e;
+    }
+    tb = l.scan_tmp_bytes;
+    if ((e = hipcub::DeviceScan::ExclusiveSum(ws + l.scan_tmp, tb, cnt2, off2, cells2, st)) != hipSuccess) return e;
+    if (pl.max_tiles2 > 0) {
+        hipLaunchKernelGGL((k_sp_level2<T, true>), dim3((unsigned)pl.max_tiles2), dim3(256), 0, st, pl,
+                           (const SpMeta*)m, (uint32_t*)nullptr, (const uint32_t*)off2, (const uint64_t*)comp1,
+                           (const T*)val1, comp2, val2);
+        if ((e = hipGetLastError()) != hipSuccess) return e;
+    }
+    return hipSuccess;
+}
+
+hipError_t launch_sparse_partition(int vtype, const Batch& bt, const SpPlan& pl, const SpLayout& l, uint8_t* ws,
+                                   int64_t stride, int K, int64_t first, int64_t rows, const Ctrl* ctrl,
+                                   uint64_t tail_cut, hipStream_t st) {
+    if (vtype == kF32) return partition_t<float>(bt, pl, l, ws, stride, K, first, rows, ctrl, tail_cut, st);
+    if (vtype == kF64) return partition_t<double>(bt, pl, l, ws, stride, K, first, rows, ctrl, tail_cut, st);
+    return hipErrorInvalidValue;
+}
+
+hipError_t launch_sparse_leaf(int vtype, void* shard, const SpPlan& pl, const SpLayout& l, uint8_t* ws, Ctrl* ctrl,
+                              const Ctrl* prev, hipStream_t st, LaunchEv ev) {
+    if (pl.nleaves <= 0) return hipSuccess;
+    const SpMeta* m = (const SpMeta*)(ws + l.meta);
+    const uint32_t* off2 = (const uint32_t*)(ws + l.off2);
+    const uint64_t* comp2 = (const uint64_t*)(ws + l.comp2);
+    uint8_t* flag = ws + l.leafflag;
+    const dim3 grid((unsigned)pl.nleaves);
+    if (vtype == kF32)
+        hipExtLaunchKernelGGL(k_sp_leaf<float>, grid, dim3(256), 0, st, ev.start, ev.stop, 0, (float*)shard, pl, m,
+                              off2, comp2, (const float*)(ws + l.val2), flag, ctrl, prev);
+    else if (vtype == kF64)
+        hipExtLaunchKernelGGL(k_sp_leaf<double>, grid, dim3(256), 0, st, ev.start, ev.stop, 0, (double*)shard, pl, m,
+                              off2, comp2, (const double*)(ws + l.val2), flag, ctrl, prev);
+    else
+        return hipErrorInvalidValue;
+    return hipGetLastError();
+}
+
+// Flagged (oversized) leaves, exactly: sort every kept record by (row, seq) and
+// run-apply the rows of flagged leaves. Synchronous; a rare path (skewed keys).
+hipError_t sparse_replay(int vtype, void* shard, const SpPlan& pl, const SpLayout& l, uint8_t* ws, hipStream_t st) {
+    SpMeta hm;
+    hipError_t e = hipMemcpyAsync(&hm, ws + l.meta, sizeof hm, hipMemcpyDeviceToHost, st);
+    if (e == hipSuccess) e = hipStreamSynchronize(st);
+    if (e != hipSuccess || hm.kept <= 0) return e;
+    const int n = (int)hm.kept;
+    uint64_t* kin = (uint64_t*)(ws + l.comp2);
+    uint64_t* kout = (uint64_t*)(ws + l.comp1);
+    size_t tmp = 0;
+    void* dtmp = nullptr;
+    if (vtype == kF32) {
+        uint32_t* vin = (uint32_t*)(ws + l.val2);
+        uint32_t* vout = (uint32_t*)(ws + l.val1);
+        e = hipcub::DeviceRadixSort::SortPairs(nullptr, tmp, kin, kout, vin, vout, n, 0, 64, st);
+        if (e == hipSuccess) e = hipMallocAsync(&dtmp, tmp, st);
+        if (e == hipSuccess) e = hipcub::DeviceRadixSort::SortPairs(dtmp, tmp, kin, kout, vin, vout, n, 0, 64, st);
+        if (e == hipSuccess)
+            hipLaunchKernelGGL(k_sp_runs<float>, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, st, (float*)shard,
+                               (const uint64_t*)kout, (const float*)vout, (int64_t)n, pl.SL,
+                               (const uint8_t*)(ws + l.leafflag));
+    } else {
+        uint64_t* vin = (uint64_t*)(ws + l.val2);
+        uint64_t* vout = (uint64_t*)(ws + l.val1);
+        e = hipcub::DeviceRadixSort::SortPairs(nullptr, tmp, kin, kout, vin, vout, n, 0, 64, st);
+        if (e == hipSuccess) e = hipMallocAsync(&dtmp, tmp, st);
+        if (e == hipSuccess) e = hipcub::DeviceRadixSort::SortPairs(dtmp, tmp, kin, kout, vin, vout, n, 0, 64, st);
+        if (e == hipSuccess)
+            hipLaunchKernelGGL(k_sp_runs<double>, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, st, (double*)shard,
+                               (const uint64_t*)kout, (const double*)vout, (int64_t)n, pl.SL,
+                               (const uint8_t*)(ws + l.leafflag));
+    }
+    if (e == hipSuccess) e = hipGetLastError();
+    if (dtmp) (void)hipFreeAsync(dtmp, st);
+    const hipError_t s2 = hipStreamSynchronize(st);
+    return e != hipSuccess ? e : s2;
+}
+
+}  // namespace dml

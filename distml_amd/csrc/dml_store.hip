@@ -24,6 +24,7 @@
 #include <mutex>
 #include <string>
 #include <unordered_map>
+#include <thread>
 #include <vector>
 
 using namespace dml;
@@ -60,6 +61,9 @@ struct Chunk {
     int nb = 0;
     int64_t max_nrec = 0;
     uint64_t tail_cut = kNoPos;
+    bool sorted = false;  // array store: partitioned + per-leaf ordered apply (dml_sparse.hip)
+    SpPlan sp{};
+    SpLayout spl{};
 };
 
 int vtype_of(const dml_desc& d) { return d.value_type; }
@@ -81,6 +85,8 @@ struct Workspace {
     hipEvent_t kstart = nullptr;      // main stream: reduce dispatch start (in-packet timestamp)
     hipEvent_t applied = nullptr;     // main stream: chunk applied (in-packet stop of its last kernel)
     hipEvent_t done = nullptr;        // copy stream: ctrl copied out (chunk retired-able)
+    uint8_t* sp = nullptr;            // sparse partition buffers (SpLayout), grown on demand
+    size_t sp_cap = 0;
 };
 
 struct Pending {
@@ -117,6 +123,12 @@ struct dml_store {
     uint8_t* hstage = nullptr;
     uint8_t* dstage = nullptr;
     size_t stage_cap = 0;
+    // fetch / checkpoint transfers: device scratch (encoded records, swapped
+    // rows) and two pinned bounce buffers that overlap DMA with the host copy
+    uint8_t* dscr = nullptr;
+    size_t dscr_cap = 0;
+    uint8_t* xbuf[2] = {nullptr, nullptr};
+    hipEvent_t xev[2] = {nullptr, nullptr};
     // sticky error (first failure)
     int err = 0;
     int64_t err_key = 0;
@@ -177,6 +189,103 @@ int ensure_stage(dml_store* s, size_t bytes) {
     return DML_OK;
 }
 
+// ---- host <-> device transfers for fetch / checkpoint ----------------------
+// Pageable destinations go through two pinned bounce buffers: the DMA of chunk
+// i+1 runs while the host copies chunk i out (several threads per chunk).
+// Pinned destinations (dml_host_alloc, hipHostRegister) are DMA'd directly.
+constexpr size_t kXferChunk = 16u << 20;
+
+bool host_pinned(const void* p) {
+    hipPointerAttribute_t a;
+    const bool pinned = hipPointerGetAttributes(&a, p) == hipSuccess && a.type == hipMemoryTypeHost;
+    (void)hipGetLastError();  // a pageable pointer leaves an error from the attribute query
+    return pinned;
+}
+
+int ensure_scratch(dml_store* s, size_t bytes) {
+    if (bytes <= s->dscr_cap) return DML_OK;
+    HIPCHK(hipStreamSynchronize(s->stream));  // queued work may still read the old scratch
+    if (s->dscr) (void)hipFree(s->dscr);
+    s->dscr = nullptr;
+    s->dscr_cap = 0;
+    HIPCHK(hipMalloc((void**)&s->dscr, bytes));
+    s->dscr_cap = bytes;
+    return DML_OK;
+}
+
+int ensure_xfer(dml_store* s) {
+    for (int i = 0; i < 2; ++i) {
+        if (!s->xbuf[i]) HIPCHK(hipHostMalloc((void**)&s->xbuf[i], kXferChunk, hipHostMallocDefault));
+        if (!s->xev[i]) HIPCHK(hipEventCreateWithFlags(&s->xev[i], hipEventDisableTiming));
+    }
+    return DML_OK;
+}
+
+void host_copy(uint8_t* d, const uint8_t* src, size_t n) {
+    constexpr size_t kPart = 2u << 20;
+    constexpr size_t kMaxThreads = 4;
+    const size_t parts = std::min(kMaxThreads, n / kPart);
+    if (parts < 2) {
+        std::memcpy(d, src, n);
+        return;
+    }
+    const size_t per = (n / parts + 63) & ~(size_t)63;
+    std::thread th[kMaxThreads];
+    for (size_t i = 1; i < parts; ++i) {
+        const size_t lo = i * per;
+        if (lo >= n) break;
+        th[i] = std::thread([=] { std::memcpy(d + lo, src + lo, std::min(per, n - lo)); });
+    }
+    std::memcpy(d, src, std::min(per, n));
+    for (size_t i = 1; i < parts; ++i)
+        if (th[i].joinable()) th[i].join();
+}
+
+// Device -> host after everything queued on s->stream; returns with the bytes in `dst`.
+int d2h(dml_store* s, uint8_t* dst, const uint8_t* src, size_t bytes) {
+    if (bytes <= (256u << 10) || host_pinned(dst)) {
+        if (bytes) HIPCHK(hipMemcpyAsync(dst, src, bytes, hipMemcpyDeviceToHost, s->stream));
+        HIPCHK(hipStreamSynchronize(s->stream));
+        return DML_OK;
+    }
+    if (int rc = ensure_xfer(s)) return rc;
+    const size_t n = (bytes + kXferChunk - 1) / kXferChunk;
+    auto issue = [&](size_t i) -> hipError_t {
+        const size_t off = i * kXferChunk, len = std::min(kXferChunk, bytes - off);
+        hipError_t e = hipMemcpyAsync(s->xbuf[i & 1], src + off, len, hipMemcpyDeviceToHost, s->stream);
+        return e == hipSuccess ? hipEventRecord(s->xev[i & 1], s->stream) : e;
+    };
+    HIPCHK(issue(0));
+    if (n > 1) HIPCHK(issue(1));
+    for (size_t i = 0; i < n; ++i) {
+        HIPCHK(hipEventSynchronize(s->xev[i & 1]));
+        const size_t off = i * kXferChunk;
+        host_copy(dst + off, s->xbuf[i & 1], std::min(kXferChunk, bytes - off));
+        if (i + 2 < n) HIPCHK(issue(i + 2));
+    }
+    return DML_OK;
+}
+
+// Host -> device, queued on s->stream; returns once `src` may be reused.
+int h2d(dml_store* s, uint8_t* dst, const uint8_t* src, size_t bytes) {
+    if (bytes <= (256u << 10) || host_pinned(src)) {
+        if (bytes) HIPCHK(hipMemcpyAsync(dst, src, bytes, hipMemcpyHostToDevice, s->stream));
+        HIPCHK(hipStreamSynchronize(s->stream));
+        return DML_OK;
+    }
+    if (int rc = ensure_xfer(s)) return rc;
+    const size_t n = (bytes + kXferChunk - 1) / kXferChunk;
+    for (size_t i = 0; i < n; ++i) {
+        if (i >= 2) HIPCHK(hipEventSynchronize(s->xev[i & 1]));  // bounce buffer drained by its DMA
+        const size_t off = i * kXferChunk, len = std::min(kXferChunk, bytes - off);
+        host_copy(s->xbuf[i & 1], src + off, len);
+        HIPCHK(hipMemcpyAsync(dst + off, s->xbuf[i & 1], len, hipMemcpyHostToDevice, s->stream));
+        HIPCHK(hipEventRecord(s->xev[i & 1], s->stream));
+    }
+    HIPCHK(hipStreamSynchronize(s->stream));
+    return DML_OK;
+}
+
 // Per-push record accounting: records with a complete key, and the position of
 // the first truncated access of a ragged tail (DataDesc.readInt past data.length).
 void plan_bucket(const dml_store* s, int64_t len, int gb, int64_t* nrec, uint64_t* tail_cut) {
@@ -226,6 +335,15 @@ int launch_apply(dml_store* s, Chunk& c, Workspace& W, const Ctrl* prev) {
             HIPCHK(launch_maxdelta_finalize(s->cand, nblk, s->md, c.bt, c.nb, s->stride, s->K, s->V, s->stream));
         if (!inpacket) HIPCHK(hipEventRecord(W.applied, s->stream));
         if (s->timing) s->ev_used.emplace_back(W.kstart, W.applied);
+    } else if (c.sorted) {
+        LaunchEv ev{};
+        if (s->timing) {
+            auto p = ev_pair(s);
+            ev = {p.first, p.second};
+            s->ev_used.push_back(p);
+        }
+        HIPCHK(launch_sparse_leaf(vtype_of(s->desc), s->data, c.sp, c.spl, W.sp, W.ctrl, prev, s->stream, ev));
+        HIPCHK(hipEventRecord(W.applied, s->stream));
     } else {
         for (int b = 0; b < c.nb; ++b) {
             LaunchEv ev{};
@@ -259,6 +377,26 @@ int launch_chunk(dml_store* s, Chunk& c, Workspace& W, const Ctrl* prev) {
     } else {
         HIPCHK(launch_array_validate(c.bt, c.nb, c.max_nrec, s->stride, s->K, s->first, s->rows, W.ctrl, c.tail_cut,
                                      is));
+        // float / double arrays: partition the chunk by leaf (row range) for the ordered
+        // per-leaf apply; int32 arrays keep the per-push atomic path (negativity check).
+        // DML_SPARSE_ATOMIC=1 forces the per-push path (A/B).
+        static const bool atomic_only = getenv("DML_SPARSE_ATOMIC") && atoi(getenv("DML_SPARSE_ATOMIC"));
+        const int vt = vtype_of(s->desc);
+        c.sorted = !atomic_only && (vt == kF32 || vt == kF64);
+        if (c.sorted) {
+            c.sp = sparse_plan(c.bt, c.nb, s->rows);
+            c.spl = sparse_layout(c.sp, s->V);
+            if (W.sp_cap < c.spl.total) {
+                HIPCHK(hipStreamSynchronize(s->stream));  // W's previous chunk is retired; be safe
+                (void)hipFree(W.sp);
+                W.sp = nullptr;
+                W.sp_cap = 0;
+                HIPCHK(hipMalloc((void**)&W.sp, c.spl.total));
+                W.sp_cap = c.spl.total;
+            }
+            HIPCHK(launch_sparse_partition(vt, c.bt, c.sp, c.spl, W.sp, s->stride, s->K, s->first, s->rows, W.ctrl,
+                                           c.tail_cut, is));
+        }
     }
     if (!serial) {
         HIPCHK(hipEventRecord(W.idx_done, s->istream));
@@ -415,6 +553,9 @@ int retire_front(dml_store* s) {
     if (s->is_matrix && ctl.no_dup == 0u) {
         rc = replay_rows(s, c, W, &ctl);
         if (rc) return rc;
+    } else if (!s->is_matrix && ctl.no_dup == 0u) {
+        // leaves too large for the LDS sort were skipped by the leaf kernel: apply them exactly
+        HIPCHK(sparse_replay(vtype_of(s->desc), s->data, c.sp, c.spl, W.sp, s->stream));
     } else if (ctl.neg_pos != kNoPos) {
         if (s->is_matrix) {
             HIPCHK(launch_rollback_i32((int32_t*)s->data, s->rows, s->cols, c.bt, c.nb, s->stride, s->K, W.slot,
@@ -638,6 +779,7 @@ void dml_store_destroy(dml_store* s) {
         for (auto& p : s->ev_free) { (void)hipEventDestroy(p.first); (void)hipEventDestroy(p.second); }
         for (Workspace& W : s->ws) {
             (void)hipFree(W.base);
+            (void)hipFree(W.sp);
             if (W.hctrl) (void)hipHostFree(W.hctrl);
             if (W.idx_done) (void)hipEventDestroy(W.idx_done);
             if (W.done) (void)hipEventDestroy(W.done);
@@ -651,6 +793,11 @@ void dml_store_destroy(dml_store* s) {
         (void)hipFree(s->md);
         (void)hipFree(s->dstage);
         if (s->hstage) (void)hipHostFree(s->hstage);
+        (void)hipFree(s->dscr);
+        for (int i = 0; i < 2; ++i) {
+            if (s->xbuf[i]) (void)hipHostFree(s->xbuf[i]);
+            if (s->xev[i]) (void)hipEventDestroy(s->xev[i]);
+        }
         if (s->stream) (void)hipStreamDestroy(s->stream);
         if (s->istream) (void)hipStreamDestroy(s->istream);
         if (s->cstream) (void)hipStreamDestroy(s->cstream);
@@ -846,8 +993,11 @@ int dml_store_max_delta(dml_store* s, float* max_delta, int32_t* row, int32_t* c
     return DML_OK;
 }
 
-static int fetch_impl(dml_store* s, const int64_t* keys, int64_t nkeys, uint8_t* out, int64_t cap, int64_t* out_len) {
-    if (nkeys < 0 || (nkeys > 0 && !keys) || !out_len) return set_err(DML_E_INVALID_ARG, "bad fetch arguments");
+// keys == nullptr: the keys are key_lo .. key_lo + nkeys - 1 (a KeyRange already
+// clipped to the shard), encoded without a key array.
+static int fetch_impl(dml_store* s, const int64_t* keys, int64_t nkeys, int64_t key_lo, uint8_t* out, int64_t cap,
+                      int64_t* out_len) {
+    if (nkeys < 0 || !out_len) return set_err(DML_E_INVALID_ARG, "bad fetch arguments");
     // record layout of handleFetch (dense column)
     int64_t rec;
     int value_slot;
@@ -860,24 +1010,21 @@ static int fetch_impl(dml_store* s, const int64_t* keys, int64_t nkeys, uint8_t*
     }
     *out_len = nkeys * rec;
     if (!out || cap < *out_len) return set_err(DML_E_CAPACITY, "fetch output buffer too small");
-    for (int64_t j = 0; j < nkeys; ++j) {
-        const int32_t idx = (int32_t)(uint32_t)((uint64_t)keys[j] - (uint64_t)s->first);
-        if (idx < 0 || idx >= s->rows) return record_error(s, DML_E_KEY_OUT_OF_SHARD, keys[j], -1);
+    if (keys) {
+        for (int64_t j = 0; j < nkeys; ++j) {
+            const int32_t idx = (int32_t)(uint32_t)((uint64_t)keys[j] - (uint64_t)s->first);
+            if (idx < 0 || idx >= s->rows) return record_error(s, DML_E_KEY_OUT_OF_SHARD, keys[j], -1);
+        }
     }
     if (nkeys == 0) return DML_OK;
-    int64_t* dkeys = nullptr;
-    uint8_t* dout = nullptr;
-    HIPCHK(hipMallocAsync((void**)&dkeys, (size_t)nkeys * 8, s->stream));
-    HIPCHK(hipMallocAsync((void**)&dout, (size_t)*out_len, s->stream));
-    HIPCHK(hipMemcpyAsync(dkeys, keys, (size_t)nkeys * 8, hipMemcpyHostToDevice, s->stream));
-    HIPCHK(hipMemsetAsync(dout, 0, (size_t)*out_len, s->stream));
-    HIPCHK(launch_fetch(vtype_of(s->desc), s->data, s->adagrad ? s->alpha : nullptr, s->cols, dkeys, nkeys, s->first,
-                        dout, rec, s->K, value_slot, s->stream));
-    HIPCHK(hipMemcpyAsync(out, dout, (size_t)*out_len, hipMemcpyDeviceToHost, s->stream));
-    HIPCHK(hipFreeAsync(dkeys, s->stream));
-    HIPCHK(hipFreeAsync(dout, s->stream));
-    HIPCHK(hipStreamSynchronize(s->stream));
-    return DML_OK;
+    const size_t kbytes = keys ? ((size_t)nkeys * 8 + 255) & ~(size_t)255 : 0;
+    if (int rc = ensure_scratch(s, kbytes + (size_t)*out_len)) return rc;
+    const int64_t* dkeys = keys ? (const int64_t*)s->dscr : nullptr;
+    if (keys) HIPCHK(hipMemcpyAsync(s->dscr, keys, (size_t)nkeys * 8, hipMemcpyHostToDevice, s->stream));
+    uint8_t* dout = s->dscr + kbytes;
+    HIPCHK(launch_fetch(vtype_of(s->desc), s->data, s->adagrad ? s->alpha : nullptr, s->cols, dkeys, key_lo, nkeys,
+                        s->first, dout, rec, s->K, value_slot, s->stream));
+    return d2h(s, out, dout, (size_t)*out_len);
 }
 
 int dml_store_fetch(dml_store* s, const int64_t* keys, int64_t nkeys, uint8_t* out, int64_t cap, int64_t* out_len) {
@@ -885,7 +1032,8 @@ int dml_store_fetch(dml_store* s, const int64_t* keys, int64_t nkeys, uint8_t* o
     std::lock_guard<std::mutex> lk(s->mu);
     DeviceGuard g(s->device);
     if (int rc = begin_call(s)) return rc;
-    return fetch_impl(s, keys, nkeys, out, cap, out_len);
+    if (nkeys > 0 && !keys) return set_err(DML_E_INVALID_ARG, "null keys");
+    return fetch_impl(s, keys, nkeys, 0, out, cap, out_len);
 }
 
 int dml_store_fetch_range(dml_store* s, int64_t first_key, int64_t last_key, uint8_t* out, int64_t cap,
@@ -896,13 +1044,29 @@ int dml_store_fetch_range(dml_store* s, int64_t first_key, int64_t last_key, uin
     if (int rc = begin_call(s)) return rc;
     // KeyRange.intersect (KeyRange.java:124-136): clip to the shard, ascending
     const int64_t lo = std::max(first_key, s->first), hi = std::min(last_key, s->last);
-    std::vector<int64_t> keys;
-    if (lo <= hi) {
-        keys.resize((size_t)(hi - lo + 1));
-        for (int64_t k = lo; k <= hi; ++k) keys[(size_t)(k - lo)] = k;
-    }
     if (!out_len) return set_err(DML_E_INVALID_ARG, "null out_len");
-    return fetch_impl(s, keys.data(), (int64_t)keys.size(), out, cap, out_len);
+    return fetch_impl(s, nullptr, lo <= hi ? hi - lo + 1 : 0, lo, out, cap, out_len);
+}
+
+// Rows [lo, hi] (local indices), big-endian, row-major: DataOutputStream.write{Float,Int,Double}.
+static int write_rows_be(dml_store* s, int64_t lo, int64_t hi, uint8_t* out) {
+    if (hi < lo) return DML_OK;
+    const int64_t n = (hi - lo + 1) * s->cols;
+    const size_t bytes = (size_t)n * (size_t)s->V;
+    if (int rc = ensure_scratch(s, bytes)) return rc;
+    HIPCHK(launch_bswap(s->V, (const uint8_t*)s->data + (size_t)lo * s->cols * s->V, s->dscr, n, s->stream));
+    return d2h(s, out, s->dscr, bytes);
+}
+
+// The first `nelem` elements from row lo on, from big-endian bytes (DataInputStream.read*).
+static int read_elems_be(dml_store* s, int64_t lo, int64_t nelem, const uint8_t* in) {
+    if (nelem <= 0) return DML_OK;
+    const size_t bytes = (size_t)nelem * (size_t)s->V;
+    if (int rc = ensure_scratch(s, bytes)) return rc;
+    if (int rc = h2d(s, s->dscr, in, bytes)) return rc;
+    HIPCHK(launch_bswap(s->V, s->dscr, (uint8_t*)s->data + (size_t)lo * s->cols * s->V, nelem, s->stream));
+    HIPCHK(hipStreamSynchronize(s->stream));
+    return DML_OK;
 }
 
 int dml_store_write_all(dml_store* s, uint8_t* out_be, int64_t cap, int64_t* out_len) {
@@ -910,16 +1074,10 @@ int dml_store_write_all(dml_store* s, uint8_t* out_be, int64_t cap, int64_t* out
     std::lock_guard<std::mutex> lk(s->mu);
     DeviceGuard g(s->device);
     if (int rc = begin_call(s)) return rc;
-    const int64_t n = s->rows * s->cols, bytes = n * s->V;
+    const int64_t bytes = s->rows * s->cols * s->V;
     if (out_len) *out_len = bytes;
     if (!out_be || cap < bytes) return set_err(DML_E_CAPACITY, "writeAll buffer too small");
-    void* tmp = nullptr;
-    HIPCHK(hipMallocAsync(&tmp, (size_t)std::max<int64_t>(bytes, 1), s->stream));
-    HIPCHK(launch_bswap(s->V, s->data, tmp, n, s->stream));
-    HIPCHK(hipMemcpyAsync(out_be, tmp, (size_t)bytes, hipMemcpyDeviceToHost, s->stream));
-    HIPCHK(hipFreeAsync(tmp, s->stream));
-    HIPCHK(hipStreamSynchronize(s->stream));
-    return DML_OK;
+    return write_rows_be(s, 0, s->rows - 1, out_be);
 }
 
 int dml_store_read_all(dml_store* s, const uint8_t* in_be, int64_t len) {
@@ -927,16 +1085,66 @@ int dml_store_read_all(dml_store* s, const uint8_t* in_be, int64_t len) {
     std::lock_guard<std::mutex> lk(s->mu);
     DeviceGuard g(s->device);
     if (int rc = begin_call(s)) return rc;
-    const int64_t n = s->rows * s->cols, bytes = n * s->V;
-    // DataInputStream.readFloat past the end throws EOFException (an IOException)
-    if (!in_be || len < bytes) return set_err(DML_E_TRUNCATED, "readAll: stream shorter than the shard");
-    void* tmp = nullptr;
-    HIPCHK(hipMallocAsync(&tmp, (size_t)std::max<int64_t>(bytes, 1), s->stream));
-    HIPCHK(hipMemcpyAsync(tmp, in_be, (size_t)bytes, hipMemcpyHostToDevice, s->stream));
-    HIPCHK(launch_bswap(s->V, tmp, s->data, n, s->stream));
-    HIPCHK(hipFreeAsync(tmp, s->stream));
-    HIPCHK(hipStreamSynchronize(s->stream));
+    const int64_t n = s->rows * s->cols;
+    if (len < 0 || (len > 0 && !in_be)) return set_err(DML_E_INVALID_ARG, "bad readAll arguments");
+    // readFloat past the end throws EOFException after the elements before it were assigned
+    const int64_t avail = std::min(n, len / s->V);
+    if (int rc = read_elems_be(s, 0, avail, in_be)) return rc;
+    if (avail < n) return set_err(DML_E_TRUNCATED, "readAll: stream shorter than the shard");
     return DML_OK;
+}
+
+int dml_store_sync_to(dml_store* s, int32_t from_row, int32_t to_row, uint8_t* out_be, int64_t cap,
+                      int64_t* out_len) {
+    if (int rc = check_store(s)) return rc;
+    std::lock_guard<std::mutex> lk(s->mu);
+    DeviceGuard g(s->device);
+    if (int rc = begin_call(s)) return rc;
+    if (!out_len) return set_err(DML_E_INVALID_ARG, "null out_len");
+    *out_len = 0;
+    if (to_row < from_row) return DML_OK;  // the loop body never runs
+    // localData[i] for i = from..to: a negative row throws before any write, a row
+    // past the shard after the rows before it were written (ArrayIndexOutOfBounds)
+    if (from_row < 0) return set_err(DML_E_KEY_OUT_OF_SHARD, "syncTo: negative row");
+    const int64_t hi = std::min<int64_t>(to_row, s->rows - 1);
+    const int64_t bytes = hi >= from_row ? (hi - from_row + 1) * s->cols * s->V : 0;
+    if (!out_be || cap < bytes) {
+        *out_len = bytes;
+        return set_err(DML_E_CAPACITY, "syncTo buffer too small");
+    }
+    if (int rc = write_rows_be(s, from_row, hi, out_be)) return rc;
+    *out_len = bytes;
+    if (to_row >= s->rows) return set_err(DML_E_KEY_OUT_OF_SHARD, "syncTo: row past the shard");
+    return DML_OK;
+}
+
+int dml_store_sync_from(dml_store* s, int32_t from_row, int32_t to_row, const uint8_t* in_be, int64_t len) {
+    if (int rc = check_store(s)) return rc;
+    std::lock_guard<std::mutex> lk(s->mu);
+    DeviceGuard g(s->device);
+    if (int rc = begin_call(s)) return rc;
+    if (len < 0 || (len > 0 && !in_be)) return set_err(DML_E_INVALID_ARG, "bad syncFrom arguments");
+    if (to_row < from_row) return DML_OK;
+    if (from_row < 0) return set_err(DML_E_KEY_OUT_OF_SHARD, "syncFrom: negative row");
+    // elements assigned in order until the stream ends (EOF) or a row falls past the shard
+    const int64_t hi = std::min<int64_t>(to_row, s->rows - 1);
+    const int64_t want = hi >= from_row ? (hi - from_row + 1) * s->cols : 0;
+    const int64_t avail = std::min(want, len / s->V);
+    if (int rc = read_elems_be(s, from_row, avail, in_be)) return rc;
+    if (avail < want) return set_err(DML_E_TRUNCATED, "syncFrom: stream shorter than the rows");
+    if (to_row >= s->rows) return set_err(DML_E_KEY_OUT_OF_SHARD, "syncFrom: row past the shard");
+    return DML_OK;
+}
+
+int dml_host_alloc(int64_t bytes, void** host_ptr) {
+    if (bytes < 0 || !host_ptr) return set_err(DML_E_INVALID_ARG, "bad host alloc arguments");
+    *host_ptr = nullptr;
+    HIPCHK(hipHostMalloc(host_ptr, (size_t)std::max<int64_t>(bytes, 1), hipHostMallocDefault));
+    return DML_OK;
+}
+
+void dml_host_free(void* host_ptr) {
+    if (host_ptr) (void)hipHostFree(host_ptr);
 }
 
 int dml_store_stream(dml_store* s, void** stream) {

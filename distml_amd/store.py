@@ -15,6 +15,7 @@ from __future__ import annotations
 
 import ctypes as C
 import struct
+import weakref
 from typing import List, Optional, Sequence
 
 import numpy as np
@@ -173,6 +174,19 @@ class DataStore:
                                     out.ctypes.data, cap, C.byref(out_len)), self)
         return out[:out_len.value].tobytes()
 
+    def handleFetchInto(self, format: DataDesc, rows: KeyRange, out) -> int:
+        """handleFetch of a KeyRange written into `out` (a writable buffer, e.g.
+        pinned_empty()); returns the byte count. No intermediate copies."""
+        self._check_format(format)
+        keys = self.localRows.intersect(rows)
+        if not isinstance(keys, KeyRange):
+            raise TypeError("handleFetchInto takes a KeyRange")
+        a = np.frombuffer(out, np.uint8) if not isinstance(out, np.ndarray) else out
+        out_len = C.c_int64()
+        check(_lib.load().dml_store_fetch_range(self._h, keys.firstKey, keys.lastKey, a.ctypes.data, a.nbytes,
+                                                C.byref(out_len)), self)
+        return out_len.value
+
     def writeAll(self, os=None) -> bytes:
         """Big-endian row-major dump (FloatMatrixStore.java:74-81); writes to `os` if given."""
         n = self._rows * self._cols * np.dtype(self.dtype).itemsize
@@ -190,18 +204,31 @@ class DataStore:
         check(_lib.load().dml_store_read_all(self._h, bytes(b), len(b)), self)
 
     def syncTo(self, os, fromRow: int, toRow: int):
-        """Rows fromRow..toRow inclusive, big-endian (FloatMatrixStore.java:94-100)."""
-        a = self.values()[fromRow:toRow + 1]
-        os.write(a.astype(a.dtype.newbyteorder(">")).tobytes())
+        """Rows fromRow..toRow inclusive, big-endian (FloatMatrixStore.java:94-100);
+        PSSync.java:131. Rows before a bad row are written before the error."""
+        v = np.dtype(self.dtype).itemsize
+        hi = min(toRow, self._rows - 1)
+        cap = max(hi - fromRow + 1, 0) * self._cols * v
+        out = np.empty(max(cap, 1), np.uint8)
+        ln = C.c_int64()
+        rc = _lib.load().dml_store_sync_to(self._h, fromRow, toRow, out.ctypes.data, cap, C.byref(ln))
+        if ln.value and rc in (0, _lib.DML_E_KEY_OUT_OF_SHARD):
+            os.write(out[:ln.value].tobytes())
+        check(rc, self)
 
     def syncFrom(self, is_, fromRow: int, toRow: int):
-        # Follows the intended row layout; the reference's matrix syncFrom shadows rowSize
-        # with the row count (SURVEY defect 5), which this store does not reproduce.
-        a = self.values()
-        n = (toRow - fromRow + 1) * self._cols
-        be = np.frombuffer(is_.read(n * a.itemsize), dtype=np.dtype(self.dtype).newbyteorder(">"))
-        a[fromRow:toRow + 1] = be.reshape(toRow - fromRow + 1, self._cols).astype(self.dtype)
-        self.load_values(a)
+        """Rows fromRow..toRow from big-endian bytes (PSSync.java:160). Follows the
+        intended row layout; the reference's matrix syncFrom shadows rowSize with the
+        row count (SURVEY defect 5), which this store does not reproduce."""
+        v = np.dtype(self.dtype).itemsize
+        hi = min(toRow, self._rows - 1)
+        n = max(hi - fromRow + 1, 0) * self._cols * v
+        if isinstance(is_, np.ndarray):  # e.g. pinned_empty(): handed to the DMA as is
+            a = np.ascontiguousarray(is_.view(np.uint8).ravel()[:n])
+            check(_lib.load().dml_store_sync_from(self._h, fromRow, toRow, a.ctypes.data, a.nbytes), self)
+            return
+        b = is_.read(n) if hasattr(is_, "read") else bytes(is_)[:n]
+        check(_lib.load().dml_store_sync_from(self._h, fromRow, toRow, b, len(b)), self)
 
     # ---- AdaGrad ----------------------------------------------------------
     def setAlpha(self, initialAlpha: float, minAlpha: float, factor: float):
@@ -287,6 +314,16 @@ class DataStore:
     @staticmethod
     def createStores(model, serverIndex: int, device: Optional[int] = None):
         return {name: DataStore.createStore(serverIndex, m, device) for name, m in model.dataMap.items()}
+
+
+def pinned_empty(nbytes: int) -> np.ndarray:
+    """uint8 array over pinned host memory (dml_host_alloc); freed with the array."""
+    L = _lib.load()
+    p = C.c_void_p()
+    check(L.dml_host_alloc(nbytes, C.byref(p)))
+    buf = (C.c_uint8 * max(nbytes, 1)).from_address(p.value)
+    weakref.finalize(buf, L.dml_host_free, p.value)
+    return np.frombuffer(buf, np.uint8, count=nbytes)
 
 
 class DeviceBatch:

@@ -156,9 +156,28 @@ int dml_store_fetch_range(dml_store* s, int64_t first_key, int64_t last_key,
                           uint8_t* out, int64_t cap, int64_t* out_len);
 
 /* writeAll/readAll (FloatMatrixStore.java:74-91 etc.): big-endian row-major
- * values, the bytes DataOutputStream.writeFloat/writeInt/writeDouble emit. */
+ * values, the bytes DataOutputStream.writeFloat/writeInt/writeDouble emit.
+ * read_all assigns the elements the stream holds before failing with
+ * DML_E_TRUNCATED when it is short (readFloat's EOFException). */
 int dml_store_write_all(dml_store* s, uint8_t* out_be, int64_t cap, int64_t* out_len);
 int dml_store_read_all(dml_store* s, const uint8_t* in_be, int64_t len);
+/* syncTo/syncFrom(stream, fromRow, toRow) (FloatMatrixStore.java:94-110,
+ * IntArrayStore.java:64-75 etc.; called by PSSync.java:131,160): local rows
+ * from..to inclusive, big-endian. to < from moves nothing; a negative from
+ * fails before any byte; rows past the shard fail with DML_E_KEY_OUT_OF_SHARD
+ * after the rows before them were moved (the reference's
+ * ArrayIndexOutOfBoundsException). sync_from uses the intended row layout
+ * (defect 5). */
+int dml_store_sync_to(dml_store* s, int32_t from_row, int32_t to_row, uint8_t* out_be, int64_t cap,
+                      int64_t* out_len);
+int dml_store_sync_from(dml_store* s, int32_t from_row, int32_t to_row, const uint8_t* in_be, int64_t len);
+
+/* Pinned host memory for callers that receive pushes or return fetches through
+ * it (a JNI DirectByteBuffer over it lets NIO read a PushRequest straight into
+ * DMA-able memory, PSAgent.java:27-62): pushes from it are DMA'd without
+ * staging, fetch / write_all / sync_to into it skip the bounce buffers. */
+int dml_host_alloc(int64_t bytes, void** host_ptr);
+void dml_host_free(void* host_ptr);
 
 /* --- stream / timing / device reduce building blocks ------------------- */
 

@@ -22,10 +22,12 @@ public class GpuDataStore extends DataStore {
     private final long handle;          // dml_store*
     private final KeyRange localRows;
     private final int rowSize;
+    private final int valueBytes;
 
     public GpuDataStore(DataDesc format, KeyRange keys, int cols, int device) {
         this.localRows = keys;
         this.rowSize = format.dataType == DataDesc.DATA_TYPE_MATRIX ? cols : 1;
+        this.valueBytes = format.valueType == DataDesc.ELEMENT_TYPE_DOUBLE ? 8 : 4;
         this.handle = nativeCreate(format.dataType, format.keyType, format.valueType,
                 format.denseRow ? 1 : 0, format.denseColumn ? 1 : 0, format.adaGrad ? 1 : 0,
                 keys.firstKey, keys.lastKey, cols, device, 0);
@@ -61,16 +63,24 @@ public class GpuDataStore extends DataStore {
         is.readFully(b);
         nativeReadAll(handle, b);
     }
+    /** PSSync.java:131 — rows fromRow..toRow, big-endian, moved by the device. */
     public void syncTo(DataOutputStream os, int fromRow, int toRow) throws IOException {
-        byte[] all = nativeWriteAll(handle);
-        int rec = all.length / (int) localRows.size();
-        os.write(all, fromRow * rec, (toRow - fromRow + 1) * rec);
+        os.write(nativeSyncTo(handle, fromRow, toRow));
     }
+    /** PSSync.java:160 — intended row layout (the reference's matrix syncFrom shadows rowSize). */
     public void syncFrom(DataInputStream is, int fromRow, int toRow) throws IOException {
-        byte[] all = nativeWriteAll(handle);
-        int rec = all.length / (int) localRows.size();
-        is.readFully(all, fromRow * rec, (toRow - fromRow + 1) * rec);
-        nativeReadAll(handle, all);
+        int last = Math.min(toRow, (int) localRows.size() - 1);
+        byte[] b = new byte[Math.max(0, last - fromRow + 1) * rowSize * valueBytes];
+        is.readFully(b);
+        nativeSyncFrom(handle, fromRow, toRow, b);
+    }
+
+    /** Wire ingest: a pinned DirectByteBuffer the NIO channel reads PushRequests into. */
+    public static java.nio.ByteBuffer allocatePinned(long bytes) { return nativeHostAlloc(bytes); }
+    public static void freePinned(java.nio.ByteBuffer b) { nativeHostFree(b); }
+    /** handlePush of the record bytes at buf[offset, offset + len) (no JVM heap copy). */
+    public void handlePushDirect(java.nio.ByteBuffer buf, int offset, int len) {
+        nativePushDirect(handle, buf, offset, len);
     }
 
     public void close() { nativeDestroy(handle); }
@@ -83,6 +93,11 @@ public class GpuDataStore extends DataStore {
     private static native byte[] nativeWriteAll(long h);
     private static native void nativeReadAll(long h, byte[] be);
     private static native long nativeShardBytes(long h);
+    private static native byte[] nativeSyncTo(long h, int from, int to);
+    private static native void nativeSyncFrom(long h, int from, int to, byte[] be);
+    private static native java.nio.ByteBuffer nativeHostAlloc(long bytes);
+    private static native void nativeHostFree(java.nio.ByteBuffer b);
+    private static native void nativePushDirect(long h, java.nio.ByteBuffer b, int offset, int len);
     private static native void nativeFill(long h, double v);
     private static native void nativeSetAlpha(long h, float a, float min, float factor);
     private static native void nativeDestroy(long h);

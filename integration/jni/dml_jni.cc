@@ -99,6 +99,50 @@ JNIEXPORT void JNICALL FN(nativeReadAll)(JNIEnv* env, jclass, jlong h, jbyteArra
     if (rc) throw_for(env, rc);
 }
 
+// syncTo / syncFrom (PSSync.java:131,160): local rows from..to, big-endian.
+JNIEXPORT jbyteArray JNICALL FN(nativeSyncTo)(JNIEnv* env, jclass, jlong h, jint from, jint to) {
+    int64_t rows = 0;
+    int32_t cols = 0;
+    dml_store_shape(H(h), &rows, &cols);
+    int64_t len = 0;
+    // size query: the rows that exist in [from, to]
+    const int64_t hi = to < rows ? to : rows - 1;
+    const int64_t cap = (from >= 0 && hi >= from) ? (hi - from + 1) * (int64_t)cols * 8 : 0;
+    std::vector<uint8_t> out((size_t)(cap > 0 ? cap : 1));
+    const int rc = dml_store_sync_to(H(h), from, to, out.data(), cap, &len);
+    jbyteArray r = env->NewByteArray((jsize)len);
+    env->SetByteArrayRegion(r, 0, (jsize)len, reinterpret_cast<const jbyte*>(out.data()));
+    if (rc) { throw_for(env, rc); return nullptr; }  // the caller writes the rows before rethrowing
+    return r;
+}
+
+JNIEXPORT void JNICALL FN(nativeSyncFrom)(JNIEnv* env, jclass, jlong h, jint from, jint to, jbyteArray a) {
+    const jsize n = env->GetArrayLength(a);
+    void* p = env->GetPrimitiveArrayCritical(a, nullptr);
+    const int rc = dml_store_sync_from(H(h), from, to, static_cast<const uint8_t*>(p), n);
+    env->ReleasePrimitiveArrayCritical(a, p, JNI_ABORT);
+    if (rc) throw_for(env, rc);
+}
+
+// Pinned host memory as a DirectByteBuffer: PSAgent's NIO channel reads a
+// PushRequest straight into it (PSAgent.java:27-62) and nativePushDirect hands
+// the record bytes to the DMA without a staging copy.
+JNIEXPORT jobject JNICALL FN(nativeHostAlloc)(JNIEnv* env, jclass, jlong bytes) {
+    void* p = nullptr;
+    if (int rc = dml_host_alloc(bytes, &p)) { throw_for(env, rc); return nullptr; }
+    return env->NewDirectByteBuffer(p, bytes);
+}
+
+JNIEXPORT void JNICALL FN(nativeHostFree)(JNIEnv* env, jclass, jobject buf) {
+    dml_host_free(env->GetDirectBufferAddress(buf));
+}
+
+JNIEXPORT void JNICALL FN(nativePushDirect)(JNIEnv* env, jclass, jlong h, jobject buf, jint offset, jint len) {
+    auto* p = static_cast<const uint8_t*>(env->GetDirectBufferAddress(buf));
+    if (!p) { throw_for(env, DML_E_INVALID_ARG); return; }
+    if (int rc = dml_store_push(H(h), p + offset, len)) throw_for(env, rc);
+}
+
 JNIEXPORT void JNICALL FN(nativeFill)(JNIEnv* env, jclass, jlong h, jdouble v) {
     if (int rc = dml_store_fill(H(h), v)) throw_for(env, rc);
 }

@@ -55,10 +55,44 @@ torch.cuda.synchronize()
 h2d = (time.perf_counter() - t0) / 3
 res["h2d_pinned_GBps"] = round(W * bench.BUCKET / h2d / 1e9, 2)
 del dev, src
-# fetch the whole shard back (KeyRange -> [key][1024 f32] records, D2H)
+# fetch / checkpoint through the C-ABI (as the JNI shim calls it), pageable and pinned host buffers
+from distml_amd import pinned_empty  # noqa: E402
+
+L = _lib.load()
+rec_bytes = bench.ROWS * (4 + 4 * bench.COLS)
+shard_bytes = bench.SHARD
+
+
+def best_ms(fn, reps=5):
+    fn()
+    ts = []
+    for _ in range(reps):
+        t0 = time.perf_counter()
+        fn()
+        ts.append(time.perf_counter() - t0)
+    return min(ts) * 1e3
+
+
+ln = C.c_int64()
+for kind in ("pageable", "pinned"):
+    fout = np.empty(rec_bytes, np.uint8) if kind == "pageable" else pinned_empty(rec_bytes)
+    cout = np.empty(shard_bytes, np.uint8) if kind == "pageable" else pinned_empty(shard_bytes)
+    t = best_ms(lambda: L.dml_store_fetch_range(store._h, 0, bench.ROWS - 1, fout.ctypes.data, rec_bytes,
+                                                C.byref(ln)))
+    res[f"fetch_range_full_shard_{kind}"] = {"ms": round(t, 3), "GBps": round(rec_bytes / t / 1e6, 2)}
+    t = best_ms(lambda: L.dml_store_write_all(store._h, cout.ctypes.data, shard_bytes, C.byref(ln)))
+    res[f"write_all_{kind}"] = {"ms": round(t, 3), "GBps": round(shard_bytes / t / 1e6, 2)}
+    t = best_ms(lambda: L.dml_store_read_all(store._h, cout.ctypes.data, shard_bytes))
+    res[f"read_all_{kind}"] = {"ms": round(t, 3), "GBps": round(shard_bytes / t / 1e6, 2)}
+# random-key fetch: 4096 keys
+keys = np.random.default_rng(1).integers(0, bench.ROWS, 4096).astype(np.int64)
+kout = pinned_empty(4096 * (4 + 4 * bench.COLS))
+t = best_ms(lambda: L.dml_store_fetch(store._h, keys.ctypes.data_as(C.POINTER(C.c_int64)), len(keys),
+                                      kout.ctypes.data, kout.nbytes, C.byref(ln)))
+res["fetch_4096_random_keys_pinned"] = {"ms": round(t, 3), "GBps": round(kout.nbytes / t / 1e6, 2)}
+# Python mirror (adds the bytes object the Java-style API returns)
 t0 = time.perf_counter()
 blob = store.handleFetch(fmt, KeyRange(0, bench.ROWS - 1))
 tf = time.perf_counter() - t0
-res["fetch_full_shard_ms"] = round(tf * 1e3, 2)
-res["fetch_GBps"] = round(len(blob) / tf / 1e9, 2)
+res["handleFetch_python_bytes_ms"] = round(tf * 1e3, 2)
 print(json.dumps(res))

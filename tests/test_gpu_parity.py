@@ -154,6 +154,71 @@ def test_array_random_parity(oracle, value_type, key_type, ref_stride):
     assert kat.bits_equal(s.values(), o.data)
 
 
+@pytest.mark.parametrize("value_type,api", [(1, "batch"), (3, "batch"), (1, "sequential")])
+def test_array_repeated_keys_in_push_exact(oracle, value_type, api):
+    """A push that lists a key several times (never produced by SparseArray.writeMap, but
+    legal bytes): the reference adds the repeats in record order. The ordered sparse path
+    sorts (row, sequence) per leaf, so the result is bit-exact; per-push float atomics
+    would not fix the order of the repeats."""
+    from distml_amd import DataDesc, encode_array_push
+    rng = np.random.default_rng(40 + value_type)
+    first, rows = 0, 50_000
+    fmt = DataDesc(0, 1, value_type)
+    s, _ = mk_store(fmt, first, first + rows - 1)
+    o = oracle_store(oracle, fmt, first, first + rows - 1)
+    init = rng.standard_normal((rows, 1)).astype(s.dtype)
+    s.load_values(init)
+    o.data[:] = init
+    pushes = []
+    for b in range(6):
+        k = rng.integers(0, 3_000, size=30_000)  # ~10 repeats of every key inside one push
+        v = rng.standard_normal(len(k)) * np.float64(2.0) ** rng.integers(-30, 10, size=len(k))
+        pushes.append(encode_array_push(first + k, v, 1, value_type))
+    for p in pushes:
+        assert o.push(p) == 0
+    if api == "batch":
+        s.handlePushBatch(fmt, pushes)
+    else:
+        for p in pushes:
+            s.handlePush(fmt, p)
+    assert kat.bits_equal(s.values(), o.data)
+    s.close()
+
+
+@pytest.mark.parametrize("value_type", [1, 3])
+def test_array_skewed_leaf_replay_exact(oracle, value_type):
+    """One key range holds far more records than a leaf sorts in LDS (2048): the leaf
+    kernel flags it and the host replays it from a full device sort, exactly."""
+    from distml_amd import DataDesc, encode_array_push
+    rng = np.random.default_rng(7 + value_type)
+    first, rows = 10, 1_000_000
+    fmt = DataDesc(0, 0, value_type)
+    s, _ = mk_store(fmt, first, first + rows - 1)
+    o = oracle_store(oracle, fmt, first, first + rows - 1)
+    init = rng.standard_normal((rows, 1)).astype(s.dtype)
+    s.load_values(init)
+    o.data[:] = init
+    pushes = []
+    for b in range(4):
+        hot = rng.integers(0, 64, size=6_000)            # 6000 records on 64 keys: one oversized leaf
+        cold = rng.choice(rows, size=20_000, replace=False)
+        k = rng.permutation(np.concatenate([hot, cold]))
+        v = rng.standard_normal(len(k)) * 1e-2
+        pushes.append(encode_array_push(first + k, v, 0, value_type))
+    for p in pushes:
+        assert o.push(p) == 0
+    s.handlePushBatch(fmt, pushes)
+    assert kat.bits_equal(s.values(), o.data)
+    # and a following batch after the replay (pipeline state intact)
+    more = [encode_array_push(first + rng.choice(rows, 5_000, replace=False), rng.standard_normal(5_000), 0,
+                              value_type) for _ in range(3)]
+    for p in more:
+        assert o.push(p) == 0
+    s.handlePushBatch(fmt, more)
+    assert kat.bits_equal(s.values(), o.data)
+    s.close()
+
+
 # ----------------------------------------------------------------- error semantics
 @pytest.mark.parametrize("kind", ["key", "trunc", "neg"])
 def test_batch_error_state_matches_sequential(oracle, kind):
@@ -302,6 +367,73 @@ def test_write_all_read_all_round_trip(oracle):
         s.syncTo(buf, 10, 20)
         assert buf.getvalue() == blob[10 * 13 * s.values().itemsize: 21 * 13 * s.values().itemsize]
         s.close()
+
+
+def test_large_fetch_checkpoint_bounce_and_pinned():
+    """80 MiB shard: fetch / writeAll / readAll / syncTo / syncFrom through the
+    pinned bounce ring (pageable buffers, 16 MiB chunks, last one partial) and
+    straight DMA (pinned_empty buffers); expected bytes built with numpy."""
+    from distml_amd import DataDesc, KeyRange, pinned_empty
+    rows, cols = 20_003, 1024
+    fmt = DataDesc(1, 0, 1)
+    s, _ = mk_store(fmt, 1000, 1000 + rows - 1, cols)
+    vals = np.random.default_rng(11).standard_normal((rows, cols)).astype(np.float32)
+    s.load_values(vals)
+    rec = np.empty((rows, 4 + 4 * cols), np.uint8)
+    rec[:, :4] = np.arange(1000, 1000 + rows, dtype="<i4").view(np.uint8).reshape(rows, 4)
+    rec[:, 4:] = vals.astype("<f4").view(np.uint8).reshape(rows, 4 * cols)
+    want = rec.tobytes()
+    assert s.handleFetch(fmt, KeyRange(0, 10**9)) == want
+    pin = pinned_empty(len(want))
+    assert s.handleFetchInto(fmt, KeyRange(1000, 1000 + rows - 1), pin) == len(want)
+    assert pin.tobytes() == want
+    be = vals.astype(">f4").tobytes()
+    assert s.writeAll() == be
+    s.zero()
+    s.readAll(io.BytesIO(be))
+    assert kat.bits_equal(s.values(), vals)
+    # pinned source for readAll-equivalent syncFrom of every row
+    s.zero()
+    pin_be = pinned_empty(len(be))
+    pin_be[:] = np.frombuffer(be, np.uint8)
+    s.syncFrom(pin_be, 0, rows - 1)
+    assert kat.bits_equal(s.values(), vals)
+    buf = io.BytesIO()
+    s.syncTo(buf, 7, 12_345)
+    assert buf.getvalue() == vals[7:12_346].astype(">f4").tobytes()
+    s.close()
+
+
+def test_sync_and_read_all_error_semantics():
+    """syncTo/syncFrom/readAll on bad rows or short streams: the reference moves the
+    rows / elements before the failure, then throws (AIOOBE / EOFException)."""
+    from distml_amd import DataDesc, DistMLException
+    fmt = DataDesc(1, 0, 0)
+    s, _ = mk_store(fmt, 0, 9, 3)
+    vals = np.arange(30, dtype=np.int32).reshape(10, 3)
+    s.load_values(vals)
+    buf = io.BytesIO()
+    with pytest.raises(DistMLException):
+        s.syncTo(buf, 8, 11)  # rows 8, 9 written, then row 10 is out of the shard
+    assert buf.getvalue() == vals[8:10].astype(">i4").tobytes()
+    buf = io.BytesIO()
+    with pytest.raises(DistMLException):
+        s.syncTo(buf, -1, 3)  # throws before writing
+    assert buf.getvalue() == b""
+    s.syncTo(buf, 5, 4)  # empty range: no bytes, no error
+    assert buf.getvalue() == b""
+    # short stream: 4 whole elements + 2 stray bytes -> rows 2..3 get 4 elements, then EOF
+    with pytest.raises(DistMLException):
+        s.syncFrom(io.BytesIO(np.array([-1, -2, -3, -4], ">i4").tobytes() + b"\x00\x01"), 2, 3)
+    got = s.values()
+    assert got[2].tolist() == [-1, -2, -3] and got[3].tolist() == [-4, 10, 11]
+    assert np.array_equal(got[4:], vals[4:]) and np.array_equal(got[:2], vals[:2])
+    prev = s.values().ravel()
+    with pytest.raises(DistMLException):
+        s.readAll(io.BytesIO(np.full(5, 7, ">i4").tobytes()))
+    got = s.values().ravel()
+    assert (got[:5] == 7).all() and np.array_equal(got[5:], prev[5:])
+    s.close()
 
 
 # ------------------------------------------------------- full-size configs (BASELINE.json)
