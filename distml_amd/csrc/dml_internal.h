@@ -128,7 +128,8 @@ hipError_t launch_synth_sparse(uint8_t* out, int K, int vtype, int value_stride,
                                hipStream_t st);
 // ---- ordered sparse scatter-add (dml_sparse.hip), float / double array stores ----
 constexpr int kSpTile = 4096;      // records per partition tile (256 threads x 16)
-constexpr int kSpLeafCap = 2048;   // records one leaf sorts in LDS
+constexpr int kSpLeafCap = 2048;   // records one leaf orders in LDS
+constexpr uint32_t kSpSkip = 0xFFFFFFFFu;  // sequence of a record at or past the cutoff (never applied)
 // Shape of one chunk's partition (host-computed, passed by value).
 struct SpPlan {
     int64_t tile_base[kMaxW + 1];  // first level-1 tile of push b (prefix of ceil(nrec / kSpTile))
@@ -144,12 +145,13 @@ struct SpMeta {
 };
 // Byte offsets of the partition buffers inside one workspace allocation.
 struct SpLayout {
-    size_t meta, comp1, val1, comp2, val2, cnt1, off1, cnt2, off2, leafflag, scan_tmp, scan_tmp_bytes, total;
+    size_t meta, comp1, val1, comp2, val2, cnt1, off1, cnt2, off2, leafflag, bounds, scan_tmp, scan_tmp_bytes,
+        total;
 };
 SpPlan sparse_plan(const Batch& bt, int nb, int64_t rows);
 SpLayout sparse_layout(const SpPlan& pl, int vbytes);
 hipError_t launch_sparse_partition(int vtype, const Batch& bt, const SpPlan& pl, const SpLayout& l, uint8_t* ws,
-                                   int64_t stride, int K, int64_t first, int64_t rows, const Ctrl* ctrl,
+                                   int64_t stride, int K, int64_t first, int64_t rows, Ctrl* ctrl,
                                    uint64_t tail_cut, hipStream_t st);
 hipError_t launch_sparse_leaf(int vtype, void* shard, const SpPlan& pl, const SpLayout& l, uint8_t* ws, Ctrl* ctrl,
                               const Ctrl* prev, hipStream_t st, LaunchEv ev);

@@ -8,18 +8,20 @@
 // partitioned by "leaf" = row >> SL (a key range holding ~1 K records on
 // average) with two 256-way digit passes (count -> exclusive scan -> scatter,
 // like one radix pass each; no ordering needed, seq travels along). A leaf
-// kernel then groups its records by row in LDS hash chains and applies each
-// row once: v = shard[row]; v += u_1; v += u_2 ... in sequence order;
-// shard[row] = v. That is the reference's value bit for bit, also when one push
-// repeats a key. A leaf's shard accesses stay inside one small row range
-// (DRAM-page friendly), which is what makes this faster than per-push scattered
-// atomics over the whole shard (scripts/ubench_scatter.hip).
+// kernel then orders its records by address in LDS (counting sort by shard
+// line) and applies each row once: v = shard[row]; v += u_1; v += u_2 ... in
+// sequence order; shard[row] = v. That is the reference's value bit for bit,
+// also when one push repeats a key. Address-ordered lanes share DRAM rows,
+// which is what makes this faster than per-push scattered atomics over the
+// whole shard (scripts/ubench_scatter.hip).
 //
-// Records at or past the chunk's cutoff (first key outside the shard / first
-// truncated access, found by k_array_validate) are dropped at partition time.
-// A leaf with more than kSpLeafCap records (skewed keys) is not applied by the
-// leaf kernel: it is flagged, Ctrl::no_dup is cleared, and the host replays the
-// flagged leaves from a full device sort of the chunk (sparse_replay).
+// The level-1 count finds the chunk's cutoff (first key outside the shard, or
+// the first truncated access): records at or past it keep their partition slot
+// with the sequence kSpSkip and are never applied.
+// A leaf with more than kSpLeafCap records, or a line bucket with more than
+// kSpBucketMax (skewed keys), is not applied by the leaf kernel: it is flagged,
+// Ctrl::no_dup is cleared, and the host replays the flagged leaves from a full
+// device sort of the chunk (sparse_replay).
 #include "dml_device.h"
 
 #include <hip/hip_ext.h>
@@ -31,11 +33,16 @@ namespace dml {
 
 namespace {
 
-// First partition tile of push b: scalar scan of the (<= 64) prefix entries.
+// Push of a level-1 tile: largest b with tile_base[b] <= tile (binary search over
+// the <= 64 prefix entries; a linear walk is a chain of dependent scalar loads).
 __device__ inline int push_of_tile(const SpPlan& pl, int64_t tile) {
-    int b = 0;
-    while (b + 1 < pl.nb && pl.tile_base[b + 1] <= tile) ++b;
-    return b;
+    int lo = 0, hi = pl.nb;
+    while (hi - lo > 1) {
+        const int mid = (lo + hi) >> 1;
+        if (pl.tile_base[mid] <= tile) lo = mid;
+        else hi = mid;
+    }
+    return lo;
 }
 
 // Records [lo, hi) of the chunk-wide first-level bin b: tile t of the bin, or
@@ -65,9 +72,14 @@ __device__ inline Tile2 tile2_of(const SpMeta* m, int nbins1, int64_t tile) {
 }  // namespace
 
 // ---- level 1: first digit of the leaf, straight from the wire records -------
+// COUNT pass: counts every record whose key lies in the shard and lowers
+// ctrl->cutoff to the first record whose key does not (the validation the
+// per-push path runs separately). SCATTER pass (cutoff final by then): writes
+// every counted record; records at or past the cutoff keep their slot but carry
+// the sequence kSpSkip and are never applied.
 template <typename T, bool SCATTER>
 __global__ __launch_bounds__(256) void k_sp_level1(const Batch bt, const SpPlan pl, int64_t stride, int K,
-                                                   int64_t first, int64_t rows, const Ctrl* __restrict__ ctrl,
+                                                   int64_t first, int64_t rows, Ctrl* __restrict__ ctrl,
                                                    uint64_t tail_cut, uint32_t* __restrict__ cnt1,
                                                    const uint32_t* __restrict__ off1, uint64_t* __restrict__ comp,
                                                    T* __restrict__ val) {
@@ -75,10 +87,15 @@ __global__ __launch_bounds__(256) void k_sp_level1(const Batch bt, const SpPlan 
     const int tid = threadIdx.x;
     const int64_t tile = blockIdx.x;
     const int b = push_of_tile(pl, tile);
+    if (!SCATTER && tile == 0 && tid == 0 && tail_cut != kNoPos)
+        atomicMin(&ctrl->cutoff, (unsigned long long)tail_cut);
     h[tid] = SCATTER ? (tid < pl.nbins1 ? off1[(int64_t)tid * pl.ntiles1 + tile] : 0u) : 0u;
     __syncthreads();
-    uint64_t cut = ctrl->cutoff;
-    if (tail_cut < cut) cut = tail_cut;
+    uint64_t cut = kNoPos;
+    if (SCATTER) {
+        cut = ctrl->cutoff;
+        if (tail_cut < cut) cut = tail_cut;
+    }
     const int64_t r0 = (tile - pl.tile_base[b]) * kSpTile + tid;
     const int64_t n = bt.nrec[b];
     const uint8_t* base = bt.base[b];
@@ -86,32 +103,39 @@ __global__ __launch_bounds__(256) void k_sp_level1(const Batch bt, const SpPlan 
     int64_t key[kPer];
 #pragma unroll
     for (int i = 0; i < kPer; ++i) {  // all key loads in flight first
-        const int64_t r = r0 + i * 256;
-        key[i] = r < n ? ld_key(base + r * stride, K) : first;
+        const int64_t r = min(r0 + i * 256, n - 1);
+        key[i] = ld_key(base + r * stride, K);
     }
     T u[kPer];
     if constexpr (SCATTER) {
 #pragma unroll
         for (int i = 0; i < kPer; ++i) {
-            const int64_t r = r0 + i * 256;
-            u[i] = r < n ? Elem<T>::load(base + r * stride + K) : T(0);
+            const int64_t r = min(r0 + i * 256, n - 1);
+            u[i] = Elem<T>::load(base + r * stride + K);
         }
     }
+    uint64_t bad = kNoPos;
 #pragma unroll
     for (int i = 0; i < kPer; ++i) {
         const int64_t r = r0 + i * 256;
-        if (r >= n || pos_of((uint64_t)bt.bidx[b], (uint64_t)(r * stride)) >= cut) continue;
-        const int64_t row = row_index(key[i], first, rows);  // in range: positions before the cutoff are valid
+        if (r >= n) continue;
+        const int64_t row = row_index(key[i], first, rows);
+        if (row < 0) {  // key outside the shard: the exception position
+            if (!SCATTER) bad = min(bad, pos_of((uint64_t)bt.bidx[b], (uint64_t)(r * stride)));
+            continue;
+        }
         const uint32_t bin = (uint32_t)((row >> pl.SL) >> pl.D2);
         if constexpr (SCATTER) {
             const uint32_t p = atomicAdd(&h[bin], 1u);
-            comp[p] = ((uint64_t)row << 32) | (uint64_t)(pl.rec_base[b] + r);
+            const bool skip = pos_of((uint64_t)bt.bidx[b], (uint64_t)(r * stride)) >= cut;
+            comp[p] = ((uint64_t)row << 32) | (skip ? (uint64_t)kSpSkip : (uint64_t)(pl.rec_base[b] + r));
             val[p] = u[i];
         } else {
             atomicAdd(&h[bin], 1u);
         }
     }
     if constexpr (!SCATTER) {
+        if (bad != kNoPos) atomicMin(&ctrl->cutoff, (unsigned long long)bad);
         __syncthreads();
         if (tid < pl.nbins1) cnt1[(int64_t)tid * pl.ntiles1 + tile] = h[tid];
     }
@@ -120,22 +144,34 @@ __global__ __launch_bounds__(256) void k_sp_level1(const Batch bt, const SpPlan 
 // ---- between the levels: bin bounds and the second-level tile table ---------
 __global__ __launch_bounds__(256) void k_sp_plan2(const SpPlan pl, const uint32_t* __restrict__ cnt1,
                                                   const uint32_t* __restrict__ off1, SpMeta* __restrict__ m) {
+    __shared__ int64_t wsum[4];
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     const int64_t cells = (int64_t)pl.nbins1 * pl.ntiles1;
     const int64_t kept = cells ? (int64_t)off1[cells - 1] + cnt1[cells - 1] : 0;
-    for (int b = threadIdx.x; b < pl.nbins1; b += blockDim.x) m->bin_start1[b] = off1[(int64_t)b * pl.ntiles1];
-    if (threadIdx.x == 0) {
+    // bin b (one per thread, nbins1 <= 256): start, and its level-2 tile count
+    int64_t start = 0, ntiles = 0;
+    if (tid < pl.nbins1) {
+        start = off1[(int64_t)tid * pl.ntiles1];
+        const int64_t end = tid + 1 < pl.nbins1 ? (int64_t)off1[(int64_t)(tid + 1) * pl.ntiles1] : kept;
+        ntiles = (end - start + kSpTile - 1) / kSpTile;
+        m->bin_start1[tid] = start;
+    }
+    if (tid == 0) {
         m->bin_start1[pl.nbins1] = kept;
         m->kept = kept;
     }
-    __syncthreads();
-    if (threadIdx.x == 0) {
-        int64_t acc = 0;
-        for (int b = 0; b < pl.nbins1; ++b) {
-            m->tile_start2[b] = acc;
-            acc += (m->bin_start1[b + 1] - m->bin_start1[b] + kSpTile - 1) / kSpTile;
-        }
-        m->tile_start2[pl.nbins1] = acc;
+    int64_t x = ntiles;  // inclusive scan of the tile counts
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+        const int64_t y = __shfl_up(x, o);
+        if (lane >= o) x += y;
     }
+    if (lane == 63) wsum[wave] = x;
+    __syncthreads();
+    int64_t base = 0;
+    for (int w = 0; w < wave; ++w) base += wsum[w];
+    if (tid < pl.nbins1) m->tile_start2[tid] = base + x - ntiles;
+    if (tid == pl.nbins1 - 1) m->tile_start2[pl.nbins1] = base + x;
 }
 
 // ---- level 2: second digit, within each first-level bin ---------------------
@@ -196,34 +232,48 @@ __device__ inline int64_t leaf_start(const SpPlan& pl, const SpMeta* m, const ui
     return nt ? (int64_t)off2[(m->tile_start2[b] << pl.D2) + d * nt] : m->bin_start1[b];
 }
 
-// ---- leaf: per-row ownership through LDS hash chains, ordered apply ----------
-// Records of the leaf go into kSpHash chains keyed by a hash of the row. A
-// record owns its row when no record of the same row has a smaller comp (=
-// earlier sequence). Owners of single-record rows (almost all) issue their
-// shard loads together and add once; owners of repeated rows walk their chain
-// in ascending comp order (the reference's record order) adding each value.
-// Chains longer than kSpChainMax (adversarial keys) send the whole leaf to the
-// exact replay instead, before any of its rows is written.
-constexpr int kSpHash = 4096;
-constexpr int kSpChainMax = 64;
+// Leaf bounds, computed once on the index stream: bounds[L] .. bounds[L + 1].
+__global__ __launch_bounds__(256) void k_sp_bounds(const SpPlan pl, const SpMeta* __restrict__ m,
+                                                   const uint32_t* __restrict__ off2, int64_t* __restrict__ bounds) {
+    const int64_t L = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (L <= pl.nleaves) bounds[L] = leaf_start(pl, m, off2, L);
+}
 
-__device__ inline uint32_t sp_hash(uint64_t row) { return ((uint32_t)row * 0x9E3779B1u) >> (32 - 12); }
-static_assert(kSpHash == 1 << 12, "sp_hash yields 12 bits");
+// ---- leaf: records in address order, one ordered RMW per row ---------------
+// A counting sort over kSpLines line buckets of the leaf's row range puts the
+// leaf's records in ascending address order (bucket = 32 rows = one 128-B line
+// at config-3 leaf sizes), so neighbouring lanes touch neighbouring shard lines
+// and a wave's accesses share DRAM rows (random 4-B RMW is bound by row
+// activations, scripts/ubench_scatter.hip). A record owns its row when no
+// record of the same row (same bucket) has a smaller comp (= earlier sequence).
+// Owners of single-record rows issue their shard loads together and add once;
+// owners of repeated rows walk their bucket in ascending comp order. Buckets
+// over kSpBucketMax records (adversarial keys) send the whole leaf to the exact
+// replay before any of its rows is written.
+constexpr int kSpLines = 1024;
+constexpr int kSpBucketMax = 64;
+constexpr int kSpLeafThreads = 512;  // 8 waves per leaf
 
 template <typename T>
-__global__ __launch_bounds__(256) void k_sp_leaf(T* __restrict__ shard, const SpPlan pl, const SpMeta* __restrict__ m,
-                                                 const uint32_t* __restrict__ off2, const uint64_t* __restrict__ comp,
-                                                 const T* __restrict__ val, uint8_t* __restrict__ leafflag,
-                                                 Ctrl* __restrict__ ctrl, const Ctrl* __restrict__ prev) {
-    __shared__ uint32_t head[kSpHash];
-    __shared__ uint16_t nxt[kSpLeafCap];
+__global__ __launch_bounds__(kSpLeafThreads) void k_sp_leaf(T* __restrict__ shard, const int64_t* __restrict__ bounds,
+                                                            const uint64_t* __restrict__ comp,
+                                                            const T* __restrict__ val, int SL, int bshift,
+                                                            uint8_t* __restrict__ leafflag, Ctrl* __restrict__ ctrl,
+                                                            const Ctrl* __restrict__ prev) {
+    constexpr int kT = kSpLeafThreads;
+    constexpr int kPer = kSpLeafCap / kT;
+    static_assert(kSpLines == 2 * kT, "the scan gives each thread two buckets");
     __shared__ uint64_t sc[kSpLeafCap];
     __shared__ T sv[kSpLeafCap];
+    __shared__ uint16_t perm[kSpLeafCap];
+    __shared__ uint32_t bstart[kSpLines + 1];
+    __shared__ uint32_t cur[kSpLines];
+    __shared__ uint32_t wsum[kT / 64];
     __shared__ int s_over;
     if (prev && ctrl_abnormal(prev)) return;  // predecessor needs the host first
     const int tid = threadIdx.x;
     const int64_t L = blockIdx.x;
-    const int64_t lo = leaf_start(pl, m, off2, L), hi = leaf_start(pl, m, off2, L + 1);
+    const int64_t lo = bounds[L], hi = bounds[L + 1];
     const int n = (int)(hi - lo);
     if (hi - lo <= 0) return;
     if (hi - lo > kSpLeafCap) {  // skewed leaf: exact replay on the host's request
@@ -233,43 +283,88 @@ __global__ __launch_bounds__(256) void k_sp_leaf(T* __restrict__ shard, const Sp
         }
         return;
     }
-    constexpr int kPer = kSpLeafCap / 256;
-    for (int i = tid; i < kSpHash; i += 256) head[i] = 0xFFFFFFFFu;
+    const uint64_t row0 = (uint64_t)L << SL;
+    for (int i = tid; i < kSpLines; i += kT) cur[i] = 0;
     if (tid == 0) s_over = 0;
+    // loads from clamped in-range indices, all in flight before the first use
+    // (a load under `if (i < n)` gets its own vmcnt(0) wait)
     uint64_t c[kPer];
+    T u[kPer];
+    uint32_t bk[kPer];
 #pragma unroll
     for (int k = 0; k < kPer; ++k) {
-        const int i = tid + k * 256;
-        c[k] = i < n ? comp[lo + i] : 0;
+        const int i = min(tid + k * kT, n - 1);
+        c[k] = comp[lo + i];
+        u[k] = val[lo + i];
+    }
+#pragma unroll
+    for (int k = 0; k < kPer; ++k) {
+        const int i = tid + k * kT;
+        bk[k] = (uint32_t)(((c[k] >> 32) - row0) >> bshift);
+        if (i < n) sv[i] = u[k];
+    }
+    __syncthreads();
+#pragma unroll
+    for (int k = 0; k < kPer; ++k) {
+        const int i = tid + k * kT;
         if (i < n) {
             sc[i] = c[k];
-            sv[i] = val[lo + i];
+            atomicAdd(&cur[bk[k]], 1u);
         }
     }
     __syncthreads();
+    {  // exclusive scan of the bucket counts: thread t owns buckets 2t, 2t+1
+        const uint32_t a0 = cur[2 * tid], a1 = cur[2 * tid + 1];
+        uint32_t x = a0 + a1;
+        const int lane = tid & 63, wave = tid >> 6;
+#pragma unroll
+        for (int o = 1; o < 64; o <<= 1) {
+            const uint32_t y = __shfl_up(x, o);
+            if (lane >= o) x += y;
+        }
+        if (lane == 63) wsum[wave] = x;
+        __syncthreads();
+        uint32_t base = 0;
+        for (int w = 0; w < wave; ++w) base += wsum[w];
+        const uint32_t ex = base + x - (a0 + a1);
+        bstart[2 * tid] = ex;
+        bstart[2 * tid + 1] = ex + a0;
+        __syncthreads();
+        cur[2 * tid] = ex;
+        cur[2 * tid + 1] = ex + a0;
+        if (tid == 0) bstart[kSpLines] = (uint32_t)n;
+        __syncthreads();
+    }
 #pragma unroll
     for (int k = 0; k < kPer; ++k) {
-        const int i = tid + k * 256;
-        if (i < n) nxt[i] = (uint16_t)atomicExch(&head[sp_hash(c[k] >> 32)], (uint32_t)i);
+        const int i = tid + k * kT;
+        if (i < n) perm[atomicAdd(&cur[bk[k]], 1u)] = (uint16_t)i;
     }
     __syncthreads();
+    // ownership, in address order: sorted position p = tid + k * kT
+    int ri[kPer];
     bool own[kPer], multi[kPer];
 #pragma unroll
     for (int k = 0; k < kPer; ++k) {
-        const int i = tid + k * 256;
+        const int p = tid + k * kT;
         own[k] = multi[k] = false;
-        if (i >= n) continue;
-        const uint64_t row = c[k] >> 32;
-        int len = 0;
+        ri[k] = 0;
+        if (p >= n) continue;
+        const int i = perm[p];
+        ri[k] = i;
+        const uint64_t ci = sc[i], row = ci >> 32;
+        if ((uint32_t)ci == kSpSkip) continue;  // past the cutoff: never applied
+        const uint32_t b = (uint32_t)((row - row0) >> bshift);
+        const uint32_t bs = bstart[b], be = bstart[b + 1];
+        if (be - bs > (uint32_t)kSpBucketMax) s_over = 1;
         bool first = true, dup = false;
-        for (uint32_t j = head[sp_hash(row)]; j < (uint32_t)kSpLeafCap; j = nxt[j]) {
-            ++len;
-            if ((int)j != i && (sc[j] >> 32) == row) {
+        for (uint32_t q = bs; q < be; ++q) {
+            const uint64_t cj = sc[perm[q]];
+            if (cj != ci && (cj >> 32) == row && (uint32_t)cj != kSpSkip) {
                 dup = true;
-                first &= sc[j] > c[k];
+                first &= cj > ci;
             }
         }
-        if (len > kSpChainMax) s_over = 1;
         own[k] = first;
         multi[k] = dup;
     }
@@ -281,39 +376,44 @@ __global__ __launch_bounds__(256) void k_sp_leaf(T* __restrict__ shard, const Sp
         }
         return;
     }
-    T cur[kPer];
+    T v[kPer];
+    uint64_t rw[kPer];
 #pragma unroll
-    for (int k = 0; k < kPer; ++k)  // every owner's shard load in flight together
-        if (own[k]) cur[k] = shard[c[k] >> 32];
+    for (int k = 0; k < kPer; ++k) rw[k] = own[k] ? sc[ri[k]] >> 32 : row0;  // row0: a valid row of this leaf
+#pragma unroll
+    for (int k = 0; k < kPer; ++k) v[k] = shard[rw[k]];  // every shard load in flight together
 #pragma unroll
     for (int k = 0; k < kPer; ++k) {
         if (!own[k]) continue;
-        const int i = tid + k * 256;
-        const uint64_t row = c[k] >> 32;
-        T v = cur[k];
+        const int i = ri[k];
+        const uint64_t row = rw[k];
+        T x = v[k];
         if (!multi[k]) {
-            v = Elem<T>::add(v, sv[i]);
+            x = Elem<T>::add(x, sv[i]);
         } else {
             // this row's records in ascending comp (= sequence) order
+            const uint32_t b = (uint32_t)((row - row0) >> bshift);
+            const uint32_t bs = bstart[b], be = bstart[b + 1];
             uint64_t last = 0;
             bool started = false;
             for (;;) {
                 uint64_t best = ~0ull;
                 int bj = -1;
-                for (uint32_t j = head[sp_hash(row)]; j < (uint32_t)kSpLeafCap; j = nxt[j]) {
+                for (uint32_t q = bs; q < be; ++q) {
+                    const int j = perm[q];
                     const uint64_t cj = sc[j];
-                    if ((cj >> 32) == row && (!started || cj > last) && cj < best) {
+                    if ((cj >> 32) == row && (uint32_t)cj != kSpSkip && (!started || cj > last) && cj < best) {
                         best = cj;
-                        bj = (int)j;
+                        bj = j;
                     }
                 }
                 if (bj < 0) break;
-                v = Elem<T>::add(v, sv[bj]);
+                x = Elem<T>::add(x, sv[bj]);
                 last = best;
                 started = true;
             }
         }
-        shard[row] = v;
+        shard[row] = x;
     }
 }
 
@@ -327,8 +427,11 @@ __global__ __launch_bounds__(256) void k_sp_runs(T* __restrict__ shard, const ui
     const uint64_t row = comp[p] >> 32;
     if (!leafflag[row >> SL]) return;
     if (p > 0 && (comp[p - 1] >> 32) == row) return;
+    if ((uint32_t)comp[p] == kSpSkip) return;  // the row's only records are past the cutoff
     T v = shard[row];
-    for (int64_t q = p; q < n && (comp[q] >> 32) == row; ++q) v = Elem<T>::add(v, val[q]);
+    // the row's run in sequence order; records past the cutoff (kSpSkip) sort last
+    for (int64_t q = p; q < n && (comp[q] >> 32) == row && (uint32_t)comp[q] != kSpSkip; ++q)
+        v = Elem<T>::add(v, val[q]);
     shard[row] = v;
 }
 
@@ -386,6 +489,7 @@ SpLayout sparse_layout(const SpPlan& pl, int vbytes) {
     l.cnt2 = take(cells2 * 4);
     l.off2 = take(cells2 * 4);
     l.leafflag = take((size_t)pl.nleaves);
+    l.bounds = take(((size_t)pl.nleaves + 1) * 8);
     size_t t1 = 0, t2 = 0;
     (void)hipcub::DeviceScan::ExclusiveSum(nullptr, t1, (uint32_t*)nullptr, (uint32_t*)nullptr, (int)cells1);
     (void)hipcub::DeviceScan::ExclusiveSum(nullptr, t2, (uint32_t*)nullptr, (uint32_t*)nullptr, (int)cells2);
@@ -396,8 +500,7 @@ SpLayout sparse_layout(const SpPlan& pl, int vbytes) {
 
 template <typename T>
 static hipError_t partition_t(const Batch& bt, const SpPlan& pl, const SpLayout& l, uint8_t* ws, int64_t stride,
-                              int K, int64_t first, int64_t rows, const Ctrl* ctrl, uint64_t tail_cut,
-                              hipStream_t st) {
+                              int K, int64_t first, int64_t rows, Ctrl* ctrl, uint64_t tail_cut, hipStream_t st) {
     SpMeta* m = (SpMeta*)(ws + l.meta);
     uint64_t* comp1 = (uint64_t*)(ws + l.comp1);
     uint64_t* comp2 = (uint64_t*)(ws + l.comp2);
@@ -417,6 +520,9 @@ static hipError_t partition_t(const Batch& bt, const SpPlan& pl, const SpLayout&
         hipLaunchKernelGGL((k_sp_level1<T, false>), dim3((unsigned)pl.ntiles1), dim3(256), 0, st, bt, pl, stride, K,
                            first, rows, ctrl, tail_cut, cnt1, (const uint32_t*)nullptr, (uint64_t*)nullptr, (T*)nullptr);
         if ((e = hipGetLastError()) != hipSuccess) return e;
+    } else if (tail_cut != kNoPos) {  // no complete record: only the truncation position
+        if ((e = hipMemcpyAsync(&ctrl->cutoff, &tail_cut, sizeof tail_cut, hipMemcpyHostToDevice, st)) != hipSuccess)
+            return e;
     }
     size_t tb = l.scan_tmp_bytes;
     if ((e = hipcub::DeviceScan::ExclusiveSum(ws + l.scan_tmp, tb, cnt1, off1, cells1, st)) != hipSuccess) return e;
@@ -441,11 +547,13 @@ static hipError_t partition_t(const Batch& bt, const SpPlan& pl, const SpLayout&
                            (const T*)val1, comp2, val2);
         if ((e = hipGetLastError()) != hipSuccess) return e;
     }
-    return hipSuccess;
+    hipLaunchKernelGGL(k_sp_bounds, dim3((unsigned)((pl.nleaves + 1 + 255) / 256)), dim3(256), 0, st, pl,
+                       (const SpMeta*)m, (const uint32_t*)off2, (int64_t*)(ws + l.bounds));
+    return hipGetLastError();
 }
 
 hipError_t launch_sparse_partition(int vtype, const Batch& bt, const SpPlan& pl, const SpLayout& l, uint8_t* ws,
-                                   int64_t stride, int K, int64_t first, int64_t rows, const Ctrl* ctrl,
+                                   int64_t stride, int K, int64_t first, int64_t rows, Ctrl* ctrl,
                                    uint64_t tail_cut, hipStream_t st) {
     if (vtype == kF32) return partition_t<float>(bt, pl, l, ws, stride, K, first, rows, ctrl, tail_cut, st);
     if (vtype == kF64) return partition_t<double>(bt, pl, l, ws, stride, K, first, rows, ctrl, tail_cut, st);
@@ -455,17 +563,21 @@ hipError_t launch_sparse_partition(int vtype, const Batch& bt, const SpPlan& pl,
 hipError_t launch_sparse_leaf(int vtype, void* shard, const SpPlan& pl, const SpLayout& l, uint8_t* ws, Ctrl* ctrl,
                               const Ctrl* prev, hipStream_t st, LaunchEv ev) {
     if (pl.nleaves <= 0) return hipSuccess;
-    const SpMeta* m = (const SpMeta*)(ws + l.meta);
-    const uint32_t* off2 = (const uint32_t*)(ws + l.off2);
+    const int64_t* bounds = (const int64_t*)(ws + l.bounds);
     const uint64_t* comp2 = (const uint64_t*)(ws + l.comp2);
     uint8_t* flag = ws + l.leafflag;
     const dim3 grid((unsigned)pl.nleaves);
+    // line buckets: leaf rows >> bshift < kSpLines
+    int bshift = 0;
+    while ((((int64_t)1 << pl.SL) >> bshift) > kSpLines) ++bshift;
     if (vtype == kF32)
-        hipExtLaunchKernelGGL(k_sp_leaf<float>, grid, dim3(256), 0, st, ev.start, ev.stop, 0, (float*)shard, pl, m,
-                              off2, comp2, (const float*)(ws + l.val2), flag, ctrl, prev);
+        hipExtLaunchKernelGGL(k_sp_leaf<float>, grid, dim3(kSpLeafThreads), 0, st, ev.start, ev.stop, 0,
+                              (float*)shard, bounds, comp2, (const float*)(ws + l.val2), pl.SL, bshift, flag, ctrl,
+                              prev);
     else if (vtype == kF64)
-        hipExtLaunchKernelGGL(k_sp_leaf<double>, grid, dim3(256), 0, st, ev.start, ev.stop, 0, (double*)shard, pl, m,
-                              off2, comp2, (const double*)(ws + l.val2), flag, ctrl, prev);
+        hipExtLaunchKernelGGL(k_sp_leaf<double>, grid, dim3(kSpLeafThreads), 0, st, ev.start, ev.stop, 0,
+                              (double*)shard, bounds, comp2, (const double*)(ws + l.val2), pl.SL, bshift, flag,
+                              ctrl, prev);
     else
         return hipErrorInvalidValue;
     return hipGetLastError();

@@ -369,20 +369,26 @@ int launch_chunk(dml_store* s, Chunk& c, Workspace& W, const Ctrl* prev) {
     // DML_SERIAL_INDEX=1: index on the apply stream (A/B of the overlap; no cross-queue wait)
     static const bool serial = getenv("DML_SERIAL_INDEX") && atoi(getenv("DML_SERIAL_INDEX"));
     hipStream_t is = serial ? s->stream : s->istream;
+    if (serial) {  // host pushes are DMA'd on the index stream: the apply stream waits for them
+        HIPCHK(hipEventRecord(W.idx_done, s->istream));
+        HIPCHK(hipStreamWaitEvent(s->stream, W.idx_done, 0));
+    }
     HIPCHK(hipMemsetAsync(W.base, 0xFF, sizeof(Ctrl) + s->slot_bytes, is));
     if (s->is_matrix) {
         HIPCHK(hipMemsetAsync(W.rowflag, 0, (size_t)s->rows * sizeof(uint32_t), is));
         HIPCHK(launch_index(c.bt, c.nb, c.max_nrec, s->stride, s->K, s->first, s->rows, W.slot, W.rowflag, W.ctrl,
                             c.tail_cut, is));
     } else {
-        HIPCHK(launch_array_validate(c.bt, c.nb, c.max_nrec, s->stride, s->K, s->first, s->rows, W.ctrl, c.tail_cut,
-                                     is));
         // float / double arrays: partition the chunk by leaf (row range) for the ordered
-        // per-leaf apply; int32 arrays keep the per-push atomic path (negativity check).
-        // DML_SPARSE_ATOMIC=1 forces the per-push path (A/B).
+        // per-leaf apply (its first pass also finds the cutoff); int32 arrays keep the
+        // validated per-push atomic path (negativity check). DML_SPARSE_ATOMIC=1 forces
+        // the per-push path (A/B).
         static const bool atomic_only = getenv("DML_SPARSE_ATOMIC") && atoi(getenv("DML_SPARSE_ATOMIC"));
         const int vt = vtype_of(s->desc);
         c.sorted = !atomic_only && (vt == kF32 || vt == kF64);
+        if (!c.sorted)
+            HIPCHK(launch_array_validate(c.bt, c.nb, c.max_nrec, s->stride, s->K, s->first, s->rows, W.ctrl,
+                                         c.tail_cut, is));
         if (c.sorted) {
             c.sp = sparse_plan(c.bt, c.nb, s->rows);
             c.spl = sparse_layout(c.sp, s->V);
