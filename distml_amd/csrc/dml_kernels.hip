@@ -397,7 +397,221 @@ __global__ __launch_bounds__(64 * WPB) void k_reduce(T* __restrict__ shard, int6
     }
 }
 
-template <typename T, int MODE, int G = 8, bool NT = false, int WPB = 4, bool SNT = false, int CPW = 1>
+// ---------------------------------------------------------------------------
+// k_reduce_rows: the plain-sum shapes (kAdd, kAddCheckI32, kPreReduce) with
+// RPW neighbouring rows per wave. One push at a time: the wave scalar-loads the
+// push's base / index and its RPW slots, issues RPW x CPW 16-B nt loads (16 for
+// config 2: four whole records), then adds them in push order. Fewer, longer
+// waves whose shard reads and write-backs come in RPW x larger bursts: measured
+// +8..20 % over one row per wave on config 2 (scripts/ubench_reduce.hip).
+// A batch with a cutoff (key / truncation error) takes a register-light
+// element-wise path instead (in-place RMW of the wave's own rows, same order),
+// so the hot loop carries no cutoff logic. Same results as k_reduce bit for bit
+// (same per-element add order, cutoff and negativity rules); rows narrower than
+// one vector use k_reduce.
+template <typename T, int MODE, int CPW, int RPW, bool NT, bool FULL>
+__global__ __launch_bounds__(256) void k_reduce_rows(T* __restrict__ shard, int64_t rows, int32_t cols,
+                                                     int32_t ngroups, const Batch bt, int nb, int64_t stride, int K,
+                                                     const int32_t* __restrict__ slot,
+                                                     const uint32_t* __restrict__ rowflag, Ctrl* __restrict__ ctrl,
+                                                     uint64_t tail_cut, RowMap rm) {
+    constexpr int VEC = Elem<T>::VEC;
+    static_assert(MODE == kAdd || MODE == kAddCheckI32 || MODE == kPreReduce, "plain-sum modes only");
+    const int lane = threadIdx.x & 63;
+    const int wid = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    const int64_t task = (int64_t)blockIdx.x * 4 + wid;
+    const int64_t ntask = (rows + RPW - 1) / RPW * (int64_t)ngroups;
+    if (task >= ntask) return;
+    if (bt.prev && ctrl_abnormal(bt.prev)) return;  // predecessor needs the host first
+    const int64_t tb = task / ngroups;
+    const int cg = (int)(task - tb * ngroups);
+
+    int32_t c0[CPW];
+    int nv[CPW], sh[CPW];
+    int64_t voff[CPW], shb[CPW];
+#pragma unroll
+    for (int c = 0; c < CPW; ++c) {
+        c0[c] = ((cg * CPW + c) * 64 + lane) * VEC;
+        // FULL: cols is a multiple of 64*VEC*CPW (every lane owns whole vectors; the
+        // chunk offsets fold into the loads' immediate offsets)
+        nv[c] = FULL ? VEC : c0[c] < cols ? (cols - c0[c] < VEC ? cols - c0[c] : VEC) : 0;
+        sh[c] = nv[c] > 0 ? VEC - nv[c] : 0;  // ragged last lane: load the 16 B ending at its last element
+        shb[c] = (int64_t)sh[c] * (int64_t)sizeof(T);
+        voff[c] = (int64_t)K + (int64_t)c0[c] * (int64_t)sizeof(T);
+    }
+    // Lanes past the row's last column (nv == 0) stay in the wave: every access
+    // below is guarded by nv, and the batch table below is read from all 64 lanes.
+
+    int64_t row[RPW];
+    T* rowp[RPW];
+    unsigned live = 0;
+    const uint8_t* fb = nullptr;  // a readable address inside a live row (target of absent loads)
+#pragma unroll
+    for (int r = 0; r < RPW; ++r) {
+        const int64_t trow = tb * RPW + r;
+        const int64_t tr = trow < rows ? trow : tb * RPW;
+        row[r] = rm.block ? (tr / rm.block) * rm.stride + rm.off + tr % rm.block : tr;
+        rowp[r] = rm.out ? (T*)rm.out + tr * (int64_t)cols : shard + row[r] * (int64_t)cols;
+        if (trow >= rows) continue;
+        if (rm.block && row[r] >= rm.rows_total) {  // padding row of a short last shard: zeros
+#pragma unroll
+            for (int c = 0; c < CPW; ++c)
+#pragma unroll
+                for (int e = 0; e < VEC; ++e)
+                    if (e < nv[c]) rowp[r][c0[c] + e] = T(0);
+            continue;
+        }
+        if (rowflag && rowflag[row[r]]) continue;  // a push repeats this row: the host replays it exactly
+        live |= 1u << r;
+        if (!fb) fb = (const uint8_t*)rowp[r];
+    }
+    if (!live) return;
+
+    uint64_t cut = ctrl->cutoff;
+    if (tail_cut < cut) cut = tail_cut;
+    uint64_t negpos = kNoPos;  // kAddCheckI32: earliest add that left a counter negative
+
+    if (cut != kNoPos) {
+        // Error batch: element-wise RMW of the wave's rows in place, pushes in order,
+        // stopping at the cutoff byte (the state the reference leaves when it throws).
+        const int cut_b = (int)(cut >> 40);
+        const uint64_t cut_off = cut & kOffMask;
+        for (int r = 0; r < RPW; ++r) {
+            if (!(live >> r & 1u)) continue;
+            T* const rp = rowp[r];
+            if (MODE == kPreReduce)
+                for (int c = 0; c < CPW; ++c)
+                    for (int e = 0; e < nv[c]; ++e) rp[c0[c] + e] = T(0);
+            const int32_t* srow = slot + row[r] * kMaxW;
+            for (int b = 0; b < nb; ++b) {
+                const int gb = bt.bidx[b];
+                if (gb > cut_b) break;
+                const int32_t rr = srow[b];
+                if (rr < 0) continue;
+                for (int c = 0; c < CPW; ++c)
+                    for (int e = 0; e < nv[c]; ++e) {
+                        const uint64_t off = (uint64_t)((int64_t)rr * stride + voff[c] + e * (int64_t)sizeof(T));
+                        if (gb == cut_b && off >= cut_off) break;
+                        const T v = Elem<T>::add(rp[c0[c] + e], Elem<T>::load(bt.base[b] + off));
+                        rp[c0[c] + e] = v;
+                        if (MODE == kAddCheckI32 && v < 0) {
+                            const uint64_t p = pos_of((uint64_t)gb, off);
+                            if (p < negpos) negpos = p;
+                        }
+                    }
+            }
+        }
+        if (MODE == kAddCheckI32 && negpos != kNoPos) atomicMin(&ctrl->neg_pos, (unsigned long long)negpos);
+        return;
+    }
+
+    // The wave's shard rows, loaded up front (a row no push lists is read but not written).
+    T acc[RPW][CPW][VEC];
+#pragma unroll
+    for (int r = 0; r < RPW; ++r)
+#pragma unroll
+        for (int c = 0; c < CPW; ++c) {
+            const bool ld = MODE != kPreReduce && (live >> r & 1u);
+            if (ld && nv[c] == VEC) {
+                unpack<T>(ldg16((const uint8_t*)(rowp[r] + c0[c])), acc[r][c]);
+            } else {
+#pragma unroll
+                for (int e = 0; e < VEC; ++e) acc[r][c][e] = ld && e < nv[c] ? rowp[r][c0[c] + e] : T(0);
+            }
+        }
+    unsigned touched = 0;
+    const uint8_t* const fbv = fb + (int64_t)c0[0] * (int64_t)sizeof(T);  // FULL: absent rows re-read a live row
+    // The batch table in registers, lane j = push j (kMaxW == 64 == wave size): the
+    // rows' slots and the push bases, read per push with v_readlane (no scalar-memory
+    // round trip between two pushes' loads). All 64 lanes are active here (no lane
+    // has returned), so every lane v_readlane reads holds its value.
+    static_assert(kMaxW == 64, "one push per lane");
+    int32_t vslot[RPW];
+#pragma unroll
+    for (int r = 0; r < RPW; ++r) vslot[r] = (live >> r & 1u) ? slot[row[r] * kMaxW + lane] : -1;
+    const uint64_t vbase = lane < nb ? (uint64_t)bt.base[lane] : 0ull;
+#pragma unroll 1
+    for (int b = 0; b < nb; ++b) {
+        int32_t rr[RPW];
+        unsigned has = 0;
+#pragma unroll
+        for (int r = 0; r < RPW; ++r) {
+            rr[r] = __builtin_amdgcn_readlane(vslot[r], b);
+            has |= (rr[r] >= 0 ? 1u : 0u) << r;
+        }
+        if (!has) continue;
+        touched |= has;
+        const uint8_t* bp = (const uint8_t*)(((uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)vbase, b)) |
+                                             ((uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)(vbase >> 32), b) << 32));
+        u32x4 raw[RPW][CPW];
+#pragma unroll
+        for (int r = 0; r < RPW; ++r) {
+            if constexpr (FULL) {
+                // one address per row; the chunks are immediate offsets of the loads
+                const uint8_t* rb = rr[r] >= 0 ? bp + (int64_t)rr[r] * stride + voff[0] : fbv;
+#pragma unroll
+                for (int c = 0; c < CPW; ++c) {
+                    const uint8_t* src = rb + c * 64 * VEC * (int)sizeof(T);
+                    raw[r][c] = NT ? ldg16_nt(src) : ldg16(src);
+                }
+            } else {
+#pragma unroll
+                for (int c = 0; c < CPW; ++c) {
+                    const uint8_t* src =
+                        (rr[r] >= 0 && nv[c] > 0) ? bp + (int64_t)rr[r] * stride + voff[c] - shb[c] : fb;
+                    raw[r][c] = NT ? ldg16_nt(src) : ldg16(src);
+                }
+            }
+        }
+#pragma unroll
+        for (int r = 0; r < RPW; ++r) {
+            if (rr[r] < 0) continue;  // wave-uniform
+#pragma unroll
+            for (int c = 0; c < CPW; ++c) {
+                T t[VEC], u[VEC];
+                unpack<T>(raw[r][c], t);
+#pragma unroll
+                for (int e = 0; e < VEC; ++e) {  // u[e] = t[e + sh] without runtime register indexing
+                    u[e] = t[e];
+#pragma unroll
+                    for (int k = 1; k < VEC - e; ++k) u[e] = sh[c] == k ? t[e + k] : u[e];
+                }
+#pragma unroll
+                for (int e = 0; e < VEC; ++e)
+                    if (e < nv[c]) {
+                        acc[r][c][e] = Elem<T>::add(acc[r][c][e], u[e]);
+                        if constexpr (MODE == kAddCheckI32)
+                            if (acc[r][c][e] < 0) {
+                                const uint64_t p = pos_of((uint64_t)bt.bidx[b],
+                                                          (uint64_t)((int64_t)rr[r] * stride + voff[c] + e * (int64_t)sizeof(T)));
+                                if (p < negpos) negpos = p;  // min over positions = first in the reference's order
+                            }
+                    }
+            }
+        }
+    }
+
+    if (MODE == kPreReduce) touched = live;  // every pre-reduce row is written (zeros if no push has it)
+#pragma unroll
+    for (int r = 0; r < RPW; ++r) {
+        if (!(touched >> r & 1u)) continue;
+#pragma unroll
+        for (int c = 0; c < CPW; ++c) {
+            T* prow = rowp[r] + c0[c];
+            if (nv[c] == VEC) {
+                stg16(prow, pack<T>(acc[r][c]));
+            } else {
+#pragma unroll
+                for (int e = 0; e < VEC; ++e)
+                    if (e < nv[c]) prow[e] = acc[r][c][e];
+            }
+        }
+    }
+    if (MODE == kAddCheckI32 && negpos != kNoPos) atomicMin(&ctrl->neg_pos, (unsigned long long)negpos);
+}
+
+template <typename T, int MODE, int G = 8, bool NT = false, int WPB = 4, bool SNT = false, int CPW = 1, int RPW = 1,
+          bool FULL = false>
 static hipError_t launch_reduce_t(void* shard, int64_t rows, int32_t cols, const Batch& bt, int nb,
                                   int64_t stride, int K, const int32_t* slot, const uint32_t* rowflag, Ctrl* ctrl,
                                   uint64_t tail_cut,
@@ -406,48 +620,78 @@ static hipError_t launch_reduce_t(void* shard, int64_t rows, int32_t cols, const
     constexpr int VEC = Elem<T>::VEC;
     const int32_t nchunks = (cols + 64 * VEC - 1) / (64 * VEC);
     const int32_t ngroups = (nchunks + CPW - 1) / CPW;
-    const int64_t ntask = rows * ngroups;
+    const int64_t ntask = (rows + RPW - 1) / RPW * ngroups;
     const int64_t nblocks = (ntask + WPB - 1) / WPB;
     if (nblocks_out) *nblocks_out = nblocks;
     if (nblocks <= 0) return hipSuccess;
-    if (ev.start || ev.stop)
-        hipExtLaunchKernelGGL((k_reduce<T, MODE, G, NT, WPB, SNT, CPW>), dim3((unsigned)nblocks), dim3(64 * WPB), 0,
-                              st, ev.start, ev.stop, 0, (T*)shard, rows, cols, ngroups, bt, nb, stride, K, slot,
-                              rowflag, ctrl, tail_cut, ada, rm);
-    else
-        hipLaunchKernelGGL((k_reduce<T, MODE, G, NT, WPB, SNT, CPW>), dim3((unsigned)nblocks), dim3(64 * WPB), 0, st,
-                           (T*)shard, rows, cols, ngroups, bt, nb, stride, K, slot, rowflag, ctrl, tail_cut, ada, rm);
+    // experiment knob: dynamic LDS per block caps the blocks resident per CU (occupancy study)
+    static const unsigned occ_lds = getenv("DML_REDUCE_LDS") ? (unsigned)atoi(getenv("DML_REDUCE_LDS")) : 0u;
+    if constexpr (RPW > 1) {
+        static_assert(WPB == 4 && MODE != kAdaGrad && MODE != kRollbackI32, "k_reduce_rows shapes");
+        if (ev.start || ev.stop)
+            hipExtLaunchKernelGGL((k_reduce_rows<T, MODE, CPW, RPW, NT, FULL>), dim3((unsigned)nblocks), dim3(256),
+                                  occ_lds, st, ev.start, ev.stop, 0, (T*)shard, rows, cols, ngroups, bt, nb, stride,
+                                  K, slot, rowflag, ctrl, tail_cut, rm);
+        else
+            hipLaunchKernelGGL((k_reduce_rows<T, MODE, CPW, RPW, NT, FULL>), dim3((unsigned)nblocks), dim3(256),
+                               occ_lds, st, (T*)shard, rows, cols, ngroups, bt, nb, stride, K, slot, rowflag, ctrl,
+                               tail_cut, rm);
+    } else {
+        if (ev.start || ev.stop)
+            hipExtLaunchKernelGGL((k_reduce<T, MODE, G, NT, WPB, SNT, CPW>), dim3((unsigned)nblocks), dim3(64 * WPB),
+                                  occ_lds, st, ev.start, ev.stop, 0, (T*)shard, rows, cols, ngroups, bt, nb, stride,
+                                  K, slot, rowflag, ctrl, tail_cut, ada, rm);
+        else
+            hipLaunchKernelGGL((k_reduce<T, MODE, G, NT, WPB, SNT, CPW>), dim3((unsigned)nblocks), dim3(64 * WPB),
+                               occ_lds, st, (T*)shard, rows, cols, ngroups, bt, nb, stride, K, slot, rowflag, ctrl,
+                               tail_cut, ada, rm);
+    }
     return hipGetLastError();
 }
 
 // Tuning variants of the f32 plain reduce (env DML_REDUCE_VARIANT, read per launch;
 // 0 = auto = the shape rule below). Kept for A/B runs (scripts/tune.py):
-// 1: G8/CPW1 nt, 3: G16/CPW1 nt, 9: G8/CPW2, 10: G4/CPW4, 11: G8/CPW4, 12: G4/CPW4 2-wave blocks,
-// 13: G4/CPW4 plain loads, 14: G2/CPW4, 15: G4/CPW4 8-wave blocks.
+// G = pushes per load group, CPW = chunks per wave, RPW = rows per wave.
+// 10: G4/CPW4/RPW1 (the previous rule, k_reduce), 13: same with plain loads, 14: G2/CPW4/RPW1,
+// 20: CPW4/RPW4 (k_reduce_rows), 21: CPW4/RPW2, 24: CPW4/RPW4 plain loads, 27: CPW2/RPW4,
+// 28: CPW4/RPW2 FULL (0 = auto: CPW4/RPW4 FULL for config 2).
 int reduce_variant() {
     const char* v = getenv("DML_REDUCE_VARIANT");
     return v ? atoi(v) : 0;
 }
 
-// Shape rule (measured, scripts/tune.py): one wave walks up to 4 neighbouring
-// 1-KiB chunks of a row (CPW) with G pushes x CPW 16-B nt loads in flight.
+// Shape rule (measured, scripts/ubench_reduce.hip + scripts/tune.py): a wave
+// owns RPW = 4 neighbouring rows and walks up to CPW = 4 neighbouring 1-KiB
+// chunks of each, with G pushes x RPW x CPW 16-B nt loads (16) in flight.
+// AdaGrad and the int32 rollback keep one row and one chunk per wave (their
+// per-element state triples the registers).
 template <typename T, int MODE>
 static hipError_t launch_auto(void* shard, int64_t rows, int32_t cols, const Batch& bt, int nb, int64_t stride, int K,
                               const int32_t* slot, const uint32_t* rowflag, Ctrl* ctrl, uint64_t tail_cut,
                               const AdaArgs& ada, hipStream_t st, int64_t* nblocks_out, LaunchEv ev, RowMap rm) {
     constexpr int VEC = Elem<T>::VEC;
     const int32_t nchunks = (cols + 64 * VEC - 1) / (64 * VEC);
-#define DML_L(G, CPW) launch_reduce_t<T, MODE, G, true, 4, false, CPW>(shard, rows, cols, bt, nb, stride, K, slot, \
-                                                                     rowflag, ctrl, tail_cut, ada, st, nblocks_out, ev, rm)
-    if (MODE == kAdaGrad || MODE == kRollbackI32) return DML_L(8, 1);
-    if (nchunks >= 4) return DML_L(4, 4);
-    if (nchunks >= 2) return DML_L(8, 2);
-    return DML_L(16, 1);
+#define DML_L(G, CPW, RPW) launch_reduce_t<T, MODE, G, true, 4, false, CPW, RPW>(shard, rows, cols, bt, nb, stride, K, \
+                                                     slot, rowflag, ctrl, tail_cut, ada, st, nblocks_out, ev, rm)
+#define DML_LF(G, CPW, RPW) launch_reduce_t<T, MODE, G, true, 4, false, CPW, RPW, true>(shard, rows, cols, bt, nb, \
+                                                     stride, K, slot, rowflag, ctrl, tail_cut, ada, st, nblocks_out, ev, rm)
+    if constexpr (MODE == kAdaGrad || MODE == kRollbackI32) {
+        return DML_L(8, 1, 1);
+    } else {
+        if (cols < VEC) return DML_L(16, 1, 1);  // narrower than one vector: k_reduce's generic path
+        if (cols % (64 * VEC * 4) == 0) return DML_LF(1, 4, 4);
+        if (nchunks >= 4) return DML_L(1, 4, 4);
+        if (cols % (64 * VEC * 2) == 0) return DML_LF(1, 2, 4);
+        if (nchunks >= 2) return DML_L(1, 2, 4);
+        if (cols % (64 * VEC) == 0) return DML_LF(1, 1, 4);
+        return DML_L(1, 1, 4);
+    }
 #undef DML_L
+#undef DML_LF
 }
 
 int64_t reduce_blocks(int vtype, int64_t rows, int32_t cols) {
-    // AdaGrad (the only caller that needs it) always runs one chunk per wave, 4 waves per block
+    // AdaGrad (the only caller that needs it) always runs one row and one chunk per wave, 4 waves per block
     const int VEC = vtype == kF64 ? 2 : 4;
     const int64_t nchunks = (cols + 64 * VEC - 1) / (64 * VEC);
     return (rows * nchunks + 3) / 4;
@@ -458,20 +702,18 @@ hipError_t launch_reduce(int vtype, int mode, void* shard, int64_t rows, int32_t
                          uint64_t tail_cut, const AdaArgs& ada, hipStream_t st, int64_t* nblocks_out, LaunchEv ev,
                          RowMap rm) {
 #define DML_A(T, M) launch_auto<T, M>(shard, rows, cols, bt, nb, stride, K, slot, rowflag, ctrl, tail_cut, ada, st, nblocks_out, ev, rm)
-#define DML_V(G, NT, WPB, SNT, CPW) launch_reduce_t<float, kAdd, G, NT, WPB, SNT, CPW>(shard, rows, cols, bt, nb, stride, K, slot, rowflag, ctrl, tail_cut, ada, st, nblocks_out, ev)
+#define DML_V(G, NT, WPB, SNT, CPW, RPW) launch_reduce_t<float, kAdd, G, NT, WPB, SNT, CPW, RPW, false>(shard, rows, cols, bt, nb, stride, K, slot, rowflag, ctrl, tail_cut, ada, st, nblocks_out, ev)
     if (vtype == kF32) {
         if (mode == kAdd) {
             switch (reduce_variant()) {
-                case 1: return DML_V(8, true, 4, false, 1);
-                case 3: return DML_V(16, true, 4, false, 1);
-                case 9: return DML_V(8, true, 4, false, 2);
-                case 10: return DML_V(4, true, 4, false, 4);
-                case 11: return DML_V(8, true, 4, false, 4);
-                case 12: return DML_V(4, true, 2, false, 4);
-                case 13: return DML_V(4, false, 4, false, 4);
-                case 14: return DML_V(2, true, 4, false, 4);
-                case 15: return DML_V(4, true, 8, false, 4);
-                case 16: return DML_V(4, true, 4, true, 4);
+                case 10: return DML_V(4, true, 4, false, 4, 1);
+                case 13: return DML_V(4, false, 4, false, 4, 1);
+                case 14: return DML_V(2, true, 4, false, 4, 1);
+                case 20: return DML_V(1, true, 4, false, 4, 4);
+                case 21: return DML_V(1, true, 4, false, 4, 2);
+                case 24: return DML_V(1, false, 4, false, 4, 4);
+                case 27: return DML_V(1, true, 4, false, 2, 4);
+                case 28: return launch_reduce_t<float, kAdd, 1, true, 4, false, 4, 2, true>(shard, rows, cols, bt, nb, stride, K, slot, rowflag, ctrl, tail_cut, ada, st, nblocks_out, ev);
                 default: return DML_A(float, kAdd);
             }
         }
