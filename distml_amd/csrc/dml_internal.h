@@ -162,6 +162,9 @@ hipError_t launch_synth_fill(int vtype, void* p, int64_t n, uint64_t s0, hipStre
 hipError_t launch_key_rows(const uint8_t* base, int64_t nrec, int64_t stride, int K, int64_t first, int64_t rows,
                            int32_t* out, hipStream_t st);
 int64_t reduce_blocks(int vtype, int64_t rows, int32_t cols);
+// True when launch_reduce(vtype, mode, cols) runs k_reduce_rows in a plain-sum mode,
+// which rewrites every slot it reads to -1 (the next batch's index then needs no memset).
+bool reduce_clears_slots(int vtype, int mode, int32_t cols);
 
 uint64_t splitmix64(uint64_t x);
 

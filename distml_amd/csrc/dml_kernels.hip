@@ -88,6 +88,43 @@ __global__ __launch_bounds__(256) void k_index(const Batch bt, int64_t stride, i
     }
 }
 
+// k_index_multi: as k_index<false>, RPT records per thread (records
+// blockIdx.x*256*RPT + j*256 + tid): all RPT key loads, then all RPT
+// returning atomics, in flight together — fewer, shorter-lived waves beside
+// the previous chunk's reduce.
+template <int RPT>
+__global__ __launch_bounds__(256) void k_index_multi(const Batch bt, int64_t stride, int K, int64_t first,
+                                                     int64_t rows, int32_t* __restrict__ slot,
+                                                     uint32_t* __restrict__ rowflag, Ctrl* __restrict__ ctrl,
+                                                     uint64_t tail_cut) {
+    const int b = blockIdx.y;
+    const int64_t r0 = (int64_t)blockIdx.x * 256 * RPT + threadIdx.x;
+    if (r0 == 0 && b == 0 && tail_cut != kNoPos) atomicMin(&ctrl->cutoff, (unsigned long long)tail_cut);
+    const int64_t nrec = bt.nrec[b];
+    const uint8_t* base = bt.base[b];
+    int64_t idx[RPT];
+#pragma unroll
+    for (int j = 0; j < RPT; ++j) {
+        const int64_t r = r0 + j * 256;
+        idx[j] = r < nrec ? row_index(ld_key(base + r * stride, K), first, rows) : -2;
+    }
+    int32_t old[RPT];
+#pragma unroll
+    for (int j = 0; j < RPT; ++j) {
+        old[j] = -1;
+        if (idx[j] >= 0) old[j] = atomicExch(&slot[idx[j] * kMaxW + b], (int32_t)(r0 + j * 256));
+    }
+#pragma unroll
+    for (int j = 0; j < RPT; ++j) {
+        if (idx[j] == -1)
+            atomicMin(&ctrl->cutoff, (unsigned long long)pos_of((uint64_t)bt.bidx[b], (uint64_t)((r0 + j * 256) * stride)));
+        if (old[j] != -1) {
+            rowflag[idx[j]] = 1u;
+            ctrl->no_dup = 0u;  // benign race: every writer stores the same value
+        }
+    }
+}
+
 // k_verify (after k_index<true>): a record whose slot holds another record lost
 // a race with a record of the same row and push -> flag the row.
 __global__ __launch_bounds__(256) void k_verify(const Batch bt, int64_t stride, int K, int64_t first, int64_t rows,
@@ -113,7 +150,19 @@ hipError_t launch_index(const Batch& bt, int nb, int64_t max_nrec, int64_t strid
                         int64_t rows, int32_t* slot, uint32_t* rowflag, Ctrl* ctrl, uint64_t tail_cut, hipStream_t st) {
     if (nb <= 0) return hipSuccess;
     dim3 grid((unsigned)std::max<int64_t>(1, (max_nrec + 255) / 256), (unsigned)nb);
-    if (index_variant() == 0) {
+    const int iv = index_variant();
+    if (iv == 2 || iv == 3) {
+        const int rpt = iv == 2 ? 8 : 4;
+        dim3 g((unsigned)std::max<int64_t>(1, (max_nrec + 256 * rpt - 1) / (256 * rpt)), (unsigned)nb);
+        if (rpt == 8)
+            hipLaunchKernelGGL(k_index_multi<8>, g, dim3(256), 0, st, bt, stride, K, first, rows, slot, rowflag, ctrl,
+                               tail_cut);
+        else
+            hipLaunchKernelGGL(k_index_multi<4>, g, dim3(256), 0, st, bt, stride, K, first, rows, slot, rowflag, ctrl,
+                               tail_cut);
+        return hipGetLastError();
+    }
+    if (iv == 0) {
         hipLaunchKernelGGL(k_index<false>, grid, dim3(256), 0, st, bt, stride, K, first, rows, slot, rowflag, ctrl,
                            tail_cut);
         return hipGetLastError();
@@ -409,10 +458,10 @@ __global__ __launch_bounds__(64 * WPB) void k_reduce(T* __restrict__ shard, int6
 // so the hot loop carries no cutoff logic. Same results as k_reduce bit for bit
 // (same per-element add order, cutoff and negativity rules); rows narrower than
 // one vector use k_reduce.
-template <typename T, int MODE, int CPW, int RPW, bool NT, bool FULL>
+template <typename T, int MODE, int CPW, int RPW, bool NT, bool FULL, int DEPTH>
 __global__ __launch_bounds__(256) void k_reduce_rows(T* __restrict__ shard, int64_t rows, int32_t cols,
                                                      int32_t ngroups, const Batch bt, int nb, int64_t stride, int K,
-                                                     const int32_t* __restrict__ slot,
+                                                     int32_t* __restrict__ slot,
                                                      const uint32_t* __restrict__ rowflag, Ctrl* __restrict__ ctrl,
                                                      uint64_t tail_cut, RowMap rm) {
     constexpr int VEC = Elem<T>::VEC;
@@ -529,7 +578,75 @@ __global__ __launch_bounds__(256) void k_reduce_rows(T* __restrict__ shard, int6
     int32_t vslot[RPW];
 #pragma unroll
     for (int r = 0; r < RPW; ++r) vslot[r] = (live >> r & 1u) ? slot[row[r] * kMaxW + lane] : -1;
+    if constexpr (MODE != kAddCheckI32) {
+        // Hand the slot rows back as the next batch's index expects them (-1 = no
+        // record), so the host skips the slot-table memset (reduce_clears_slots). The
+        // int32-check mode keeps them: its rollback re-reads the table.
+#pragma unroll
+        for (int r = 0; r < RPW; ++r)
+            if ((live >> r & 1u) && lane < nb) slot[row[r] * kMaxW + lane] = -1;
+    }
     const uint64_t vbase = lane < nb ? (uint64_t)bt.base[lane] : 0ull;
+    if constexpr (DEPTH == 2) {
+        static_assert(FULL, "two-deep ring: whole-vector rows only");
+        // Two pushes' loads in flight (a ring of two register sets): push b+2's loads
+        // are issued as soon as push b is added, so the wave never drains its loads.
+        // Absent rows and pushes past the batch load a live row (an L2 hit) and add nothing.
+        auto issue = [&](int b, u32x4 (&raw)[RPW][CPW], unsigned& h, int32_t (&rrb)[RPW]) {
+            const int bb = b < nb ? b : (nb > 0 ? nb - 1 : 0);
+            const uint8_t* bp =
+                (const uint8_t*)(((uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)vbase, bb)) |
+                                 ((uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)(vbase >> 32), bb) << 32));
+            h = 0;
+#pragma unroll
+            for (int r = 0; r < RPW; ++r) {
+                rrb[r] = b < nb ? __builtin_amdgcn_readlane(vslot[r], bb) : -1;
+                h |= (rrb[r] >= 0 ? 1u : 0u) << r;
+                const uint8_t* rb = rrb[r] >= 0 ? bp + (int64_t)rrb[r] * stride + voff[0] : fbv;
+#pragma unroll
+                for (int c = 0; c < CPW; ++c) {
+                    const uint8_t* src = rb + c * 64 * VEC * (int)sizeof(T);
+                    raw[r][c] = NT ? ldg16_nt(src) : ldg16(src);
+                }
+            }
+        };
+        auto consume = [&](const u32x4 (&raw)[RPW][CPW], unsigned h, const int32_t (&rrb)[RPW], int b) {
+            touched |= h;
+#pragma unroll
+            for (int r = 0; r < RPW; ++r) {
+                const bool on = (h >> r) & 1u;
+#pragma unroll
+                for (int c = 0; c < CPW; ++c) {
+                    T t[VEC];
+                    unpack<T>(raw[r][c], t);
+#pragma unroll
+                    for (int e = 0; e < VEC; ++e) {
+                        const T sum = Elem<T>::add(acc[r][c][e], t[e]);
+                        if constexpr (MODE == kAddCheckI32) {
+                            if (on && sum < 0) {
+                                const uint64_t p = pos_of((uint64_t)bt.bidx[b < nb ? b : 0],
+                                                          (uint64_t)((int64_t)rrb[r] * stride + voff[c] + e * (int64_t)sizeof(T)));
+                                negpos = p < negpos ? p : negpos;
+                            }
+                        }
+                        acc[r][c][e] = on ? sum : acc[r][c][e];  // a select: an absent row keeps its bits (-0.0)
+                    }
+                }
+            }
+        };
+        u32x4 ra[RPW][CPW], rb2[RPW][CPW];
+        unsigned ha, hb;
+        int32_t rra[RPW], rrb2[RPW];
+        issue(0, ra, ha, rra);
+        issue(1, rb2, hb, rrb2);
+#pragma unroll 1
+        for (int b = 0; b < nb; b += 2) {
+            consume(ra, ha, rra, b);
+            issue(b + 2, ra, ha, rra);
+            consume(rb2, hb, rrb2, b + 1);
+            issue(b + 3, rb2, hb, rrb2);
+        }
+    } else
 #pragma unroll 1
     for (int b = 0; b < nb; ++b) {
         int32_t rr[RPW];
@@ -629,13 +746,13 @@ static hipError_t launch_reduce_t(void* shard, int64_t rows, int32_t cols, const
     if constexpr (RPW > 1) {
         static_assert(WPB == 4 && MODE != kAdaGrad && MODE != kRollbackI32, "k_reduce_rows shapes");
         if (ev.start || ev.stop)
-            hipExtLaunchKernelGGL((k_reduce_rows<T, MODE, CPW, RPW, NT, FULL>), dim3((unsigned)nblocks), dim3(256),
+            hipExtLaunchKernelGGL((k_reduce_rows<T, MODE, CPW, RPW, NT, FULL, (FULL && G == 2) ? 2 : 1>), dim3((unsigned)nblocks), dim3(256),
                                   occ_lds, st, ev.start, ev.stop, 0, (T*)shard, rows, cols, ngroups, bt, nb, stride,
-                                  K, slot, rowflag, ctrl, tail_cut, rm);
+                                  K, const_cast<int32_t*>(slot), rowflag, ctrl, tail_cut, rm);
         else
-            hipLaunchKernelGGL((k_reduce_rows<T, MODE, CPW, RPW, NT, FULL>), dim3((unsigned)nblocks), dim3(256),
-                               occ_lds, st, (T*)shard, rows, cols, ngroups, bt, nb, stride, K, slot, rowflag, ctrl,
-                               tail_cut, rm);
+            hipLaunchKernelGGL((k_reduce_rows<T, MODE, CPW, RPW, NT, FULL, (FULL && G == 2) ? 2 : 1>), dim3((unsigned)nblocks), dim3(256),
+                               occ_lds, st, (T*)shard, rows, cols, ngroups, bt, nb, stride, K, const_cast<int32_t*>(slot), rowflag,
+                               ctrl, tail_cut, rm);
     } else {
         if (ev.start || ev.stop)
             hipExtLaunchKernelGGL((k_reduce<T, MODE, G, NT, WPB, SNT, CPW>), dim3((unsigned)nblocks), dim3(64 * WPB),
@@ -654,7 +771,8 @@ static hipError_t launch_reduce_t(void* shard, int64_t rows, int32_t cols, const
 // G = pushes per load group, CPW = chunks per wave, RPW = rows per wave.
 // 10: G4/CPW4/RPW1 (the previous rule, k_reduce), 13: same with plain loads, 14: G2/CPW4/RPW1,
 // 20: CPW4/RPW4 (k_reduce_rows), 21: CPW4/RPW2, 24: CPW4/RPW4 plain loads, 27: CPW2/RPW4,
-// 28: CPW4/RPW2 FULL (0 = auto: CPW4/RPW4 FULL for config 2).
+// 28: CPW4/RPW2 FULL, 30: CPW4/RPW4 FULL two-deep ring, 31: CPW4/RPW2 FULL two-deep ring
+// (0 = auto: CPW4/RPW4 FULL for config 2).
 int reduce_variant() {
     const char* v = getenv("DML_REDUCE_VARIANT");
     return v ? atoi(v) : 0;
@@ -690,6 +808,17 @@ static hipError_t launch_auto(void* shard, int64_t rows, int32_t cols, const Bat
 #undef DML_LF
 }
 
+bool reduce_clears_slots(int vtype, int mode, int32_t cols) {
+    if (mode != kAdd && mode != kPreReduce) return false;
+    const int VEC = vtype == kF64 ? 2 : 4;
+    if (cols < VEC) return false;  // k_reduce's generic path
+    if (vtype == kF32 && mode == kAdd) {
+        const int v = reduce_variant();
+        if (v == 10 || v == 13 || v == 14) return false;  // the one-row k_reduce variants
+    }
+    return true;
+}
+
 int64_t reduce_blocks(int vtype, int64_t rows, int32_t cols) {
     // AdaGrad (the only caller that needs it) always runs one row and one chunk per wave, 4 waves per block
     const int VEC = vtype == kF64 ? 2 : 4;
@@ -713,6 +842,8 @@ hipError_t launch_reduce(int vtype, int mode, void* shard, int64_t rows, int32_t
                 case 21: return DML_V(1, true, 4, false, 4, 2);
                 case 24: return DML_V(1, false, 4, false, 4, 4);
                 case 27: return DML_V(1, true, 4, false, 2, 4);
+                case 30: return launch_reduce_t<float, kAdd, 2, true, 4, false, 4, 4, true>(shard, rows, cols, bt, nb, stride, K, slot, rowflag, ctrl, tail_cut, ada, st, nblocks_out, ev);
+                case 31: return launch_reduce_t<float, kAdd, 2, true, 4, false, 4, 2, true>(shard, rows, cols, bt, nb, stride, K, slot, rowflag, ctrl, tail_cut, ada, st, nblocks_out, ev);
                 case 28: return launch_reduce_t<float, kAdd, 1, true, 4, false, 4, 2, true>(shard, rows, cols, bt, nb, stride, K, slot, rowflag, ctrl, tail_cut, ada, st, nblocks_out, ev);
                 default: return DML_A(float, kAdd);
             }

@@ -87,6 +87,8 @@ struct Workspace {
     hipEvent_t done = nullptr;        // copy stream: ctrl copied out (chunk retired-able)
     uint8_t* sp = nullptr;            // sparse partition buffers (SpLayout), grown on demand
     size_t sp_cap = 0;
+    bool clears = false;              // the chunk's reduce leaves its slot table all -1
+    bool clean = false;               // slot table all -1 and rowflags 0: only the Ctrl needs a reset
 };
 
 struct Pending {
@@ -329,6 +331,7 @@ int launch_apply(dml_store* s, Chunk& c, Workspace& W, const Ctrl* prev) {
         LaunchEv ev = inpacket ? LaunchEv{W.kstart, W.applied} : LaunchEv{};
         if (s->timing && !inpacket) HIPCHK(hipEventRecord(W.kstart, s->stream));
         int64_t nblk = 0;
+        W.clears = reduce_clears_slots(vtype_of(s->desc), reduce_mode(s), s->cols);
         HIPCHK(launch_reduce(vtype_of(s->desc), reduce_mode(s), s->data, s->rows, s->cols, c.bt, c.nb, s->stride,
                              s->K, W.slot, W.rowflag, W.ctrl, c.tail_cut, ada_args(s), s->stream, &nblk, ev));
         if (s->adagrad)
@@ -373,9 +376,15 @@ int launch_chunk(dml_store* s, Chunk& c, Workspace& W, const Ctrl* prev) {
         HIPCHK(hipEventRecord(W.idx_done, s->istream));
         HIPCHK(hipStreamWaitEvent(s->stream, W.idx_done, 0));
     }
-    HIPCHK(hipMemsetAsync(W.base, 0xFF, sizeof(Ctrl) + s->slot_bytes, is));
+    // A workspace whose last chunk retired normally through a slot-clearing reduce
+    // (k_reduce_rows, plain-sum modes) already holds an all -1 slot table and zero
+    // rowflags: only its Ctrl is reset (the 4 MiB-class memsets otherwise compete
+    // with the running reduce).
+    const bool clean = W.clean;
+    W.clean = false;
+    HIPCHK(hipMemsetAsync(W.base, 0xFF, sizeof(Ctrl) + (clean ? 0 : s->slot_bytes), is));
     if (s->is_matrix) {
-        HIPCHK(hipMemsetAsync(W.rowflag, 0, (size_t)s->rows * sizeof(uint32_t), is));
+        if (!clean) HIPCHK(hipMemsetAsync(W.rowflag, 0, (size_t)s->rows * sizeof(uint32_t), is));
         HIPCHK(launch_index(c.bt, c.nb, c.max_nrec, s->stride, s->K, s->first, s->rows, W.slot, W.rowflag, W.ctrl,
                             c.tail_cut, is));
     } else {
@@ -555,6 +564,7 @@ int retire_front(dml_store* s) {
     Ctrl ctl = *W.hctrl;
     if (s->timing) ev_collect(s);
     const bool abnormal = ctrl_abnormal(&ctl);
+    W.clean = s->is_matrix && !abnormal && W.clears;
     int rc = DML_OK;
     if (s->is_matrix && ctl.no_dup == 0u) {
         rc = replay_rows(s, c, W, &ctl);
@@ -733,7 +743,14 @@ int dml_store_create_range(const dml_desc* desc, int64_t first_key, int64_t last
         return set_err(DML_E_HIP, std::string(what) + ": " + hipGetErrorString(e));
     };
     hipError_t e;
-    if ((e = hipStreamCreateWithFlags(&s->stream, hipStreamNonBlocking)) != hipSuccess) return fail(e, "stream");
+    // DML_STREAM_PRIO=1: apply stream at high priority, index stream at low priority
+    // (the next chunk's index then fills the wave slots the reduce leaves free).
+    static const int prio_mode = getenv("DML_STREAM_PRIO") ? atoi(getenv("DML_STREAM_PRIO")) : 0;
+    int prio_least = 0, prio_greatest = 0;
+    if (prio_mode) (void)hipDeviceGetStreamPriorityRange(&prio_least, &prio_greatest);
+    if ((e = prio_mode ? hipStreamCreateWithPriority(&s->stream, hipStreamNonBlocking, prio_greatest)
+                       : hipStreamCreateWithFlags(&s->stream, hipStreamNonBlocking)) != hipSuccess)
+        return fail(e, "stream");
     const size_t nbytes = (size_t)rows * (size_t)s->cols * (size_t)s->V;
     if ((e = hipMalloc(&s->data, nbytes)) != hipSuccess) return fail(e, "shard alloc");
     if ((e = hipMemsetAsync(s->data, 0, nbytes, s->stream)) != hipSuccess) return fail(e, "shard zero");
@@ -751,7 +768,9 @@ int dml_store_create_range(const dml_desc* desc, int64_t first_key, int64_t last
     }
     s->slot_bytes = s->is_matrix ? (size_t)rows * kMaxW * sizeof(int32_t) : 0;
     s->ws_bytes = sizeof(Ctrl) + s->slot_bytes + (s->is_matrix ? (size_t)rows * sizeof(uint32_t) : 0);
-    if ((e = hipStreamCreateWithFlags(&s->istream, hipStreamNonBlocking)) != hipSuccess) return fail(e, "index stream");
+    if ((e = prio_mode ? hipStreamCreateWithPriority(&s->istream, hipStreamNonBlocking, prio_least)
+                       : hipStreamCreateWithFlags(&s->istream, hipStreamNonBlocking)) != hipSuccess)
+        return fail(e, "index stream");
     if ((e = hipStreamCreateWithFlags(&s->cstream, hipStreamNonBlocking)) != hipSuccess) return fail(e, "copy stream");
     for (Workspace& W : s->ws) {
         if ((e = hipMalloc((void**)&W.base, s->ws_bytes)) != hipSuccess) return fail(e, "workspace alloc");
@@ -1209,6 +1228,7 @@ int dml_store_apply_dense_device(dml_store* s, const void* dev_src, int64_t elem
 struct WsLease {
     uint8_t* ptr = nullptr;
     size_t bytes = 0;
+    bool clean = false;  // slot table all -1 and rowflags 0 (left so by a clearing pre-reduce)
 };
 static std::mutex g_ws_mu;
 static std::unordered_map<int, std::vector<WsLease>> g_ws_free;
@@ -1291,6 +1311,7 @@ int dml_reduce_buckets_dense(const dml_desc* desc, int64_t first_key, int64_t ro
         else if (h.no_dup == 0u) rc = set_err(DML_E_UNSUPPORTED, "pre-reduce: a bucket repeats a row");
         if (n == 0) break;
     }
+    lease.clean = false;  // this path memsets per chunk and does not track cleanliness
     ws_release(dev, lease);
     return rc;
 }
@@ -1313,6 +1334,7 @@ struct dml_prereduce {
     uint32_t* rowflag = nullptr;
     hipStream_t stream = nullptr;
     int device = 0;
+    int64_t rows_done = 0;  // model rows the pieces reduced (all of them: the slot table is clean again)
 };
 
 extern "C" {
@@ -1357,11 +1379,13 @@ int dml_prereduce_begin(const dml_desc* desc, int64_t first_key, int64_t rows, i
     }
     p->ws = lease.ptr;
     p->ws_bytes = lease.bytes;
+    const bool clean = lease.clean;
     p->ctrl = (Ctrl*)p->ws;
     p->slot = (int32_t*)(p->ws + sizeof(Ctrl));
     p->rowflag = (uint32_t*)(p->ws + sizeof(Ctrl) + sb);
-    hipError_t e = hipMemsetAsync(p->ws, 0xFF, sizeof(Ctrl) + sb, p->stream);
-    if (e == hipSuccess) e = hipMemsetAsync(p->rowflag, 0, (size_t)rows * sizeof(uint32_t), p->stream);
+    // a clean lease needs only its Ctrl reset (see launch_chunk)
+    hipError_t e = hipMemsetAsync(p->ws, 0xFF, sizeof(Ctrl) + (clean ? 0 : sb), p->stream);
+    if (e == hipSuccess && !clean) e = hipMemsetAsync(p->rowflag, 0, (size_t)rows * sizeof(uint32_t), p->stream);
     if (e == hipSuccess)
         e = launch_index(p->bt, n, max_nrec, p->stride, p->K, first_key, rows, p->slot, p->rowflag, p->ctrl, kNoPos,
                          p->stream);
@@ -1390,6 +1414,12 @@ int dml_prereduce_piece(dml_prereduce* p, int64_t row_block, int64_t row_stride,
     AdaArgs none{};
     HIPCHK(launch_reduce(p->desc.value_type, kPreReduce, dev_out, ntask_rows, p->cols, p->bt, p->nb, p->stride, p->K,
                          p->slot, nullptr, p->ctrl, kNoPos, none, st, nullptr, LaunchEv{}, rm));
+    // model rows this piece covered: blocks of row_block task rows at row_off + q*row_stride
+    for (int64_t t0 = 0; t0 < ntask_rows; t0 += row_block) {
+        const int64_t lo = (t0 / row_block) * row_stride + row_off;
+        const int64_t hi = std::min(lo + std::min(row_block, ntask_rows - t0), p->rows);
+        if (hi > lo) p->rows_done += hi - lo;
+    }
     return DML_OK;
 }
 
@@ -1402,8 +1432,11 @@ int dml_prereduce_end(dml_prereduce* p) {
     if (e != hipSuccess) rc = set_err(DML_E_HIP, hipGetErrorString(e));
     else if (h.cutoff != kNoPos) rc = set_err(DML_E_KEY_OUT_OF_SHARD, "pre-reduce: key outside the matrix");
     else if (h.no_dup == 0u) rc = set_err(DML_E_UNSUPPORTED, "pre-reduce: a push repeats a row");
-    // after a failed sync the device state is unknown: drop the lease
-    if (e == hipSuccess) ws_release(p->device, WsLease{p->ws, p->ws_bytes});
+    // after a failed sync the device state is unknown: drop the lease. A normal chunk
+    // whose pieces reduced every row through the clearing kernel left the table clean.
+    const bool clean = rc == DML_OK && p->rows_done == p->rows &&
+                       reduce_clears_slots(p->desc.value_type, kPreReduce, p->cols);
+    if (e == hipSuccess) ws_release(p->device, WsLease{p->ws, p->ws_bytes, clean});
     delete p;
     return rc;
 }
