@@ -30,6 +30,11 @@ import time
 
 ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
+# One hardware queue per stream: the store (apply / index / copy), torch's default
+# stream and the group path's index / comm streams each need their own queue, or
+# HIP multiplexes them onto HIP's default 4 and work meant to overlap serializes
+# (measured on the --group path: the next call's key index queued behind the pieces).
+os.environ.setdefault("GPU_MAX_HW_QUEUES", "8")
 
 ROWS, COLS, W = 16384, 1024, 32
 REC = 4 + 4 * COLS
@@ -160,6 +165,7 @@ def main():
     ap.add_argument("--no-cpu", action="store_true", help="skip the CPU baseline leg")
     ap.add_argument("--no-timing", action="store_true", help="no kernel timing events in the timed region")
     ap.add_argument("--sparse-steps", type=int, default=5, help="config-3 sparse leg steps (0 = skip)")
+    ap.add_argument("--pieces", type=int, default=4, help="pre-reduce row slices per call (sharded path)")
     ap.add_argument("--group", action="store_true",
                     help="use the sharded pre-reduce/reduce-scatter path even at N=1 (path check)")
     args = ap.parse_args()
@@ -205,7 +211,7 @@ def main():
         timed_store = store
         algo_per_rank = W * BUCKET + 2 * SHARD
     else:
-        group = ShardGroup(fmt, ROWS, COLS, rank, world, device=local)
+        group = ShardGroup(fmt, ROWS, COLS, rank, world, device=local, pieces=args.pieces)
         bufs = make_buckets(L, torch, fmt, W, ROWS)
         ptrs, lens = [b.data_ptr() for b in bufs], [b.numel() for b in bufs]
         st = torch.cuda.current_stream().cuda_stream

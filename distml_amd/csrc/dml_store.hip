@@ -1228,7 +1228,8 @@ int dml_store_apply_dense_device(dml_store* s, const void* dev_src, int64_t elem
 struct WsLease {
     uint8_t* ptr = nullptr;
     size_t bytes = 0;
-    bool clean = false;  // slot table all -1 and rowflags 0 (left so by a clearing pre-reduce)
+    bool clean = false;     // slot table all -1 and rowflags 0 (left so by a clearing pre-reduce)
+    Ctrl* hctrl = nullptr;  // pinned host copy of the Ctrl (read without touching a stream)
 };
 static std::mutex g_ws_mu;
 static std::unordered_map<int, std::vector<WsLease>> g_ws_free;
@@ -1246,7 +1247,11 @@ static int ws_acquire(int dev, size_t bytes, WsLease* out) {
     }
     WsLease l;
     hipError_t e = hipMalloc((void**)&l.ptr, bytes);
-    if (e != hipSuccess) return set_err(DML_E_HIP, hipGetErrorString(e));
+    if (e == hipSuccess) e = hipHostMalloc((void**)&l.hctrl, sizeof(Ctrl), hipHostMallocDefault);
+    if (e != hipSuccess) {
+        if (l.ptr) (void)hipFree(l.ptr);
+        return set_err(DML_E_HIP, hipGetErrorString(e));
+    }
     l.bytes = bytes;
     *out = l;
     return DML_OK;
@@ -1335,7 +1340,18 @@ struct dml_prereduce {
     hipStream_t stream = nullptr;
     int device = 0;
     int64_t rows_done = 0;  // model rows the pieces reduced (all of them: the slot table is clean again)
+    Ctrl* hctrl = nullptr;  // the lease's pinned Ctrl copy, DMA'd right behind the index
+    hipEvent_t idx_ev = nullptr;   // begin stream: key index built
+    hipEvent_t last_ev = nullptr;  // piece stream: last piece enqueued so far
+    hipStream_t last_st = nullptr;
+    bool idx_waited = false;
 };
+
+static void prereduce_free(dml_prereduce* p) {
+    if (p->idx_ev) (void)hipEventDestroy(p->idx_ev);
+    if (p->last_ev) (void)hipEventDestroy(p->last_ev);
+    delete p;
+}
 
 extern "C" {
 
@@ -1379,6 +1395,7 @@ int dml_prereduce_begin(const dml_desc* desc, int64_t first_key, int64_t rows, i
     }
     p->ws = lease.ptr;
     p->ws_bytes = lease.bytes;
+    p->hctrl = lease.hctrl;
     const bool clean = lease.clean;
     p->ctrl = (Ctrl*)p->ws;
     p->slot = (int32_t*)(p->ws + sizeof(Ctrl));
@@ -1389,11 +1406,16 @@ int dml_prereduce_begin(const dml_desc* desc, int64_t first_key, int64_t rows, i
     if (e == hipSuccess)
         e = launch_index(p->bt, n, max_nrec, p->stride, p->K, first_key, rows, p->slot, p->rowflag, p->ctrl, kNoPos,
                          p->stream);
+    // the index alone writes the Ctrl: copy it out now, so _end reads it without
+    // queueing anything behind the caller's later work
+    if (e == hipSuccess) e = hipMemcpyAsync(p->hctrl, p->ctrl, sizeof(Ctrl), hipMemcpyDeviceToHost, p->stream);
+    if (e == hipSuccess) e = hipEventCreateWithFlags(&p->idx_ev, hipEventDisableTiming);
+    if (e == hipSuccess) e = hipEventRecord(p->idx_ev, p->stream);
     if (e != hipSuccess) {
         // the stream may still reference the workspace: drain it before reuse
         (void)hipStreamSynchronize(p->stream);
-        ws_release(p->device, WsLease{p->ws, p->ws_bytes});
-        delete p;
+        ws_release(p->device, WsLease{p->ws, p->ws_bytes, false, p->hctrl});
+        prereduce_free(p);
         return set_err(DML_E_HIP, hipGetErrorString(e));
     }
     *out = p;
@@ -1403,8 +1425,14 @@ int dml_prereduce_begin(const dml_desc* desc, int64_t first_key, int64_t rows, i
 int dml_prereduce_piece(dml_prereduce* p, int64_t row_block, int64_t row_stride, int64_t row_off, int64_t ntask_rows,
                         void* dev_out, void* stream) {
     if (!p || !dev_out || row_block <= 0 || ntask_rows < 0) return set_err(DML_E_INVALID_ARG, "bad piece arguments");
-    hipStream_t st = stream ? (hipStream_t)stream : p->stream;
-    if (st != p->stream) return set_err(DML_E_INVALID_ARG, "pieces run on the begin() stream");
+    hipStream_t st = (hipStream_t)stream;  // as given: 0 is HIP's null stream
+    if (st != p->stream && !p->idx_waited) {
+        // pieces on another stream (the index ran on a side stream, overlapping the
+        // caller's previous work): wait for the index on the host, then enqueue the
+        // piece straight behind whatever that stream runs (no cross-queue barrier)
+        HIPCHK(hipEventSynchronize(p->idx_ev));
+        p->idx_waited = true;
+    }
     RowMap rm;
     rm.block = row_block;
     rm.stride = row_stride;
@@ -1412,22 +1440,32 @@ int dml_prereduce_piece(dml_prereduce* p, int64_t row_block, int64_t row_stride,
     rm.rows_total = p->rows;
     rm.out = dev_out;
     AdaArgs none{};
+    if (!p->last_ev) HIPCHK(hipEventCreateWithFlags(&p->last_ev, hipEventDisableTiming));
+    // the piece's completion event rides in its dispatch packet (no marker packet between pieces)
     HIPCHK(launch_reduce(p->desc.value_type, kPreReduce, dev_out, ntask_rows, p->cols, p->bt, p->nb, p->stride, p->K,
-                         p->slot, nullptr, p->ctrl, kNoPos, none, st, nullptr, LaunchEv{}, rm));
+                         p->slot, nullptr, p->ctrl, kNoPos, none, st, nullptr, LaunchEv{nullptr, p->last_ev}, rm));
     // model rows this piece covered: blocks of row_block task rows at row_off + q*row_stride
     for (int64_t t0 = 0; t0 < ntask_rows; t0 += row_block) {
         const int64_t lo = (t0 / row_block) * row_stride + row_off;
         const int64_t hi = std::min(lo + std::min(row_block, ntask_rows - t0), p->rows);
         if (hi > lo) p->rows_done += hi - lo;
     }
+    p->last_st = st;
+    return DML_OK;
+}
+
+int dml_prereduce_stream_wait(dml_prereduce* p, void* stream) {
+    if (!p || !p->last_ev) return set_err(DML_E_INVALID_ARG, "no piece enqueued yet");
+    HIPCHK(hipStreamWaitEvent((hipStream_t)stream, p->last_ev, 0));
     return DML_OK;
 }
 
 int dml_prereduce_end(dml_prereduce* p) {
     if (!p) return set_err(DML_E_INVALID_ARG, "null pre-reduce");
-    Ctrl h{};
-    hipError_t e = hipMemcpyAsync(&h, p->ctrl, sizeof h, hipMemcpyDeviceToHost, p->stream);
-    if (e == hipSuccess) e = hipStreamSynchronize(p->stream);
+    hipError_t e = hipEventSynchronize(p->idx_ev);  // index done, Ctrl copied out
+    const Ctrl h = *p->hctrl;
+    // the workspace is free once the last piece ran
+    if (e == hipSuccess && p->last_ev) e = hipEventSynchronize(p->last_ev);
     int rc = DML_OK;
     if (e != hipSuccess) rc = set_err(DML_E_HIP, hipGetErrorString(e));
     else if (h.cutoff != kNoPos) rc = set_err(DML_E_KEY_OUT_OF_SHARD, "pre-reduce: key outside the matrix");
@@ -1436,8 +1474,8 @@ int dml_prereduce_end(dml_prereduce* p) {
     // whose pieces reduced every row through the clearing kernel left the table clean.
     const bool clean = rc == DML_OK && p->rows_done == p->rows &&
                        reduce_clears_slots(p->desc.value_type, kPreReduce, p->cols);
-    if (e == hipSuccess) ws_release(p->device, WsLease{p->ws, p->ws_bytes, clean});
-    delete p;
+    if (e == hipSuccess) ws_release(p->device, WsLease{p->ws, p->ws_bytes, clean, p->hctrl});
+    prereduce_free(p);
     return rc;
 }
 

@@ -59,6 +59,9 @@ class HipOps:
     def end(self, h) -> None:
         check(_lib.load().dml_prereduce_end(C.c_void_p(h)))
 
+    def stream_wait(self, h, stream: int) -> None:
+        check(_lib.load().dml_prereduce_stream_wait(C.c_void_p(h), C.c_void_p(stream)))
+
 
 class ShardGroup:
     def __init__(self, fmt: DataDesc, total_rows: int, cols: int, rank: int, world: int,
@@ -83,11 +86,25 @@ class ShardGroup:
         dev = torch.device("cuda", device) if device is not None else torch.device("cpu")
         self.partial = torch.empty(world * self.step_rows * cols, dtype=self.dtype, device=dev)
         self.recv = torch.empty(self.step_rows * cols, dtype=self.dtype, device=dev)
-        # pipelining of the full-range path: P row slices, reduce-scattered on a comm stream
+        # pipelining of the full-range path: P row slices, reduce-scattered on a comm stream;
+        # calls alternate between two partial/recv buffer sets so call k+1's key index
+        # (side stream) and pre-reduce overlap call k's reduce-scatter and apply
         self.pieces = pieces
+        self._pending: list = []  # pre-reduce handles whose errors are not yet collected
+        self._k = 0
         if self.partial.is_cuda:
             self.comm = torch.cuda.Stream(device=dev)
-            self._ev = [torch.cuda.Event() for _ in range(pieces)]
+            self.cstream = torch.cuda.Stream(device=dev)  # pre-reduce pieces
+            self._ready = torch.cuda.Event()
+            # high priority: a HIP stream of another priority class gets its own hardware
+            # queue, so the next call's index never queues behind this call's pieces
+            self.istream = torch.cuda.Stream(device=dev, priority=-1)
+            self._partials = [self.partial, torch.empty_like(self.partial)]
+            self._recvs = [self.recv, torch.empty_like(self.recv)]
+            self._rs_done = [torch.cuda.Event(), torch.cuda.Event()]
+            self._applied = [torch.cuda.Event(), torch.cuda.Event()]
+            self._store_stream = (torch.cuda.ExternalStream(self.store.stream(), device=dev)
+                                  if hasattr(self.store, "stream") else None)
 
     def _default_reduce_scatter(self, out, inp) -> None:
         dist = self.dist
@@ -119,29 +136,64 @@ class ShardGroup:
     def _push_pipelined(self, dev_ptrs, lens) -> None:
         """Pre-reduce in `pieces` row slices; slice j holds rows [q*S + j*S/P, q*S + (j+1)*S/P)
         of every rank q, laid out [rank][row], so its reduce-scatter (comm stream) runs
-        while slice j+1 is pre-reduced (compute stream)."""
+        while slice j+1 is pre-reduced (compute stream).
+
+        Asynchronous across calls: the key index runs on a side stream (overlapping
+        the previous call's pre-reduce), the owner apply is queued on the store's
+        stream behind the reduce-scatter, and the call's key / repeated-row errors are
+        raised by the next call or flush() (like DML_FLAG_ASYNC)."""
         torch = self.torch
         S, P, cols, world = self.step_rows, self.pieces, self.cols, self.world
         blk = S // P
-        cur = torch.cuda.current_stream()
-        st = cur.cuda_stream
-        h = self.ops.begin(self.fmt, 0, self.total_rows, cols, dev_ptrs, lens, st)
+        k = self._k
+        self._k ^= 1
+        # pieces run on the group's own stream, after whatever the caller's current
+        # stream has enqueued (the producers of the pushes)
+        self._ready.record(torch.cuda.current_stream())
+        self.cstream.wait_event(self._ready)
+        st = self.cstream.cuda_stream
+        partial, recv = self._partials[k], self._recvs[k]
+        h = self.ops.begin(self.fmt, 0, self.total_rows, cols, dev_ptrs, lens, self.istream.cuda_stream)
+        # buffer set k was last used two calls ago: its apply (queued behind its
+        # reduce-scatter) has finished with recv[k], and so has the scatter with partial[k]
+        self._applied[k].synchronize()
         try:
             for j in range(P):
-                piece = self.partial[j * world * blk * cols:(j + 1) * world * blk * cols]
+                piece = partial[j * world * blk * cols:(j + 1) * world * blk * cols]
                 self.ops.piece(h, blk, S, j * blk, world * blk, piece.data_ptr(), st)
-                self._ev[j].record(cur)
+                self.ops.stream_wait(h, self.comm.cuda_stream)  # in-packet completion event of the piece
                 with torch.cuda.stream(self.comm):
-                    self.comm.wait_event(self._ev[j])
-                    self._rs(self.recv[j * blk * cols:(j + 1) * blk * cols], piece)
-        finally:
-            self.ops.end(h)  # waits for the pre-reduce; key / repeated-row errors
-        self.comm.synchronize()
-        self.ops.apply(self.store, self.recv.data_ptr(), self.shard.size() * cols)
+                    self._rs(recv[j * blk * cols:(j + 1) * blk * cols], piece)
+        except BaseException:
+            self.ops.end(h)
+            raise
+        self._rs_done[k].record(self.comm)
+        if self._store_stream is not None:
+            self._store_stream.wait_event(self._rs_done[k])
+        else:
+            self.comm.synchronize()
+        self.ops.apply(self.store, recv.data_ptr(), self.shard.size() * cols)
+        if self._store_stream is not None:
+            self._applied[k].record(self._store_stream)
+        self._pending.append(h)
+        self._end_pending(keep=1)  # the previous call's pieces are done by now or soon
+
+    def _end_pending(self, keep: int = 0) -> None:
+        while len(self._pending) > keep:
+            self.ops.end(self._pending.pop(0))
 
     def push_local(self, dev_ptrs: Sequence[int], lens: Sequence[int]) -> None:
         """Pushes already split to this shard: exact ordered apply, no exchange."""
         self.store.pushDevice(dev_ptrs, lens)
 
     def flush(self):
-        self.store.flush()
+        """Every pushed call applied; raises the first deferred pre-reduce error."""
+        try:
+            self._end_pending(0)
+        finally:
+            if self.partial.is_cuda:
+                self.cstream.synchronize()
+                self.comm.synchronize()
+                for ev in self._applied:
+                    ev.synchronize()
+            self.store.flush()

@@ -206,7 +206,10 @@ int dml_reduce_buckets_dense(const dml_desc* desc, int64_t first_key, int64_t ro
  * writes the ordered sum of rows r(t) = (t / row_block) * row_stride + row_off
  * + t % row_block, t < ntask_rows, to dev_out + t*cols (rows >= `rows`, the
  * padding of linearSplit's short last shard, are zeros); _end waits for the
- * stream and reports key-out-of-matrix / repeated-row errors. Opaque handle. */
+ * index and every piece and reports key-out-of-matrix / repeated-row errors.
+ * Each piece runs on its own `stream` argument (0 = the null stream), which may
+ * differ from _begin's (the first such piece waits for the index on the host),
+ * so the next call's index can overlap the current call's pieces. Opaque handle. */
 typedef struct dml_prereduce dml_prereduce;
 int dml_prereduce_begin(const dml_desc* desc, int64_t first_key, int64_t rows, int32_t cols,
                         const void* const* dev_bufs, const int64_t* lens, int32_t n, void* stream,
@@ -214,6 +217,9 @@ int dml_prereduce_begin(const dml_desc* desc, int64_t first_key, int64_t rows, i
 int dml_prereduce_piece(dml_prereduce* p, int64_t row_block, int64_t row_stride, int64_t row_off,
                         int64_t ntask_rows, void* dev_out, void* stream);
 int dml_prereduce_end(dml_prereduce* p);
+/* Make `stream` wait (device side) for the pieces enqueued so far, e.g. the
+ * communication stream that reduce-scatters the piece just written. */
+int dml_prereduce_stream_wait(dml_prereduce* p, void* stream);
 
 /* --- synthetic workload generators (bench/test support) ----------------- *
  * Counter-based (SplitMix64) so the CPU oracle regenerates the same bytes.
