@@ -727,13 +727,18 @@ __global__ __launch_bounds__(256) void k_reduce_rows(T* __restrict__ shard, int6
     if (MODE == kAddCheckI32 && negpos != kNoPos) atomicMin(&ctrl->neg_pos, (unsigned long long)negpos);
 }
 
+// Occupancy cap: dynamic LDS (unused by the kernels) so that at most `bpc`
+// 256-thread blocks fit on a CU (160 KiB of LDS per CU). 0 = no cap.
+constexpr unsigned kLdsPerCU = 160 * 1024;
+inline unsigned lds_for_blocks_per_cu(int bpc) { return bpc > 0 ? kLdsPerCU / (unsigned)(bpc + 1) + 256u : 0u; }
+
 template <typename T, int MODE, int G = 8, bool NT = false, int WPB = 4, bool SNT = false, int CPW = 1, int RPW = 1,
           bool FULL = false>
 static hipError_t launch_reduce_t(void* shard, int64_t rows, int32_t cols, const Batch& bt, int nb,
                                   int64_t stride, int K, const int32_t* slot, const uint32_t* rowflag, Ctrl* ctrl,
                                   uint64_t tail_cut,
                                   const AdaArgs& ada, hipStream_t st, int64_t* nblocks_out, LaunchEv ev = {},
-                                  RowMap rm = {}) {
+                                  RowMap rm = {}, int bpc = 0) {
     constexpr int VEC = Elem<T>::VEC;
     const int32_t nchunks = (cols + 64 * VEC - 1) / (64 * VEC);
     const int32_t ngroups = (nchunks + CPW - 1) / CPW;
@@ -741,8 +746,9 @@ static hipError_t launch_reduce_t(void* shard, int64_t rows, int32_t cols, const
     const int64_t nblocks = (ntask + WPB - 1) / WPB;
     if (nblocks_out) *nblocks_out = nblocks;
     if (nblocks <= 0) return hipSuccess;
-    // experiment knob: dynamic LDS per block caps the blocks resident per CU (occupancy study)
-    static const unsigned occ_lds = getenv("DML_REDUCE_LDS") ? (unsigned)atoi(getenv("DML_REDUCE_LDS")) : 0u;
+    // blocks per CU: the shape's cap, or DML_REDUCE_LDS bytes of dynamic LDS (occupancy study)
+    static const char* lds_env = getenv("DML_REDUCE_LDS");
+    const unsigned occ_lds = lds_env ? (unsigned)atoi(lds_env) : lds_for_blocks_per_cu(bpc);
     if constexpr (RPW > 1) {
         static_assert(WPB == 4 && MODE != kAdaGrad && MODE != kRollbackI32, "k_reduce_rows shapes");
         if (ev.start || ev.stop)
@@ -771,17 +777,19 @@ static hipError_t launch_reduce_t(void* shard, int64_t rows, int32_t cols, const
 // G = pushes per load group, CPW = chunks per wave, RPW = rows per wave.
 // 10: G4/CPW4/RPW1 (the previous rule, k_reduce), 13: same with plain loads, 14: G2/CPW4/RPW1,
 // 20: CPW4/RPW4 (k_reduce_rows), 21: CPW4/RPW2, 24: CPW4/RPW4 plain loads, 27: CPW2/RPW4,
-// 28: CPW4/RPW2 FULL, 30: CPW4/RPW4 FULL two-deep ring, 31: CPW4/RPW2 FULL two-deep ring
-// (0 = auto: CPW4/RPW4 FULL for config 2).
+// 28: CPW4/RPW2 FULL uncapped, 29: CPW4/RPW4 FULL, 30: CPW4/RPW4 FULL two-deep ring, 31: CPW4/RPW2 FULL two-deep ring
+// (0 = auto: CPW4/RPW2 FULL, 2 blocks per CU, for config 2).
 int reduce_variant() {
     const char* v = getenv("DML_REDUCE_VARIANT");
     return v ? atoi(v) : 0;
 }
 
-// Shape rule (measured, scripts/ubench_reduce.hip + scripts/tune.py): a wave
-// owns RPW = 4 neighbouring rows and walks up to CPW = 4 neighbouring 1-KiB
-// chunks of each, with G pushes x RPW x CPW 16-B nt loads (16) in flight.
-// AdaGrad and the int32 rollback keep one row and one chunk per wave (their
+// Shape rule (measured, scripts/ubench_reduce.hip, scripts/exp_variants.py): a
+// wave owns RPW neighbouring rows and walks up to CPW = 4 neighbouring 1-KiB
+// chunks of each, RPW x CPW 16-B nt loads of one push in flight. Whole 4-KiB
+// rows: RPW = 2 with the CU capped at 2 blocks (8 waves, 64 KiB of loads in
+// flight); other widths RPW = 4 at their register-limited occupancy. AdaGrad and
+// the int32 rollback keep one row and one chunk per wave (k_reduce: their
 // per-element state triples the registers).
 template <typename T, int MODE>
 static hipError_t launch_auto(void* shard, int64_t rows, int32_t cols, const Batch& bt, int nb, int64_t stride, int K,
@@ -791,17 +799,20 @@ static hipError_t launch_auto(void* shard, int64_t rows, int32_t cols, const Bat
     const int32_t nchunks = (cols + 64 * VEC - 1) / (64 * VEC);
 #define DML_L(G, CPW, RPW) launch_reduce_t<T, MODE, G, true, 4, false, CPW, RPW>(shard, rows, cols, bt, nb, stride, K, \
                                                      slot, rowflag, ctrl, tail_cut, ada, st, nblocks_out, ev, rm)
-#define DML_LF(G, CPW, RPW) launch_reduce_t<T, MODE, G, true, 4, false, CPW, RPW, true>(shard, rows, cols, bt, nb, \
-                                                     stride, K, slot, rowflag, ctrl, tail_cut, ada, st, nblocks_out, ev, rm)
+#define DML_LF(G, CPW, RPW, BPC) launch_reduce_t<T, MODE, G, true, 4, false, CPW, RPW, true>(shard, rows, cols, bt, nb, \
+                                                     stride, K, slot, rowflag, ctrl, tail_cut, ada, st, nblocks_out, ev, rm, BPC)
     if constexpr (MODE == kAdaGrad || MODE == kRollbackI32) {
         return DML_L(8, 1, 1);
     } else {
         if (cols < VEC) return DML_L(16, 1, 1);  // narrower than one vector: k_reduce's generic path
-        if (cols % (64 * VEC * 4) == 0) return DML_LF(1, 4, 4);
+        // whole 4-KiB rows: two rows per wave and at most 8 waves per CU (64 KiB of
+        // loads in flight per CU) measured 3.5-5 % faster than 4 rows per wave at the
+        // register-limited 12-24 waves (scripts/exp_variants.py)
+        if (cols % (64 * VEC * 4) == 0) return DML_LF(1, 4, 2, 2);
         if (nchunks >= 4) return DML_L(1, 4, 4);
-        if (cols % (64 * VEC * 2) == 0) return DML_LF(1, 2, 4);
+        if (cols % (64 * VEC * 2) == 0) return DML_LF(1, 2, 4, 0);
         if (nchunks >= 2) return DML_L(1, 2, 4);
-        if (cols % (64 * VEC) == 0) return DML_LF(1, 1, 4);
+        if (cols % (64 * VEC) == 0) return DML_LF(1, 1, 4, 0);
         return DML_L(1, 1, 4);
     }
 #undef DML_L
@@ -845,6 +856,7 @@ hipError_t launch_reduce(int vtype, int mode, void* shard, int64_t rows, int32_t
                 case 30: return launch_reduce_t<float, kAdd, 2, true, 4, false, 4, 4, true>(shard, rows, cols, bt, nb, stride, K, slot, rowflag, ctrl, tail_cut, ada, st, nblocks_out, ev);
                 case 31: return launch_reduce_t<float, kAdd, 2, true, 4, false, 4, 2, true>(shard, rows, cols, bt, nb, stride, K, slot, rowflag, ctrl, tail_cut, ada, st, nblocks_out, ev);
                 case 28: return launch_reduce_t<float, kAdd, 1, true, 4, false, 4, 2, true>(shard, rows, cols, bt, nb, stride, K, slot, rowflag, ctrl, tail_cut, ada, st, nblocks_out, ev);
+                case 29: return launch_reduce_t<float, kAdd, 1, true, 4, false, 4, 4, true>(shard, rows, cols, bt, nb, stride, K, slot, rowflag, ctrl, tail_cut, ada, st, nblocks_out, ev);
                 default: return DML_A(float, kAdd);
             }
         }
