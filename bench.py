@@ -265,7 +265,7 @@ def main():
             pk = stream_peaks(L, torch)
             line["roofline"] = {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS,
                                 "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic,
-                                "kernel": "k_reduce<float,kAdd>", "avg_kernel_us": round(avg_s * 1e6, 2),
+                                "kernel": "k_reduce_rows<float,kAdd> (2 rows x 4 KiB per wave)", "avg_kernel_us": round(avg_s * 1e6, 2),
                                 "launches": k_n, "measured_read_peak": round(pk["read"], 1),
                                 "frac_of_measured_read": round(achieved / pk["read"], 4),
                                 "measured_copy_peak": round(pk["copy"], 1)}
