@@ -66,6 +66,12 @@ SIGNATURES = {
     "dml_prereduce_piece": (C.c_int, [_vp, _i64, _i64, _i64, _i64, _vp, _vp]),
     "dml_prereduce_end": (C.c_int, [_vp]),
     "dml_prereduce_stream_wait": (C.c_int, [_vp, _vp]),
+    "dml_group_unique_id": (C.c_int, [_vp, _i32]),
+    "dml_group_create": (C.c_int, [_vp, _i32, _i32, _i32, _P(dml_desc), _i64, _i32, _i32, _P(_vp)]),
+    "dml_group_store": (C.c_int, [_vp, _P(_vp)]),
+    "dml_group_push_full_range": (C.c_int, [_vp, _P(_vp), _P(_i64), _i32]),
+    "dml_group_flush": (C.c_int, [_vp]),
+    "dml_group_destroy": (None, [_vp]),
     "dml_synth_dense_bucket": (C.c_int, [_vp, _P(dml_desc), _i64, _i64, _i64, _i32, _u64, _u64, _u64, _vp]),
     "dml_synth_sparse_bucket": (C.c_int, [_vp, _P(dml_desc), _i64, _i64, _i64, _u64, _u64, _u64, _vp]),
     "dml_synth_fill_store": (C.c_int, [_vp, _u64]),

@@ -1,0 +1,228 @@
+// dml_group.hip — native multi-GPU shard group over RCCL (C-ABI dml_group_*).
+//
+// The JNI deployment has no torch.distributed: one PS process per GPU owns
+// shard `rank` of KeyRange.linearSplit(world) (KeyRange.java:68-80,
+// DMatrix.partition DMatrix.java:53-64) and reduces device-resident full-range
+// pushes with the same three steps as distml_amd/group.py:
+//   1. ordered pre-reduce of the rank's pushes into a partial of the whole
+//      matrix (dml_prereduce_*, k_reduce_rows in pre-reduce mode), in P row
+//      slices laid out [rank][row];
+//   2. ncclReduceScatter(sum) of each slice on a communication stream as soon
+//      as the slice is written (xGMI under the next slice's pre-reduce);
+//   3. owner apply shard += received on the store's stream.
+// Calls are asynchronous and overlap exactly as in group.py: the next call's key
+// index runs on a high-priority side stream, two partial / receive buffer sets
+// alternate, and a call's key / repeated-row errors surface at the next call or
+// at dml_group_flush. The communicator comes from ncclCommInitRank with a
+// unique id the caller distributes (the JVM's control plane).
+#include <rccl/rccl.h>
+
+#include <cstring>
+#include <deque>
+#include <string>
+#include <vector>
+
+#include "distml_ps.h"
+#include "dml_internal.h"
+
+using namespace dml;
+
+#define GHIP(x)                                                                                        \
+    do {                                                                                               \
+        hipError_t e_ = (x);                                                                           \
+        if (e_ != hipSuccess) return set_error(DML_E_HIP, std::string(#x) + ": " + hipGetErrorString(e_)); \
+    } while (0)
+#define GNCCL(x)                                                                                       \
+    do {                                                                                               \
+        ncclResult_t r_ = (x);                                                                         \
+        if (r_ != ncclSuccess) return set_error(DML_E_HIP, std::string(#x) + ": " + ncclGetErrorString(r_)); \
+    } while (0)
+#define GRC(x)                     \
+    do {                           \
+        int rc_ = (x);             \
+        if (rc_ != DML_OK) return rc_; \
+    } while (0)
+
+struct dml_group {
+    int rank = 0, world = 1, device = 0, pieces = 4;
+    dml_desc desc{};
+    int64_t total_rows = 0, step_rows = 0, shard_first = 0, shard_rows = 0;
+    int32_t cols = 0;
+    size_t vbytes = 4;
+    ncclComm_t comm = nullptr;
+    ncclDataType_t dtype = ncclFloat32;
+    hipStream_t cstream = nullptr;  // pre-reduce pieces
+    hipStream_t istream = nullptr;  // key index of the next call (high priority: its own queue)
+    hipStream_t rstream = nullptr;  // reduce-scatter
+    dml_store* store = nullptr;
+    hipStream_t sstream = nullptr;  // the store's stream (owner apply)
+    void* partial[2] = {nullptr, nullptr};
+    void* recv[2] = {nullptr, nullptr};
+    hipEvent_t rs_done[2] = {nullptr, nullptr};
+    hipEvent_t applied[2] = {nullptr, nullptr};
+    std::deque<dml_prereduce*> pending;
+    int k = 0;
+};
+
+namespace {
+
+int end_pending(dml_group* g, size_t keep) {
+    int rc = DML_OK;
+    while (g->pending.size() > keep) {
+        dml_prereduce* p = g->pending.front();
+        g->pending.pop_front();
+        const int r = dml_prereduce_end(p);
+        if (rc == DML_OK) rc = r;
+    }
+    return rc;
+}
+
+void group_free(dml_group* g) {
+    if (!g) return;
+    (void)hipSetDevice(g->device);
+    (void)end_pending(g, 0);
+    for (int i = 0; i < 2; ++i) {
+        if (g->partial[i]) (void)hipFree(g->partial[i]);
+        if (g->recv[i]) (void)hipFree(g->recv[i]);
+        if (g->rs_done[i]) (void)hipEventDestroy(g->rs_done[i]);
+        if (g->applied[i]) (void)hipEventDestroy(g->applied[i]);
+    }
+    if (g->comm) (void)ncclCommDestroy(g->comm);
+    if (g->store) dml_store_destroy(g->store);
+    for (hipStream_t s : {g->cstream, g->istream, g->rstream})
+        if (s) (void)hipStreamDestroy(s);
+    delete g;
+}
+
+int group_init(dml_group* g, const uint8_t* unique_id) {
+    GHIP(hipSetDevice(g->device));
+    int lo = 0, hi = 0;
+    GHIP(hipDeviceGetStreamPriorityRange(&lo, &hi));
+    GHIP(hipStreamCreateWithFlags(&g->cstream, hipStreamNonBlocking));
+    GHIP(hipStreamCreateWithPriority(&g->istream, hipStreamNonBlocking, hi));
+    GHIP(hipStreamCreateWithFlags(&g->rstream, hipStreamNonBlocking));
+    // linearSplit(world): every rank's slice of the partial is step_rows long
+    std::vector<int64_t> f((size_t)g->world), l((size_t)g->world);
+    GRC(dml_linear_split(0, g->total_rows - 1, g->world, f.data(), l.data()));
+    g->step_rows = l[0] - f[0] + 1;
+    g->shard_first = f[(size_t)g->rank];
+    g->shard_rows = l[(size_t)g->rank] - f[(size_t)g->rank] + 1;
+    if (g->shard_rows <= 0) return set_error(DML_E_UNSUPPORTED, "empty shard (world > rows)");
+    GRC(dml_store_create_range(&g->desc, g->shard_first, l[(size_t)g->rank], g->cols, g->device, 0, &g->store));
+    void* ss = nullptr;
+    GRC(dml_store_stream(g->store, &ss));
+    g->sstream = (hipStream_t)ss;
+    const size_t part = (size_t)g->world * (size_t)g->step_rows * (size_t)g->cols * g->vbytes;
+    const size_t rcv = (size_t)g->step_rows * (size_t)g->cols * g->vbytes;
+    for (int i = 0; i < 2; ++i) {
+        GHIP(hipMalloc(&g->partial[i], part));
+        GHIP(hipMalloc(&g->recv[i], rcv));
+        GHIP(hipEventCreateWithFlags(&g->rs_done[i], hipEventDisableTiming));
+        GHIP(hipEventCreateWithFlags(&g->applied[i], hipEventDisableTiming));
+    }
+    ncclUniqueId id;
+    memcpy(&id, unique_id, sizeof id);
+    GNCCL(ncclCommInitRank(&g->comm, g->world, id, g->rank));
+    return DML_OK;
+}
+
+}  // namespace
+
+extern "C" {
+
+int dml_group_unique_id(uint8_t* out, int32_t cap) {
+    if (!out || cap < NCCL_UNIQUE_ID_BYTES) return set_error(DML_E_INVALID_ARG, "need 128 bytes for the unique id");
+    ncclUniqueId id;
+    GNCCL(ncclGetUniqueId(&id));
+    memcpy(out, &id, sizeof id);
+    return DML_OK;
+}
+
+int dml_group_create(const uint8_t* unique_id, int32_t world, int32_t rank, int32_t device, const dml_desc* desc,
+                     int64_t total_rows, int32_t cols, int32_t pieces, dml_group** out) {
+    if (!unique_id || !desc || !out || world <= 0 || rank < 0 || rank >= world || total_rows <= 0 || cols <= 0 ||
+        pieces <= 0)
+        return set_error(DML_E_INVALID_ARG, "bad group arguments");
+    if (desc->data_type != DML_DATA_TYPE_MATRIX || !desc->dense_column || desc->ada_grad)
+        return set_error(DML_E_UNSUPPORTED, "the sharded path supports dense-column plain matrices");
+    auto* g = new (std::nothrow) dml_group();
+    if (!g) return set_error(DML_E_NOMEM, "out of host memory");
+    g->world = world;
+    g->rank = rank;
+    g->device = device;
+    g->desc = *desc;
+    g->total_rows = total_rows;
+    g->cols = cols;
+    g->pieces = pieces;
+    switch (desc->value_type) {
+        case DML_ELEMENT_TYPE_FLOAT: g->dtype = ncclFloat32; g->vbytes = 4; break;
+        case DML_ELEMENT_TYPE_INT: g->dtype = ncclInt32; g->vbytes = 4; break;  // exact: mod 2^32 like the JVM int
+        case DML_ELEMENT_TYPE_DOUBLE: g->dtype = ncclFloat64; g->vbytes = 8; break;
+        default: delete g; return set_error(DML_E_BAD_DESC, "bad value type");
+    }
+    if (int rc = group_init(g, unique_id)) {
+        group_free(g);
+        return rc;
+    }
+    *out = g;
+    return DML_OK;
+}
+
+int dml_group_store(dml_group* g, dml_store** store) {
+    if (!g || !store) return set_error(DML_E_INVALID_ARG, "null group");
+    *store = g->store;
+    return DML_OK;
+}
+
+int dml_group_push_full_range(dml_group* g, const void* const* dev_bufs, const int64_t* lens, int32_t n) {
+    if (!g || n < 0 || n > kMaxW || (n > 0 && (!dev_bufs || !lens)))
+        return set_error(DML_E_INVALID_ARG, "bad push arguments (n must be <= 64)");
+    GHIP(hipSetDevice(g->device));
+    const int64_t S = g->step_rows, P = g->pieces;
+    if (S % P) return set_error(DML_E_INVALID_ARG, "pieces must divide the linearSplit step");
+    const int64_t blk = S / P, W = g->world, C = g->cols;
+    const int k = g->k;
+    g->k ^= 1;
+    dml_prereduce* h = nullptr;
+    GRC(dml_prereduce_begin(&g->desc, 0, g->total_rows, g->cols, dev_bufs, lens, n, g->istream, &h));
+    // buffer set k was used two calls ago: its apply (behind its reduce-scatter) is done
+    int rc = hipEventSynchronize(g->applied[k]) == hipSuccess ? DML_OK : set_error(DML_E_HIP, "applied wait");
+    uint8_t* part = (uint8_t*)g->partial[k];
+    uint8_t* rcv = (uint8_t*)g->recv[k];
+    for (int64_t j = 0; j < P && rc == DML_OK; ++j) {
+        uint8_t* piece = part + (size_t)(j * W * blk * C) * g->vbytes;
+        rc = dml_prereduce_piece(h, blk, S, j * blk, W * blk, piece, g->cstream);
+        if (rc == DML_OK) rc = dml_prereduce_stream_wait(h, g->rstream);
+        if (rc == DML_OK) {
+            const ncclResult_t r = ncclReduceScatter(piece, rcv + (size_t)(j * blk * C) * g->vbytes,
+                                                     (size_t)(blk * C), g->dtype, ncclSum, g->comm, g->rstream);
+            if (r != ncclSuccess) rc = set_error(DML_E_HIP, std::string("ncclReduceScatter: ") + ncclGetErrorString(r));
+        }
+    }
+    if (rc != DML_OK) {
+        (void)dml_prereduce_end(h);
+        return rc;
+    }
+    GHIP(hipEventRecord(g->rs_done[k], g->rstream));
+    GHIP(hipStreamWaitEvent(g->sstream, g->rs_done[k], 0));
+    GRC(dml_store_apply_dense_device(g->store, rcv, g->shard_rows * C));
+    GHIP(hipEventRecord(g->applied[k], g->sstream));
+    g->pending.push_back(h);
+    return end_pending(g, 1);  // the previous call's errors
+}
+
+int dml_group_flush(dml_group* g) {
+    if (!g) return set_error(DML_E_INVALID_ARG, "null group");
+    GHIP(hipSetDevice(g->device));
+    int rc = end_pending(g, 0);
+    for (hipStream_t s : {g->cstream, g->rstream})
+        if (hipStreamSynchronize(s) != hipSuccess && rc == DML_OK) rc = set_error(DML_E_HIP, "group stream sync");
+    for (hipEvent_t e : g->applied)
+        if (hipEventSynchronize(e) != hipSuccess && rc == DML_OK) rc = set_error(DML_E_HIP, "apply sync");
+    const int r2 = dml_store_flush(g->store);
+    return rc != DML_OK ? rc : r2;
+}
+
+void dml_group_destroy(dml_group* g) { group_free(g); }
+
+}  // extern "C"

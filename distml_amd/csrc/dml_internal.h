@@ -4,6 +4,8 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
+#include <string>
+
 namespace dml {
 
 // One ordered batch chunk holds at most this many pushes (the slot table is
@@ -167,5 +169,9 @@ int64_t reduce_blocks(int vtype, int64_t rows, int32_t cols);
 bool reduce_clears_slots(int vtype, int mode, int32_t cols);
 
 uint64_t splitmix64(uint64_t x);
+
+// Records `msg` as the calling thread's dml_last_error() and returns `code`
+// (dml_store.hip; shared by the C-ABI translation units).
+int set_error(int code, const std::string& msg);
 
 }  // namespace dml

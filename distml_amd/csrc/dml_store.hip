@@ -35,6 +35,7 @@ static int set_err(int code, const std::string& msg) {
     g_err = msg;
     return code;
 }
+int dml::set_error(int code, const std::string& msg) { return set_err(code, msg); }
 
 #define HIPCHK(x)                                                                                  \
     do {                                                                                           \

@@ -197,3 +197,54 @@ class ShardGroup:
                 for ev in self._applied:
                     ev.synchronize()
             self.store.flush()
+
+
+class NativeShardGroup:
+    """The same sharded path through the C-ABI's own RCCL communicator
+    (dml_group_*, distml_amd/csrc/dml_group.hip): what a host without
+    torch.distributed (the JNI deployment) binds. `unique_id` is the 128 bytes
+    NativeShardGroup.unique_id() returns on rank 0, distributed by the caller."""
+
+    def __init__(self, fmt: DataDesc, total_rows: int, cols: int, rank: int, world: int, unique_id: bytes,
+                 device: int = 0, pieces: int = 4):
+        L = _lib.load()
+        self._L = L
+        if len(unique_id) != 128:
+            raise ValueError("unique_id must be the 128 bytes of NativeShardGroup.unique_id()")
+        h = C.c_void_p()
+        idb = (C.c_uint8 * 128).from_buffer_copy(unique_id)
+        check(L.dml_group_create(idb, world, rank, device, C.byref(fmt.to_c()), total_rows, cols, pieces,
+                                 C.byref(h)))
+        self._h = h.value
+        self.fmt, self.cols, self.rank, self.world = fmt, cols, rank, world
+        self.shard = KeyRange(0, total_rows - 1).linearSplit(world)[rank]
+        sp = C.c_void_p()
+        check(L.dml_group_store(C.c_void_p(self._h), C.byref(sp)))
+        self.store = DataStore._wrap(fmt, self.shard, cols, device, sp.value)
+
+    @staticmethod
+    def unique_id() -> bytes:
+        buf = (C.c_uint8 * 128)()
+        check(_lib.load().dml_group_unique_id(buf, 128))
+        return bytes(buf)
+
+    def push_full_range(self, dev_ptrs: Sequence[int], lens: Sequence[int]) -> None:
+        n = len(dev_ptrs)
+        ptrs = (C.c_void_p * max(n, 1))(*dev_ptrs)
+        ls = (C.c_int64 * max(n, 1))(*lens)
+        check(self._L.dml_group_push_full_range(C.c_void_p(self._h), ptrs, ls, n))
+
+    def flush(self) -> None:
+        check(self._L.dml_group_flush(C.c_void_p(self._h)))
+
+    def close(self) -> None:
+        if self._h:
+            self.store._h = None  # owned by the group
+            self._L.dml_group_destroy(C.c_void_p(self._h))
+            self._h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass

@@ -93,8 +93,24 @@ class DataStore:
         self._rows, self._cols = rows.value, c.value
         self.dtype = VALUE_DTYPE[format.valueType]
 
+    @classmethod
+    def _wrap(cls, format: DataDesc, keys: KeyRange, cols: int, device: int, handle: int) -> "DataStore":
+        """A view of a store owned elsewhere (a dml_group's shard): same API, no ownership."""
+        self = cls.__new__(cls)
+        self.format, self.localRows, self.device = format, keys, device
+        self._h = handle
+        self._owned = False
+        rows, c = C.c_int64(), C.c_int32()
+        _lib.load().dml_store_shape(self._h, C.byref(rows), C.byref(c))
+        self._rows, self._cols = rows.value, c.value
+        self.dtype = VALUE_DTYPE[format.valueType]
+        return self
+
     # ---- lifecycle ----------------------------------------------------------
     def close(self):
+        if not getattr(self, "_owned", True):
+            self._h = None
+            return
         if getattr(self, "_h", None):
             _lib.load().dml_store_destroy(self._h)
             self._h = None

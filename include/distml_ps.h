@@ -221,6 +221,27 @@ int dml_prereduce_end(dml_prereduce* p);
  * communication stream that reduce-scatters the piece just written. */
 int dml_prereduce_stream_wait(dml_prereduce* p, void* stream);
 
+/* --- native multi-GPU shard group (RCCL) -------------------------------- *
+ * One process per GPU; rank r owns shard r of KeyRange.linearSplit(world)
+ * (KeyRange.java:68-80). Full-range device-resident pushes are pre-reduced in
+ * push order, reduce-scattered over xGMI (ncclReduceScatter, sum) and applied
+ * by the owner — the path distml_amd/group.py runs over torch.distributed, for
+ * hosts without Python (the JNI deployment). The caller distributes the
+ * 128-byte unique id from rank 0 (e.g. over the PS control plane). Pushes are
+ * asynchronous: buffers stay valid until the next dml_group_flush, and a
+ * call's key / repeated-row errors surface at the next call or the flush.
+ * fp32 results differ from the sequential order only by summation order
+ * (DESIGN.md §6); int32 is exact. */
+typedef struct dml_group dml_group;
+int dml_group_unique_id(uint8_t* out, int32_t cap);
+int dml_group_create(const uint8_t* unique_id, int32_t world, int32_t rank, int32_t device, const dml_desc* desc,
+                     int64_t total_rows, int32_t cols, int32_t pieces, dml_group** out);
+/* The rank's shard store (fetch / checkpoint / read), owned by the group. */
+int dml_group_store(dml_group* g, dml_store** store);
+int dml_group_push_full_range(dml_group* g, const void* const* dev_bufs, const int64_t* lens, int32_t n);
+int dml_group_flush(dml_group* g);
+void dml_group_destroy(dml_group* g);
+
 /* --- synthetic workload generators (bench/test support) ----------------- *
  * Counter-based (SplitMix64) so the CPU oracle regenerates the same bytes.
  * Spec in DESIGN.md §Synthetic data. Run on `stream` (void* hipStream_t). */

@@ -154,3 +154,63 @@ JNIEXPORT void JNICALL FN(nativeSetAlpha)(JNIEnv* env, jclass, jlong h, jfloat a
 JNIEXPORT void JNICALL FN(nativeDestroy)(JNIEnv*, jclass, jlong h) { dml_store_destroy(H(h)); }
 
 }  // extern "C"
+
+// ---- com.intel.distml.util.store.GpuShardGroup -> dml_group_* -------------
+#define GFN(name) Java_com_intel_distml_util_store_GpuShardGroup_##name
+static dml_group* G(jlong h) { return reinterpret_cast<dml_group*>(h); }
+
+extern "C" {
+
+JNIEXPORT jbyteArray JNICALL GFN(nativeUniqueId)(JNIEnv* env, jclass) {
+    uint8_t id[128];
+    if (int rc = dml_group_unique_id(id, 128)) {
+        throw_for(env, rc);
+        return nullptr;
+    }
+    jbyteArray out = env->NewByteArray(128);
+    env->SetByteArrayRegion(out, 0, 128, reinterpret_cast<const jbyte*>(id));
+    return out;
+}
+
+JNIEXPORT jlong JNICALL GFN(nativeGroupCreate)(JNIEnv* env, jclass, jbyteArray id, jint world, jint rank,
+                                               jint device, jint dt, jint kt, jint vt, jint dr, jint dc, jint ada,
+                                               jlong total_rows, jint cols, jint pieces) {
+    uint8_t buf[128] = {0};
+    if (env->GetArrayLength(id) != 128) {
+        env->ThrowNew(env->FindClass("java/lang/IllegalArgumentException"), "unique id must be 128 bytes");
+        return 0;
+    }
+    env->GetByteArrayRegion(id, 0, 128, reinterpret_cast<jbyte*>(buf));
+    dml_desc d{dt, kt, vt, dr, dc, ada};
+    dml_group* g = nullptr;
+    if (int rc = dml_group_create(buf, world, rank, device, &d, total_rows, cols, pieces, &g)) throw_for(env, rc);
+    return reinterpret_cast<jlong>(g);
+}
+
+JNIEXPORT void JNICALL GFN(nativeGroupPush)(JNIEnv* env, jclass, jlong g, jlongArray ptrs, jlongArray lens) {
+    const jsize n = env->GetArrayLength(ptrs);
+    std::vector<jlong> p((size_t)n), l((size_t)n);
+    env->GetLongArrayRegion(ptrs, 0, n, p.data());
+    env->GetLongArrayRegion(lens, 0, n, l.data());
+    std::vector<const void*> dp((size_t)n);
+    std::vector<int64_t> dl((size_t)n);
+    for (jsize i = 0; i < n; ++i) {
+        dp[(size_t)i] = reinterpret_cast<const void*>(p[(size_t)i]);
+        dl[(size_t)i] = l[(size_t)i];
+    }
+    if (int rc = dml_group_push_full_range(G(g), dp.data(), dl.data(), (int32_t)n)) throw_for(env, rc);
+}
+
+JNIEXPORT void JNICALL GFN(nativeGroupFlush)(JNIEnv* env, jclass, jlong g) {
+    if (int rc = dml_group_flush(G(g))) throw_for(env, rc);
+}
+
+JNIEXPORT jlong JNICALL GFN(nativeGroupStore)(JNIEnv* env, jclass, jlong g) {
+    dml_store* s = nullptr;
+    if (int rc = dml_group_store(G(g), &s)) throw_for(env, rc);
+    return reinterpret_cast<jlong>(s);
+}
+
+JNIEXPORT void JNICALL GFN(nativeGroupDestroy)(JNIEnv*, jclass, jlong g) { dml_group_destroy(G(g)); }
+
+}  // extern "C"

@@ -642,3 +642,42 @@ def test_prereduce_pieces_row_map(oracle):
             r = (t // blk) * S + j * blk + t % blk
             want = o.data[r] if r < rows else np.zeros(cols, np.float32)
             assert got[j, t].tobytes() == want.tobytes(), (j, t, r)
+
+
+@pytest.mark.parametrize("vt", [1, 0])
+def test_native_group_rccl_world1(oracle, vt):
+    """dml_group_* (the C-ABI's own RCCL communicator, no torch.distributed) at world 1:
+    two asynchronous full-range calls + flush. fp32 within the summation-order bound of
+    tests/test_group_gloo.py, int32 exact."""
+    from distml_amd import DataDesc
+    from distml_amd.group import NativeShardGroup
+    rows, cols, W = 1000, 256, 5
+    fmt = DataDesc(1, 0, vt)
+    g = NativeShardGroup(fmt, rows, cols, 0, 1, NativeShardGroup.unique_id(), device=0, pieces=4)
+    try:
+        g.store.rand(3)
+        pas = [1, 3, 7, 9, 11]  # coprime with 1000: each push lists every row once
+        host = [oracle.synth_dense_bucket(0, vt, 0, rows, rows, cols, 70 + b, pas[b], 3 * b) for b in range(W)]
+        dev = [torch.from_numpy(h).cuda() for h in host]
+        torch.cuda.synchronize()
+        ptrs, lens = [d.data_ptr() for d in dev], [d.numel() for d in dev]
+        g.push_full_range(ptrs[:3], lens[:3])
+        g.push_full_range(ptrs[3:], lens[3:])
+        g.flush()
+        o = oracle_store(oracle, fmt, 0, rows - 1, cols)
+        o.synth_fill(3)
+        init = o.data.copy()
+        for h in host:
+            assert o.push(h.tobytes()) == 0
+        got = g.store.values()
+        if vt == 0:
+            assert np.array_equal(got, o.data)
+            return
+        terms = np.abs(init.astype(np.float64))
+        for h in host:
+            rec = h.reshape(rows, 4 + 4 * cols)
+            terms[rec[:, :4].copy().view("<i4").ravel()] += np.abs(rec[:, 4:].copy().view("<f4"))
+        diff = np.abs(got.astype(np.float64) - o.data.astype(np.float64))
+        assert np.all(diff <= 2 * W * 2.0 ** -24 * terms)
+    finally:
+        g.close()
