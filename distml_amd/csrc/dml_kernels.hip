@@ -458,8 +458,8 @@ __global__ __launch_bounds__(64 * WPB) void k_reduce(T* __restrict__ shard, int6
 // so the hot loop carries no cutoff logic. Same results as k_reduce bit for bit
 // (same per-element add order, cutoff and negativity rules); rows narrower than
 // one vector use k_reduce.
-template <typename T, int MODE, int CPW, int RPW, bool NT, bool FULL, int DEPTH>
-__global__ __launch_bounds__(256) void k_reduce_rows(T* __restrict__ shard, int64_t rows, int32_t cols,
+template <typename T, int MODE, int CPW, int RPW, bool NT, bool FULL, int DEPTH, int WPB = 4, int SNT = 0>
+__global__ __launch_bounds__(64 * WPB) void k_reduce_rows(T* __restrict__ shard, int64_t rows, int32_t cols,
                                                      int32_t ngroups, const Batch bt, int nb, int64_t stride, int K,
                                                      int32_t* __restrict__ slot,
                                                      const uint32_t* __restrict__ rowflag, Ctrl* __restrict__ ctrl,
@@ -468,7 +468,7 @@ __global__ __launch_bounds__(256) void k_reduce_rows(T* __restrict__ shard, int6
     static_assert(MODE == kAdd || MODE == kAddCheckI32 || MODE == kPreReduce, "plain-sum modes only");
     const int lane = threadIdx.x & 63;
     const int wid = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-    const int64_t task = (int64_t)blockIdx.x * 4 + wid;
+    const int64_t task = (int64_t)blockIdx.x * WPB + wid;
     const int64_t ntask = (rows + RPW - 1) / RPW * (int64_t)ngroups;
     if (task >= ntask) return;
     if (bt.prev && ctrl_abnormal(bt.prev)) return;  // predecessor needs the host first
@@ -716,7 +716,20 @@ __global__ __launch_bounds__(256) void k_reduce_rows(T* __restrict__ shard, int6
         for (int c = 0; c < CPW; ++c) {
             T* prow = rowp[r] + c0[c];
             if (nv[c] == VEC) {
-                stg16(prow, pack<T>(acc[r][c]));
+                // SNT: 0 plain, 1 non-temporal, 2 write-through (sc1: no dirty L2 line left
+                // for the kernel-end writeback)
+                if constexpr (SNT == 2) {
+                    const uint64_t rb = (uint64_t)rowp[r];
+                    const void* base = (const void*)(((uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)rb)) |
+                                                     ((uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)(rb >> 32)) << 32));
+                    const auto rsrc = __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(base), 0,
+                                                                        cols * (int)sizeof(T), 0x00020000);
+                    __builtin_amdgcn_raw_buffer_store_b128(pack<T>(acc[r][c]), rsrc, c0[c] * (int)sizeof(T), 0, 16);
+                } else if constexpr (SNT == 1) {
+                    stg16_nt(prow, pack<T>(acc[r][c]));
+                } else {
+                    stg16(prow, pack<T>(acc[r][c]));
+                }
             } else {
 #pragma unroll
                 for (int e = 0; e < VEC; ++e)
@@ -732,7 +745,7 @@ __global__ __launch_bounds__(256) void k_reduce_rows(T* __restrict__ shard, int6
 constexpr unsigned kLdsPerCU = 160 * 1024;
 inline unsigned lds_for_blocks_per_cu(int bpc) { return bpc > 0 ? kLdsPerCU / (unsigned)(bpc + 1) + 256u : 0u; }
 
-template <typename T, int MODE, int G = 8, bool NT = false, int WPB = 4, bool SNT = false, int CPW = 1, int RPW = 1,
+template <typename T, int MODE, int G = 8, bool NT = false, int WPB = 4, int SNT = 0, int CPW = 1, int RPW = 1,
           bool FULL = false>
 static hipError_t launch_reduce_t(void* shard, int64_t rows, int32_t cols, const Batch& bt, int nb,
                                   int64_t stride, int K, const int32_t* slot, const uint32_t* rowflag, Ctrl* ctrl,
@@ -750,13 +763,13 @@ static hipError_t launch_reduce_t(void* shard, int64_t rows, int32_t cols, const
     static const char* lds_env = getenv("DML_REDUCE_LDS");
     const unsigned occ_lds = lds_env ? (unsigned)atoi(lds_env) : lds_for_blocks_per_cu(bpc);
     if constexpr (RPW > 1) {
-        static_assert(WPB == 4 && MODE != kAdaGrad && MODE != kRollbackI32, "k_reduce_rows shapes");
+        static_assert(MODE != kAdaGrad && MODE != kRollbackI32, "k_reduce_rows shapes");
         if (ev.start || ev.stop)
-            hipExtLaunchKernelGGL((k_reduce_rows<T, MODE, CPW, RPW, NT, FULL, (FULL && G == 2) ? 2 : 1>), dim3((unsigned)nblocks), dim3(256),
+            hipExtLaunchKernelGGL((k_reduce_rows<T, MODE, CPW, RPW, NT, FULL, (FULL && G == 2) ? 2 : 1, WPB, SNT>), dim3((unsigned)nblocks), dim3(64 * WPB),
                                   occ_lds, st, ev.start, ev.stop, 0, (T*)shard, rows, cols, ngroups, bt, nb, stride,
                                   K, const_cast<int32_t*>(slot), rowflag, ctrl, tail_cut, rm);
         else
-            hipLaunchKernelGGL((k_reduce_rows<T, MODE, CPW, RPW, NT, FULL, (FULL && G == 2) ? 2 : 1>), dim3((unsigned)nblocks), dim3(256),
+            hipLaunchKernelGGL((k_reduce_rows<T, MODE, CPW, RPW, NT, FULL, (FULL && G == 2) ? 2 : 1, WPB, SNT>), dim3((unsigned)nblocks), dim3(64 * WPB),
                                occ_lds, st, (T*)shard, rows, cols, ngroups, bt, nb, stride, K, const_cast<int32_t*>(slot), rowflag,
                                ctrl, tail_cut, rm);
     } else {
@@ -856,6 +869,12 @@ hipError_t launch_reduce(int vtype, int mode, void* shard, int64_t rows, int32_t
                 case 30: return launch_reduce_t<float, kAdd, 2, true, 4, false, 4, 4, true>(shard, rows, cols, bt, nb, stride, K, slot, rowflag, ctrl, tail_cut, ada, st, nblocks_out, ev);
                 case 31: return launch_reduce_t<float, kAdd, 2, true, 4, false, 4, 2, true>(shard, rows, cols, bt, nb, stride, K, slot, rowflag, ctrl, tail_cut, ada, st, nblocks_out, ev);
                 case 28: return launch_reduce_t<float, kAdd, 1, true, 4, false, 4, 2, true>(shard, rows, cols, bt, nb, stride, K, slot, rowflag, ctrl, tail_cut, ada, st, nblocks_out, ev);
+                case 32: return launch_reduce_t<float, kAdd, 1, true, 8, false, 4, 2, true>(shard, rows, cols, bt, nb, stride, K, slot, rowflag, ctrl, tail_cut, ada, st, nblocks_out, ev, {}, 1);
+                case 33: return launch_reduce_t<float, kAdd, 1, true, 2, false, 4, 2, true>(shard, rows, cols, bt, nb, stride, K, slot, rowflag, ctrl, tail_cut, ada, st, nblocks_out, ev, {}, 4);
+                case 34: return launch_reduce_t<float, kAdd, 1, true, 4, true, 4, 2, true>(shard, rows, cols, bt, nb, stride, K, slot, rowflag, ctrl, tail_cut, ada, st, nblocks_out, ev, {}, 2);
+                case 35: return launch_reduce_t<float, kAdd, 1, true, 1, false, 4, 2, true>(shard, rows, cols, bt, nb, stride, K, slot, rowflag, ctrl, tail_cut, ada, st, nblocks_out, ev, {}, 8);
+                case 37: return launch_reduce_t<float, kAdd, 1, true, 4, 2, 4, 2, true>(shard, rows, cols, bt, nb, stride, K, slot, rowflag, ctrl, tail_cut, ada, st, nblocks_out, ev, {}, 2);
+                case 36: return launch_reduce_t<float, kAdd, 1, true, 4, false, 4, 1 + 1, true>(shard, rows, cols, bt, nb, stride, K, slot, rowflag, ctrl, tail_cut, ada, st, nblocks_out, ev, {}, 2);
                 case 29: return launch_reduce_t<float, kAdd, 1, true, 4, false, 4, 4, true>(shard, rows, cols, bt, nb, stride, K, slot, rowflag, ctrl, tail_cut, ada, st, nblocks_out, ev);
                 default: return DML_A(float, kAdd);
             }
