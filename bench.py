@@ -104,7 +104,8 @@ def sparse_leg(L, torch, steps: int):
         bufs.append(t)
     torch.cuda.synchronize()
     batch = DeviceBatch([b.data_ptr() for b in bufs], [b.numel() for b in bufs])
-    store.pushDevice(batch)
+    for _ in range(max(2, steps)):  # warmup: as many untimed steps as timed ones
+        store.pushDevice(batch)
     store.flush()
     store.set_timing(True)
     store.kernel_time(reset=True)
@@ -160,11 +161,13 @@ def load_traffic():
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=20)
-    ap.add_argument("--warmup", type=int, default=3)
+    # ~0.2 s of warmup and ~0.4 s timed at N=1: a few-ms window on a GPU that sat idle
+    # through process start-up measured 5 % slow (clocks still ramping)
+    ap.add_argument("--steps", type=int, default=1000)
+    ap.add_argument("--warmup", type=int, default=500)
     ap.add_argument("--no-cpu", action="store_true", help="skip the CPU baseline leg")
     ap.add_argument("--no-timing", action="store_true", help="no kernel timing events in the timed region")
-    ap.add_argument("--sparse-steps", type=int, default=5, help="config-3 sparse leg steps (0 = skip)")
+    ap.add_argument("--sparse-steps", type=int, default=20, help="config-3 sparse leg steps (0 = skip)")
     ap.add_argument("--pieces", type=int, default=4, help="pre-reduce row slices per call (sharded path)")
     ap.add_argument("--group", action="store_true",
                     help="use the sharded pre-reduce/reduce-scatter path even at N=1 (path check)")

@@ -10,8 +10,8 @@ tail -2 gpurun_out/gpu_tests.log
 timeout -k 10 120 python -c "import __graft_entry__ as g; g.smoke()"
 timeout -k 10 300 python bench.py > gpurun_out/bench.json 2> gpurun_out/bench.err
 cat gpurun_out/bench.json
-timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $R/gpurun_out/prof_stats -o run --output-format csv -- python3 bench.py --steps 20 --warmup 3 --no-cpu --sparse-steps 0 > gpurun_out/prof_stats.log 2>&1
-timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $R/gpurun_out/prof_sparse -o run --output-format csv -- python3 bench.py --steps 2 --warmup 1 --no-cpu --sparse-steps 5 > gpurun_out/prof_sparse.log 2>&1
-timeout -s KILL 120 rocprofv3 --pmc FETCH_SIZE -d $R/gpurun_out/prof_fetch -o run --output-format csv -- python3 bench.py --steps 4 --warmup 1 --no-cpu --sparse-steps 0 > gpurun_out/prof_fetch.log 2>&1
-timeout -s KILL 120 rocprofv3 --pmc WRITE_SIZE -d $R/gpurun_out/prof_write -o run --output-format csv -- python3 bench.py --steps 4 --warmup 1 --no-cpu --sparse-steps 0 > gpurun_out/prof_write.log 2>&1
+timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $R/gpurun_out/prof_stats -o run --output-format csv -- python3 bench.py --steps 200 --warmup 100 --no-cpu --sparse-steps 0 > gpurun_out/prof_stats.log 2>&1
+timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $R/gpurun_out/prof_sparse -o run --output-format csv -- python3 bench.py --steps 2 --warmup 1 --no-cpu --sparse-steps 10 > gpurun_out/prof_sparse.log 2>&1
+timeout -s KILL 120 rocprofv3 --pmc FETCH_SIZE -d $R/gpurun_out/prof_fetch -o run --output-format csv -- python3 bench.py --steps 10 --warmup 20 --no-cpu --sparse-steps 0 > gpurun_out/prof_fetch.log 2>&1
+timeout -s KILL 120 rocprofv3 --pmc WRITE_SIZE -d $R/gpurun_out/prof_write -o run --output-format csv -- python3 bench.py --steps 10 --warmup 20 --no-cpu --sparse-steps 0 > gpurun_out/prof_write.log 2>&1
 echo all-done

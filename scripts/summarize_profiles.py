@@ -47,8 +47,8 @@ def main(tag):
     if os.path.exists(bp):
         bench = open(bp).read().strip()
     with open(os.path.join(PROF, f"{tag}_summary.md"), "w") as f:
-        f.write(f"# {tag}: rocprofv3 summary (MI355X, config 2 bench, 20 timed steps)\n\n")
-        f.write("Command: `rocprofv3 --kernel-trace --stats -- python3 bench.py --steps 20 --warmup 3 "
+        f.write(f"# {tag}: rocprofv3 summary (MI355X, config 2 bench, 200 timed steps)\n\n")
+        f.write("Command: `rocprofv3 --kernel-trace --stats -- python3 bench.py --steps 200 --warmup 100 "
                 "--no-cpu --sparse-steps 0`; counters: separate `--pmc FETCH_SIZE` and `--pmc WRITE_SIZE` passes.\n\n")
         f.write("| kernel | calls | avg µs | min µs | max µs | % time |\n|---|---|---|---|---|---|\n")
         for r in rows:
@@ -67,7 +67,7 @@ def main(tag):
         shutil.copy(sp, os.path.join(PROF, f"{tag}_sparse_kernel_stats.csv"))
         with open(os.path.join(PROF, f"{tag}_summary.md"), "a") as f:
             f.write("\n## Sparse leg (config 3), `rocprofv3 --kernel-trace --stats -- python3 bench.py --steps 2 "
-                    "--warmup 1 --no-cpu --sparse-steps 5`\n\n| kernel | calls | avg µs | % time |\n|---|---|---|---|\n")
+                    "--warmup 1 --no-cpu --sparse-steps 10`\n\n| kernel | calls | avg µs | % time |\n|---|---|---|---|\n")
             for r in csv.DictReader(open(sp)):
                 f.write(f"| `{r['Name'][:90]}` | {r['Calls']} | {float(r['AverageNs'])/1e3:.1f} | "
                         f"{float(r['Percentage']):.1f} |\n")
