@@ -106,7 +106,9 @@ hipError_t launch_reduce(int vtype, int mode, void* shard, int64_t rows, int32_t
 hipError_t launch_rollback_i32(int32_t* shard, int64_t rows, int32_t cols, const Batch& bt, int nb,
                                int64_t stride, int K, const int32_t* slot, const uint32_t* rowflag, Ctrl* ctrl,
                                uint64_t tail_cut, hipStream_t st);
-hipError_t launch_maxdelta_finalize(const DeltaCand* cand, int64_t n, MaxDelta* md, const Batch& bt, int nb,
+// `cand` holds n candidates plus kMdParts entries of scratch after them.
+constexpr int kMdParts = 256;
+hipError_t launch_maxdelta_finalize(DeltaCand* cand, int64_t n, MaxDelta* md, const Batch& bt, int nb,
                                     int64_t stride, int K, int V, hipStream_t st);
 hipError_t launch_array_validate(const Batch& bt, int nb, int64_t max_nrec, int64_t stride,
                                  int K, int64_t first, int64_t rows, Ctrl* ctrl, uint64_t tail_cut, hipStream_t st);

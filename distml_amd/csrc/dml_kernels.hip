@@ -176,6 +176,38 @@ hipError_t launch_index(const Batch& bt, int nb, int64_t max_nrec, int64_t strid
 }
 
 // ---------------------------------------------------------------------------
+// AdaGrad maxDelta candidates: (valid, value, position), best = largest value,
+// then smallest position (the first in the reference's order). Associative, so
+// a block reduces them as a butterfly inside each wave, then across its waves
+// through LDS; the result lands in thread 0. Every thread of the block calls it.
+__device__ inline bool cand_better(bool ok, float v, uint64_t p, bool ok2, float v2, uint64_t p2) {
+    return ok && (!ok2 || v > v2 || (v == v2 && p < p2));
+}
+template <int WPB>
+__device__ inline void cand_block_best(bool& ok, float& v, uint64_t& p) {
+#pragma unroll
+    for (int m = 32; m > 0; m >>= 1) {
+        const float ov = __shfl_xor(v, m);
+        const uint32_t olo = (uint32_t)__shfl_xor((int)(uint32_t)p, m);
+        const uint32_t ohi = (uint32_t)__shfl_xor((int)(uint32_t)(p >> 32), m);
+        const bool ook = __shfl_xor((int)ok, m) != 0;
+        const uint64_t op = (uint64_t)olo | ((uint64_t)ohi << 32);
+        if (cand_better(ook, ov, op, ok, v, p)) { ok = true; v = ov; p = op; }
+    }
+    if constexpr (WPB > 1) {
+        __shared__ float sv[WPB];
+        __shared__ uint64_t sp[WPB];
+        __shared__ int sok[WPB];
+        const int w = threadIdx.x >> 6;
+        if ((threadIdx.x & 63) == 0) { sv[w] = v; sp[w] = p; sok[w] = ok; }
+        __syncthreads();
+        if (threadIdx.x == 0)
+            for (int i = 1; i < WPB; ++i)
+                if (cand_better(sok[i] != 0, sv[i], sp[i], ok, v, p)) { ok = true; v = sv[i]; p = sp[i]; }
+    }
+}
+
+// ---------------------------------------------------------------------------
 // k_reduce: one wave per (shard row, CPW consecutive 64*VEC-column chunks); a
 // block = WPB waves. The wave reads the row's slots (wave-uniform scalar loads),
 // keeps its row chunks in registers, adds every push's values in push order
@@ -248,7 +280,10 @@ __global__ __launch_bounds__(64 * WPB) void k_reduce(T* __restrict__ shard, int6
         const int32_t* srow = slot + row * kMaxW;
 
         T acc[CPW][VEC];
-        float dl[CPW][VEC], al[CPW][VEC];
+        // AdaGrad: delta; the delta after the last push that left it above 1 (0 =
+        // none); the last strict rise of delta (value, batch position).
+        float dl[CPW][VEC], lg[CPW][VEC], rv[CPW][VEC];
+        uint64_t rp[CPW][VEC];
         bool touched = false;
         bool negf = false;
         uint64_t negpos = kNoPos;
@@ -272,7 +307,9 @@ __global__ __launch_bounds__(64 * WPB) void k_reduce(T* __restrict__ shard, int6
 #pragma unroll
                     for (int e = 0; e < VEC; ++e) {
                         dl[c][e] = e < nv[c] ? ada.delta[ei + e] : 0.f;
-                        al[c][e] = e < nv[c] ? ada.alpha[ei + e] : 0.f;
+                        lg[c][e] = 0.f;
+                        rv[c][e] = 0.f;
+                        rp[c][e] = kNoPos;
                     }
                 }
             }
@@ -288,20 +325,17 @@ __global__ __launch_bounds__(64 * WPB) void k_reduce(T* __restrict__ shard, int6
                     if (!negf && acc[c][e] < 0) { negf = true; negpos = p; }
                 }
                 if constexpr (MODE == kAdaGrad) {
-                    // FloatMatrixStoreAdaGrad.java:265-277
+                    // FloatMatrixStoreAdaGrad.java:265-277. Every push whose delta ends
+                    // above 1 overwrites alpha with f(delta), others leave it: the alpha
+                    // the batch leaves is f(the last such delta), computed once at
+                    // write-back instead of a double sqrt + divide per push. delta never
+                    // falls (u*u >= 0; NaN never rises), so the last strict rise is the
+                    // element's maxDelta candidate.
                     const float uu = __fmul_rn((float)u, (float)u);
                     const float nd = __fadd_rn(dl[c][e], uu);
-                    if (nd > dl[c][e]) {  // delta rose: candidate for maxDelta (NaN never rises)
-                        if (!cand_ok || nd > cand_v || (nd == cand_v && p < cand_p)) {
-                            cand_ok = true; cand_v = nd; cand_p = p;
-                        }
-                    }
+                    if (nd > dl[c][e]) { rv[c][e] = nd; rp[c][e] = p; }
+                    if (nd > 1.0f) lg[c][e] = nd;
                     dl[c][e] = nd;
-                    if ((double)nd > 1.0) {
-                        float a = (float)((double)ada.initial_alpha / ((double)ada.factor * sqrt((double)nd)));
-                        if (a < ada.min_alpha) a = ada.min_alpha;
-                        al[c][e] = a;
-                    }
                 }
             }
         };
@@ -413,7 +447,20 @@ __global__ __launch_bounds__(64 * WPB) void k_reduce(T* __restrict__ shard, int6
                 }
                 if constexpr (MODE == kAdaGrad) {
                     const int64_t ei = row * (int64_t)cols + c0[c];
-                    for (int e = 0; e < nv[c]; ++e) { ada.delta[ei + e] = dl[c][e]; ada.alpha[ei + e] = al[c][e]; }
+#pragma unroll
+                    for (int e = 0; e < VEC; ++e) {
+                        if (e >= nv[c]) continue;
+                        ada.delta[ei + e] = dl[c][e];
+                        if (lg[c][e] > 1.0f) {
+                            float a = (float)((double)ada.initial_alpha / ((double)ada.factor * sqrt((double)lg[c][e])));
+                            if (a < ada.min_alpha) a = ada.min_alpha;
+                            ada.alpha[ei + e] = a;
+                        }
+                        if (rp[c][e] != kNoPos &&
+                            (!cand_ok || rv[c][e] > cand_v || (rv[c][e] == cand_v && rp[c][e] < cand_p))) {
+                            cand_ok = true; cand_v = rv[c][e]; cand_p = rp[c][e];
+                        }
+                    }
                 }
             }
         }
@@ -421,26 +468,10 @@ __global__ __launch_bounds__(64 * WPB) void k_reduce(T* __restrict__ shard, int6
     } while (0);
 
     if constexpr (MODE == kAdaGrad) {
-        // Block-wide best candidate: max value, then min position.
-        static_assert(WPB == 4, "AdaGrad reduction assumes 256-thread blocks");
-        __shared__ float sv[256];
-        __shared__ unsigned long long sp[256];
-        __shared__ int sok[256];
-        sv[threadIdx.x] = cand_v; sp[threadIdx.x] = cand_p; sok[threadIdx.x] = cand_ok;
-        __syncthreads();
-        for (int s = 128; s > 0; s >>= 1) {
-            if ((int)threadIdx.x < s) {
-                const int o = threadIdx.x + s;
-                if (sok[o] && (!sok[threadIdx.x] || sv[o] > sv[threadIdx.x] ||
-                               (sv[o] == sv[threadIdx.x] && sp[o] < sp[threadIdx.x]))) {
-                    sv[threadIdx.x] = sv[o]; sp[threadIdx.x] = sp[o]; sok[threadIdx.x] = 1;
-                }
-            }
-            __syncthreads();
-        }
+        cand_block_best<WPB>(cand_ok, cand_v, cand_p);
         if (threadIdx.x == 0) {
             DeltaCand c;
-            c.value = sv[0]; c.valid = sok[0]; c.pos = sp[0];
+            c.value = cand_v; c.valid = cand_ok; c.pos = cand_p;
             ada.cand[blockIdx.x] = c;
         }
     }
@@ -646,6 +677,98 @@ __global__ __launch_bounds__(64 * WPB) void k_reduce_rows(T* __restrict__ shard,
             consume(rb2, hb, rrb2, b + 1);
             issue(b + 3, rb2, hb, rrb2);
         }
+    } else if constexpr (DEPTH == 3) {
+        // Pair-packed: the wave's (push, row) records in push order, RPW of them per
+        // load group whatever push they come from. A batch whose pushes list few of
+        // these rows (LDA's and Word2Vec's touched-row pushes) keeps RPW x CPW loads in
+        // flight instead of one push's mostly absent rows; full pushes give exactly
+        // the push-major groups. Per row the adds stay in push order.
+        uint64_t pm[RPW];
+#pragma unroll
+        for (int r = 0; r < RPW; ++r) pm[r] = __ballot(lane < nb && vslot[r] >= 0);  // wave-uniform
+        for (;;) {
+            int pb[RPW], pr[RPW];
+            int np = 0;
+#pragma unroll
+            for (int g = 0; g < RPW; ++g) {
+                int bmin = 64, rsel = 0;  // the lowest push any row still holds, its first row
+#pragma unroll
+                for (int r = 0; r < RPW; ++r) {
+                    const int tz = pm[r] ? (int)__builtin_ctzll(pm[r]) : 64;
+                    if (tz < bmin) { bmin = tz; rsel = r; }
+                }
+                pb[g] = bmin;
+                pr[g] = rsel;
+                if (bmin < 64) {
+#pragma unroll
+                    for (int r = 0; r < RPW; ++r)
+                        if (r == rsel) pm[r] &= pm[r] - 1;  // bmin is its lowest set bit
+                    ++np;
+                }
+            }
+            if (np == 0) break;
+            u32x4 raw[RPW][CPW];
+            int32_t prr[RPW];
+#pragma unroll
+            for (int g = 0; g < RPW; ++g) {
+                const int b = pb[g] < 64 ? pb[g] : 0;
+                int32_t vs = vslot[0];
+#pragma unroll
+                for (int r = 1; r < RPW; ++r) vs = pr[g] == r ? vslot[r] : vs;
+                const int32_t rr = pb[g] < 64 ? __builtin_amdgcn_readlane(vs, b) : -1;
+                prr[g] = rr;
+                const uint8_t* bp =
+                    (const uint8_t*)(((uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)vbase, b)) |
+                                     ((uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)(vbase >> 32), b) << 32));
+                if constexpr (FULL) {
+                    const uint8_t* rb = rr >= 0 ? bp + (int64_t)rr * stride + voff[0] : fbv;
+#pragma unroll
+                    for (int c = 0; c < CPW; ++c) {
+                        const uint8_t* src = rb + c * 64 * VEC * (int)sizeof(T);
+                        raw[g][c] = NT ? ldg16_nt(src) : ldg16(src);
+                    }
+                } else {
+#pragma unroll
+                    for (int c = 0; c < CPW; ++c) {
+                        const uint8_t* src =
+                            (rr >= 0 && nv[c] > 0) ? bp + (int64_t)rr * stride + voff[c] - shb[c] : fb;
+                        raw[g][c] = NT ? ldg16_nt(src) : ldg16(src);
+                    }
+                }
+            }
+#pragma unroll
+            for (int g = 0; g < RPW; ++g) {
+                if (pb[g] >= 64) continue;  // wave-uniform
+                touched |= 1u << pr[g];
+#pragma unroll
+                for (int r = 0; r < RPW; ++r) {
+                    if (r != pr[g]) continue;  // wave-uniform: static register indices below
+#pragma unroll
+                    for (int c = 0; c < CPW; ++c) {
+                        T t[VEC], u[VEC];
+                        unpack<T>(raw[g][c], t);
+#pragma unroll
+                        for (int e = 0; e < VEC; ++e) {
+                            u[e] = t[e];
+#pragma unroll
+                            for (int k = 1; k < VEC - e; ++k) u[e] = sh[c] == k ? t[e + k] : u[e];
+                        }
+#pragma unroll
+                        for (int e = 0; e < VEC; ++e)
+                            if (e < nv[c]) {
+                                acc[r][c][e] = Elem<T>::add(acc[r][c][e], u[e]);
+                                if constexpr (MODE == kAddCheckI32)
+                                    if (acc[r][c][e] < 0) {
+                                        const uint64_t p = pos_of((uint64_t)bt.bidx[pb[g]],
+                                                                  (uint64_t)((int64_t)prr[g] * stride + voff[c] +
+                                                                             e * (int64_t)sizeof(T)));
+                                        if (p < negpos) negpos = p;
+                                    }
+                            }
+                    }
+                }
+            }
+        }
     } else
 #pragma unroll 1
     for (int b = 0; b < nb; ++b) {
@@ -765,12 +888,12 @@ static hipError_t launch_reduce_t(void* shard, int64_t rows, int32_t cols, const
     if constexpr (RPW > 1) {
         static_assert(MODE != kAdaGrad && MODE != kRollbackI32, "k_reduce_rows shapes");
         if (ev.start || ev.stop)
-            hipExtLaunchKernelGGL((k_reduce_rows<T, MODE, CPW, RPW, NT, FULL, (FULL && G == 2) ? 2 : 1, WPB, SNT>), dim3((unsigned)nblocks), dim3(64 * WPB),
-                                  occ_lds, st, ev.start, ev.stop, 0, (T*)shard, rows, cols, ngroups, bt, nb, stride,
+            hipExtLaunchKernelGGL((k_reduce_rows<T, MODE, CPW, RPW, NT, FULL, G == 3 ? 3 : (FULL && G == 2) ? 2 : 1, WPB, SNT>), dim3((unsigned)nblocks),
+                                  dim3(64 * WPB), occ_lds, st, ev.start, ev.stop, 0, (T*)shard, rows, cols, ngroups, bt, nb, stride,
                                   K, const_cast<int32_t*>(slot), rowflag, ctrl, tail_cut, rm);
         else
-            hipLaunchKernelGGL((k_reduce_rows<T, MODE, CPW, RPW, NT, FULL, (FULL && G == 2) ? 2 : 1, WPB, SNT>), dim3((unsigned)nblocks), dim3(64 * WPB),
-                               occ_lds, st, (T*)shard, rows, cols, ngroups, bt, nb, stride, K, const_cast<int32_t*>(slot), rowflag,
+            hipLaunchKernelGGL((k_reduce_rows<T, MODE, CPW, RPW, NT, FULL, G == 3 ? 3 : (FULL && G == 2) ? 2 : 1, WPB, SNT>), dim3((unsigned)nblocks),
+                               dim3(64 * WPB), occ_lds, st, (T*)shard, rows, cols, ngroups, bt, nb, stride, K, const_cast<int32_t*>(slot), rowflag,
                                ctrl, tail_cut, rm);
     } else {
         if (ev.start || ev.stop)
@@ -818,15 +941,19 @@ static hipError_t launch_auto(void* shard, int64_t rows, int32_t cols, const Bat
         return DML_L(8, 1, 1);
     } else {
         if (cols < VEC) return DML_L(16, 1, 1);  // narrower than one vector: k_reduce's generic path
+        // pair-packed load groups (k_reduce_rows DEPTH 3) unless DML_PAIRS=0 (A/B)
+        static const bool pairs = !(getenv("DML_PAIRS") && atoi(getenv("DML_PAIRS")) == 0);
         // whole 4-KiB rows: two rows per wave and at most 8 waves per CU (64 KiB of
         // loads in flight per CU) measured 3.5-5 % faster than 4 rows per wave at the
         // register-limited 12-24 waves (scripts/exp_variants.py)
         if (cols % (64 * VEC * 4) == 0) return DML_LF(1, 4, 2, 2);
-        if (nchunks >= 4) return DML_L(1, 4, 4);
+        static const int nf_rpw = getenv("DML_NF_RPW") ? atoi(getenv("DML_NF_RPW")) : 4;  // A/B knob
+        if (nchunks >= 4 && nf_rpw == 2) return DML_L(3, 4, 2);
+        if (nchunks >= 4) return pairs ? DML_L(3, 4, 4) : DML_L(1, 4, 4);
         if (cols % (64 * VEC * 2) == 0) return DML_LF(1, 2, 4, 0);
-        if (nchunks >= 2) return DML_L(1, 2, 4);
+        if (nchunks >= 2) return pairs ? DML_L(3, 2, 4) : DML_L(1, 2, 4);
         if (cols % (64 * VEC) == 0) return DML_LF(1, 1, 4, 0);
-        return DML_L(1, 1, 4);
+        return pairs ? DML_L(3, 1, 4) : DML_L(1, 1, 4);
     }
 #undef DML_L
 #undef DML_LF
@@ -874,6 +1001,7 @@ hipError_t launch_reduce(int vtype, int mode, void* shard, int64_t rows, int32_t
                 case 34: return launch_reduce_t<float, kAdd, 1, true, 4, true, 4, 2, true>(shard, rows, cols, bt, nb, stride, K, slot, rowflag, ctrl, tail_cut, ada, st, nblocks_out, ev, {}, 2);
                 case 35: return launch_reduce_t<float, kAdd, 1, true, 1, false, 4, 2, true>(shard, rows, cols, bt, nb, stride, K, slot, rowflag, ctrl, tail_cut, ada, st, nblocks_out, ev, {}, 8);
                 case 37: return launch_reduce_t<float, kAdd, 1, true, 4, 2, 4, 2, true>(shard, rows, cols, bt, nb, stride, K, slot, rowflag, ctrl, tail_cut, ada, st, nblocks_out, ev, {}, 2);
+                case 38: return launch_reduce_t<float, kAdd, 3, true, 4, 0, 4, 2, true>(shard, rows, cols, bt, nb, stride, K, slot, rowflag, ctrl, tail_cut, ada, st, nblocks_out, ev, {}, 2);
                 case 36: return launch_reduce_t<float, kAdd, 1, true, 4, false, 4, 1 + 1, true>(shard, rows, cols, bt, nb, stride, K, slot, rowflag, ctrl, tail_cut, ada, st, nblocks_out, ev, {}, 2);
                 case 29: return launch_reduce_t<float, kAdd, 1, true, 4, false, 4, 4, true>(shard, rows, cols, bt, nb, stride, K, slot, rowflag, ctrl, tail_cut, ada, st, nblocks_out, ev);
                 default: return DML_A(float, kAdd);
@@ -903,48 +1031,61 @@ hipError_t launch_rollback_i32(int32_t* shard, int64_t rows, int32_t cols, const
 }
 
 // ---------------------------------------------------------------------------
-// maxDelta finalize: reduce the per-block candidates and apply the reference's
-// strict `deltas[i] > maxDelta` update (FloatMatrixStoreAdaGrad.java:273-277).
+// maxDelta finalize: reduce the per-block candidates in two launches (kMdParts
+// blocks over strided slices -> cand[n .. n + kMdParts), then one block) and
+// apply the reference's strict `deltas[i] > maxDelta` update
+// (FloatMatrixStoreAdaGrad.java:273-277). One block over 10^5+ candidates was
+// bound by a single CU's load rate.
+__device__ inline void cand_scan(const DeltaCand* __restrict__ cand, int64_t i, int64_t n, int64_t step, bool& ok,
+                                 float& v, uint64_t& p) {
+    for (; i < n; i += step) {
+        const DeltaCand c = cand[i];
+        if (cand_better(c.valid != 0, c.value, c.pos, ok, v, p)) { ok = true; v = c.value; p = c.pos; }
+    }
+}
+
+__global__ __launch_bounds__(256) void k_maxdelta_part(DeltaCand* __restrict__ cand, int64_t n) {
+    bool ok = false;
+    float v = 0.f;
+    uint64_t p = kNoPos;
+    cand_scan(cand, (int64_t)blockIdx.x * 256 + threadIdx.x, n, (int64_t)gridDim.x * 256, ok, v, p);
+    cand_block_best<4>(ok, v, p);
+    if (threadIdx.x == 0) {
+        DeltaCand c;
+        c.value = v; c.valid = ok; c.pos = p;
+        cand[n + blockIdx.x] = c;
+    }
+}
+
 __global__ __launch_bounds__(256) void k_maxdelta(const DeltaCand* __restrict__ cand, int64_t n,
                                                   MaxDelta* __restrict__ md, const Batch bt, int nb,
                                                   int64_t stride, int K, int V) {
-    __shared__ float sv[256];
-    __shared__ unsigned long long sp[256];
-    __shared__ int sok[256];
+    bool ok = false;
     float v = 0.f;
-    unsigned long long p = kNoPos;
-    int ok = 0;
-    for (int64_t i = threadIdx.x; i < n; i += 256) {
-        const DeltaCand c = cand[i];
-        if (c.valid && (!ok || c.value > v || (c.value == v && c.pos < p))) { ok = 1; v = c.value; p = c.pos; }
-    }
-    sv[threadIdx.x] = v; sp[threadIdx.x] = p; sok[threadIdx.x] = ok;
-    __syncthreads();
-    for (int s = 128; s > 0; s >>= 1) {
-        if ((int)threadIdx.x < s) {
-            const int o = threadIdx.x + s;
-            if (sok[o] && (!sok[threadIdx.x] || sv[o] > sv[threadIdx.x] ||
-                           (sv[o] == sv[threadIdx.x] && sp[o] < sp[threadIdx.x]))) {
-                sv[threadIdx.x] = sv[o]; sp[threadIdx.x] = sp[o]; sok[threadIdx.x] = 1;
-            }
-        }
-        __syncthreads();
-    }
-    if (threadIdx.x == 0 && sok[0] && sv[0] > md->value) {
-        const int gb = (int)(sp[0] >> 40);
+    uint64_t p = kNoPos;
+    cand_scan(cand, threadIdx.x, n, 256, ok, v, p);
+    cand_block_best<4>(ok, v, p);
+    if (threadIdx.x == 0 && ok && v > md->value) {
+        const int gb = (int)(p >> 40);
         int b = 0;
         while (b < nb - 1 && bt.bidx[b] != gb) ++b;
-        const int64_t off = (int64_t)(sp[0] & kOffMask);
+        const int64_t off = (int64_t)(p & kOffMask);
         const int64_t r = off / stride;
-        md->value = sv[0];
+        md->value = v;
         md->row = (int32_t)ld_key(bt.base[b] + r * stride, K);  // maxDeltaRow = (int)key
         md->col = (int32_t)((off - r * stride - K) / V);
     }
 }
 
-hipError_t launch_maxdelta_finalize(const DeltaCand* cand, int64_t n, MaxDelta* md, const Batch& bt, int nb,
+hipError_t launch_maxdelta_finalize(DeltaCand* cand, int64_t n, MaxDelta* md, const Batch& bt, int nb,
                                     int64_t stride, int K, int V, hipStream_t st) {
-    hipLaunchKernelGGL(k_maxdelta, dim3(1), dim3(256), 0, st, cand, n, md, bt, nb, stride, K, V);
+    if (n > 4 * 256 * kMdParts) {
+        hipLaunchKernelGGL(k_maxdelta_part, dim3(kMdParts), dim3(256), 0, st, cand, n);
+        hipLaunchKernelGGL(k_maxdelta, dim3(1), dim3(256), 0, st, cand + n, (int64_t)kMdParts, md, bt, nb, stride, K,
+                           V);
+    } else {
+        hipLaunchKernelGGL(k_maxdelta, dim3(1), dim3(256), 0, st, cand, n, md, bt, nb, stride, K, V);
+    }
     return hipGetLastError();
 }
 

@@ -762,7 +762,7 @@ int dml_store_create_range(const dml_desc* desc, int64_t first_key, int64_t last
         if ((e = hipMemsetAsync(s->alpha, 0, n * 4, s->stream)) != hipSuccess) return fail(e, "alpha zero");
         if ((e = hipMemsetAsync(s->delta, 0, n * 4, s->stream)) != hipSuccess) return fail(e, "delta zero");
         s->cand_n = reduce_blocks(d.value_type, rows, s->cols);
-        if ((e = hipMalloc((void**)&s->cand, sizeof(DeltaCand) * (size_t)std::max<int64_t>(s->cand_n, 1))) != hipSuccess)
+        if ((e = hipMalloc((void**)&s->cand, sizeof(DeltaCand) * (size_t)(s->cand_n + kMdParts))) != hipSuccess)
             return fail(e, "cand alloc");
         if ((e = hipMalloc((void**)&s->md, sizeof(MaxDelta))) != hipSuccess) return fail(e, "md alloc");
         if ((e = hipMemsetAsync(s->md, 0, sizeof(MaxDelta), s->stream)) != hipSuccess) return fail(e, "md zero");
