@@ -304,9 +304,14 @@ __global__ __launch_bounds__(64 * WPB) void k_reduce(T* __restrict__ shard, int6
                 }
                 if constexpr (MODE == kAdaGrad) {
                     const int64_t ei = row * (int64_t)cols + c0[c];
+                    if (nv[c] == VEC) {
+                        const u32x4 t = SNT ? ldg16_nt((const uint8_t*)(ada.delta + ei))
+                                            : ldg16((const uint8_t*)(ada.delta + ei));
+                        unpack<float>(t, dl[c]);
+                    }
 #pragma unroll
                     for (int e = 0; e < VEC; ++e) {
-                        dl[c][e] = e < nv[c] ? ada.delta[ei + e] : 0.f;
+                        if (nv[c] != VEC) dl[c][e] = e < nv[c] ? ada.delta[ei + e] : 0.f;
                         lg[c][e] = 0.f;
                         rv[c][e] = 0.f;
                         rp[c][e] = kNoPos;
@@ -428,6 +433,14 @@ __global__ __launch_bounds__(64 * WPB) void k_reduce(T* __restrict__ shard, int6
             }
         }
 
+        if constexpr (MODE == kAdaGrad) {
+            // Hand the slot table back clean (reduce_clears_slots): with one chunk group
+            // per row this wave is the row's only reader and its slot reads are done.
+            if (ngroups == 1) {
+                const int nact = (cols + VEC - 1) / VEC < 64 ? (cols + VEC - 1) / VEC : 64;  // live lanes
+                for (int j = lane; j < nb; j += nact) const_cast<int32_t*>(slot)[row * kMaxW + j] = -1;
+            }
+        }
         if (MODE == kPreReduce && !touched) {
 #pragma unroll
             for (int c = 0; c < CPW; ++c)
@@ -447,15 +460,31 @@ __global__ __launch_bounds__(64 * WPB) void k_reduce(T* __restrict__ shard, int6
                 }
                 if constexpr (MODE == kAdaGrad) {
                     const int64_t ei = row * (int64_t)cols + c0[c];
+                    float na[VEC];
+                    bool all_a = nv[c] == VEC;
+#pragma unroll
+                    for (int e = 0; e < VEC; ++e) {
+                        na[e] = 0.f;
+                        if (e < nv[c] && lg[c][e] > 1.0f) {
+                            na[e] = (float)((double)ada.initial_alpha / ((double)ada.factor * sqrt((double)lg[c][e])));
+                            if (na[e] < ada.min_alpha) na[e] = ada.min_alpha;
+                        } else {
+                            all_a = false;
+                        }
+                    }
+                    if (nv[c] == VEC) {
+                        if (SNT) stg16_nt(ada.delta + ei, pack<float>(dl[c]));
+                        else stg16(ada.delta + ei, pack<float>(dl[c]));
+                    }
+                    if (all_a) {  // every element's alpha changed: one 16-B store
+                        if (SNT) stg16_nt(ada.alpha + ei, pack<float>(na));
+                        else stg16(ada.alpha + ei, pack<float>(na));
+                    }
 #pragma unroll
                     for (int e = 0; e < VEC; ++e) {
                         if (e >= nv[c]) continue;
-                        ada.delta[ei + e] = dl[c][e];
-                        if (lg[c][e] > 1.0f) {
-                            float a = (float)((double)ada.initial_alpha / ((double)ada.factor * sqrt((double)lg[c][e])));
-                            if (a < ada.min_alpha) a = ada.min_alpha;
-                            ada.alpha[ei + e] = a;
-                        }
+                        if (nv[c] != VEC) ada.delta[ei + e] = dl[c][e];
+                        if (!all_a && lg[c][e] > 1.0f) ada.alpha[ei + e] = na[e];
                         if (rp[c][e] != kNoPos &&
                             (!cand_ok || rv[c][e] > cand_v || (rv[c][e] == cand_v && rp[c][e] < cand_p))) {
                             cand_ok = true; cand_v = rv[c][e]; cand_p = rp[c][e];
@@ -937,7 +966,25 @@ static hipError_t launch_auto(void* shard, int64_t rows, int32_t cols, const Bat
                                                      slot, rowflag, ctrl, tail_cut, ada, st, nblocks_out, ev, rm)
 #define DML_LF(G, CPW, RPW, BPC) launch_reduce_t<T, MODE, G, true, 4, false, CPW, RPW, true>(shard, rows, cols, bt, nb, \
                                                      stride, K, slot, rowflag, ctrl, tail_cut, ada, st, nblocks_out, ev, rm, BPC)
-    if constexpr (MODE == kAdaGrad || MODE == kRollbackI32) {
+    if constexpr (MODE == kAdaGrad) {
+        // default G8 with nt shard / delta / alpha traffic (measured best).
+        // DML_ADA_VARIANT (A/B, read once): 1 G4 cached, 2 G16 cached, 3 G8 nt, 4 plain loads,
+        // 5 WPB 8 cached, 7 G8 cached (the previous default), 8 G4 nt, 9 G16 nt, 10 G8 nt WPB 8
+        // (the candidate buffer holds one entry per 4-wave block: no WPB below 4)
+        static const int av = getenv("DML_ADA_VARIANT") ? atoi(getenv("DML_ADA_VARIANT")) : 0;
+        switch (av) {
+            case 1: return DML_L(4, 1, 1);
+            case 2: return DML_L(16, 1, 1);
+            case 3: return launch_reduce_t<T, MODE, 8, true, 4, true, 1, 1>(shard, rows, cols, bt, nb, stride, K, slot, rowflag, ctrl, tail_cut, ada, st, nblocks_out, ev, rm);
+            case 4: return launch_reduce_t<T, MODE, 8, false, 4, false, 1, 1>(shard, rows, cols, bt, nb, stride, K, slot, rowflag, ctrl, tail_cut, ada, st, nblocks_out, ev, rm);
+            case 5: return launch_reduce_t<T, MODE, 8, true, 8, false, 1, 1>(shard, rows, cols, bt, nb, stride, K, slot, rowflag, ctrl, tail_cut, ada, st, nblocks_out, ev, rm);
+            case 7: return DML_L(8, 1, 1);
+            case 8: return launch_reduce_t<T, MODE, 4, true, 4, true, 1, 1>(shard, rows, cols, bt, nb, stride, K, slot, rowflag, ctrl, tail_cut, ada, st, nblocks_out, ev, rm);
+            case 9: return launch_reduce_t<T, MODE, 16, true, 4, true, 1, 1>(shard, rows, cols, bt, nb, stride, K, slot, rowflag, ctrl, tail_cut, ada, st, nblocks_out, ev, rm);
+            case 10: return launch_reduce_t<T, MODE, 8, true, 8, true, 1, 1>(shard, rows, cols, bt, nb, stride, K, slot, rowflag, ctrl, tail_cut, ada, st, nblocks_out, ev, rm);
+            default: return launch_reduce_t<T, MODE, 8, true, 4, true, 1, 1>(shard, rows, cols, bt, nb, stride, K, slot, rowflag, ctrl, tail_cut, ada, st, nblocks_out, ev, rm);
+        }
+    } else if constexpr (MODE == kRollbackI32) {
         return DML_L(8, 1, 1);
     } else {
         if (cols < VEC) return DML_L(16, 1, 1);  // narrower than one vector: k_reduce's generic path
@@ -960,6 +1007,7 @@ static hipError_t launch_auto(void* shard, int64_t rows, int32_t cols, const Bat
 }
 
 bool reduce_clears_slots(int vtype, int mode, int32_t cols) {
+    if (mode == kAdaGrad) return vtype == kF32 && cols <= 64 * 4;  // k_reduce, one chunk group per row
     if (mode != kAdd && mode != kPreReduce) return false;
     const int VEC = vtype == kF64 ? 2 : 4;
     if (cols < VEC) return false;  // k_reduce's generic path

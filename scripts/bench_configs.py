@@ -126,13 +126,13 @@ def main():
         perms = [(coprime((4000 + b) * 2654435761 % rows | 1, rows), b * 331 % rows) for b in range(W)]
         print(json.dumps(run("config5 LDA IntMatrixStore shard 125000x1000 int32, 32 pushes x 8192 rows",
                              DataDesc(1, 0, 0), rows, cols, nrec, W, [4000 + b for b in range(W)], perms, 11,
-                             steps=20, cpu_budget_s=8.0)), flush=True)
+                             steps=20, cpu_budget_s=float(os.environ.get("CFG_CPU_S", "8.0")))), flush=True)
     if "4" in which:
         rows, cols, W = 1_250_000, 200, 8
         perms = [(coprime((3000 + b) * 2654435761 % rows | 1, rows), b * 7919 % rows) for b in range(W)]
         print(json.dumps(run("config4 Word2Vec FloatMatrixStoreAdaGrad shard 1250000x200 fp32, 8 full-range pushes",
                              DataDesc(1, 0, 1, False, True, True), rows, cols, rows, W,
-                             [3000 + b for b in range(W)], perms, 13, steps=5, cpu_budget_s=8.0,
+                             [3000 + b for b in range(W)], perms, 13, steps=5, cpu_budget_s=float(os.environ.get("CFG_CPU_S", "8.0")),
                              ada=(0.025, 0.0001, 1.0))), flush=True)
 
 
