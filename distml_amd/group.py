@@ -62,6 +62,17 @@ class HipOps:
     def stream_wait(self, h, stream: int) -> None:
         check(_lib.load().dml_prereduce_stream_wait(C.c_void_p(h), C.c_void_p(stream)))
 
+    def split(self, fmt: DataDesc, cols: int, total_rows: int, world: int, dev_ptrs: Sequence[int],
+              lens: Sequence[int], out_ptr: int, out_cap: int, stream: int) -> List[List[int]]:
+        """dml_shard_split: counts[b][d] records of push b for shard d, written dest-major to out."""
+        n = len(dev_ptrs)
+        ptrs = (C.c_void_p * max(n, 1))(*dev_ptrs)
+        ls = (C.c_int64 * max(n, 1))(*lens)
+        cnt = (C.c_int64 * max(n * world, 1))()
+        check(_lib.load().dml_shard_split(C.byref(fmt.to_c()), cols, total_rows, world, ptrs, ls, n,
+                                          C.c_void_p(out_ptr), out_cap, cnt, C.c_void_p(stream)))
+        return [[cnt[b * world + d] for d in range(world)] for b in range(n)]
+
 
 class ShardGroup:
     def __init__(self, fmt: DataDesc, total_rows: int, cols: int, rank: int, world: int,
@@ -91,6 +102,7 @@ class ShardGroup:
         # (side stream) and pre-reduce overlap call k's reduce-scatter and apply
         self.pieces = pieces
         self._pending: list = []  # pre-reduce handles whose errors are not yet collected
+        self._xbufs: list = []    # exchange receive buffers the store may still read
         self._k = 0
         if self.partial.is_cuda:
             self.comm = torch.cuda.Stream(device=dev)
@@ -182,6 +194,67 @@ class ShardGroup:
         while len(self._pending) > keep:
             self.ops.end(self._pending.pop(0))
 
+    def record_stride(self) -> int:
+        f = self.fmt
+        return f.keySize + (f.valueSize * self.cols if f.dataType == DataDesc.DATA_TYPE_MATRIX else f.valueSize)
+
+    def push_exchange(self, dev_ptrs: Sequence[int], lens: Sequence[int]) -> None:
+        """Bit-exact path for pushes whose sum does not commute with the store's
+        update (AdaGrad, int32 negativity checks) or that hold key subsets: the
+        reference's own data flow. Each local push is split by owner shard
+        (SparseMatrix.push's per-partition split, SparseMatrix.java:46-60;
+        dml_shard_split), the slices go to their owners in one all-to-all (RCCL
+        send/recv over xGMI), and every owner applies its W slices in global push
+        order — rank-major: rank 0's pushes, then rank 1's — through the store's
+        ordered reduce (exact, errors included). Every rank passes the same number
+        of pushes per call; keys outside the matrix are dropped like the client does."""
+        torch, dist = self.torch, self.dist
+        n, world = len(dev_ptrs), self.world
+        stride = self.record_stride()
+        dev = self.partial.device
+        cap = int(sum(lens))
+        send = torch.empty(max(cap, 1), dtype=torch.uint8, device=dev)
+        st = torch.cuda.current_stream(dev).cuda_stream if send.is_cuda else 0
+        counts = self.ops.split(self.fmt, self.cols, self.total_rows, world, list(dev_ptrs), list(lens),
+                                send.data_ptr(), cap, st) if n else []
+        mine = torch.tensor([[counts[b][d] for b in range(n)] for d in range(world)], dtype=torch.int64)
+        theirs = torch.empty_like(mine)  # [source rank][its push b]
+        # gloo has no device all-to-all: host copies (CPU tests, ranks sharing one GPU)
+        host_a2a = world > 1 and (not send.is_cuda or dist.get_backend() == "gloo")
+        if world == 1:
+            theirs.copy_(mine)
+        elif host_a2a:
+            dist.all_to_all_single(theirs.view(-1), mine.view(-1))
+        else:
+            t = theirs.to(dev)
+            dist.all_to_all_single(t.view(-1), mine.to(dev).view(-1))
+            theirs = t.cpu()
+        send_sizes = [int(mine[d].sum()) * stride for d in range(world)]
+        recv_sizes = [int(theirs[q].sum()) * stride for q in range(world)]
+        nsend, nrecv = sum(send_sizes), sum(recv_sizes)
+        recv = torch.empty(max(nrecv, 1), dtype=torch.uint8, device=dev)
+        if world == 1:
+            recv[:nrecv].copy_(send[:nsend])
+        elif host_a2a and send.is_cuda:
+            hr = torch.empty(nrecv, dtype=torch.uint8)
+            dist.all_to_all_single(hr, send[:nsend].cpu(), recv_sizes, send_sizes)
+            recv[:nrecv].copy_(hr)
+        else:
+            dist.all_to_all_single(recv[:nrecv], send[:nsend], recv_sizes, send_sizes)
+        if recv.is_cuda:
+            torch.cuda.current_stream(dev).synchronize()  # the store's streams read recv next
+        ptrs, ls, off = [], [], 0
+        for q in range(world):
+            for b in range(n):
+                ln = int(theirs[q][b]) * stride
+                if ln:
+                    ptrs.append(recv.data_ptr() + off)
+                    ls.append(ln)
+                off += ln
+        if ptrs:
+            self.store.pushDevice(ptrs, ls)
+            self._xbufs.append(recv)  # alive until the store has consumed it (flush)
+
     def push_local(self, dev_ptrs: Sequence[int], lens: Sequence[int]) -> None:
         """Pushes already split to this shard: exact ordered apply, no exchange."""
         self.store.pushDevice(dev_ptrs, lens)
@@ -197,6 +270,7 @@ class ShardGroup:
                 for ev in self._applied:
                     ev.synchronize()
             self.store.flush()
+            self._xbufs.clear()
 
 
 class NativeShardGroup:

@@ -221,6 +221,22 @@ int dml_prereduce_end(dml_prereduce* p);
  * communication stream that reduce-scatters the piece just written. */
 int dml_prereduce_stream_wait(dml_prereduce* p, void* stream);
 
+/* --- per-shard split of device-resident pushes (multi-GPU exchange path) -- */
+
+/* The client-side split of SparseMatrix.push / SparseArray.push
+ * (SparseMatrix.java:46-60): the records of each of the n pushes `dev_bufs[b]`
+ * (lens[b] bytes, whole records of the desc's wire layout; `cols` for matrices)
+ * are partitioned by owner shard under KeyRange(0, total_rows-1).linearSplit(world)
+ * (KeyRange.java:68-80), keeping each push's record order, and written to
+ * `dev_out` dest-major: [dest 0: push 0's records, push 1's, ...][dest 1: ...].
+ * counts[b*world + d] (host, n*world) receives the record count of push b for
+ * dest d. Keys outside [0, total_rows) are dropped (the client's p.contains(k)).
+ * Kernels run on `stream`; the call returns when dev_out is written.
+ * DML_E_CAPACITY when out_cap is smaller than the kept bytes; world <= 64, n <= 64. */
+int dml_shard_split(const dml_desc* desc, int32_t cols, int64_t total_rows, int32_t world,
+                    const void* const* dev_bufs, const int64_t* lens, int32_t n, void* dev_out,
+                    int64_t out_cap, int64_t* counts, void* stream);
+
 /* --- native multi-GPU shard group (RCCL) -------------------------------- *
  * One process per GPU; rank r owns shard r of KeyRange.linearSplit(world)
  * (KeyRange.java:68-80). Full-range device-resident pushes are pre-reduced in

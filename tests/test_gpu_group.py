@@ -114,3 +114,86 @@ def test_shard_group_hip_multiprocess(tmp_path, oracle, world, vt, rows, pieces,
     err_ref = float(np.max(np.abs(o.data.astype(np.float64) - exact) / terms))
     assert err_ours <= 1e-6, (err_ours, err_ref)
     assert err_ours <= err_ref + 2.0 ** -24, (err_ours, err_ref)
+
+
+# ---------------------------------------------------------------- exact exchange path
+XR, XC, XW = 2000, 200, 4
+XADA = (0.025, 0.0001, 1.5)
+
+
+def _xbuckets(vt, rank):
+    from distml_amd import encode_matrix_push
+    out = []
+    for b in range(XW):
+        rng = np.random.default_rng(500 * rank + b)
+        keys = rng.permutation(XR)[: rng.integers(XR // 4, XR)]
+        vals = ((rng.standard_normal((len(keys), XC)) * 0.6).astype(np.float32) if vt == 1
+                else rng.integers(-2, 3, size=(len(keys), XC)).astype(np.int32))
+        out.append(np.frombuffer(encode_matrix_push(keys, vals, 0, vt), np.uint8).copy())
+    return out
+
+
+def _xworker(rank, world, port, vt, out_dir):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    sys.path[:0] = [ROOT, os.path.join(ROOT, "oracle")]
+    import torch
+    import torch.distributed as dist
+
+    from distml_amd.datadesc import DataDesc
+    from distml_amd.group import ShardGroup
+
+    torch.cuda.set_device(0)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    fmt = DataDesc(1, 0, vt, False, True, vt == 1)
+    g = ShardGroup(fmt, XR, XC, rank, world, device=0)
+    sh = g.shard
+    g.store.load_values(_init(vt, XR, XC)[sh.firstKey:sh.lastKey + 1])
+    if vt == 1:
+        g.store.setAlpha(*XADA)
+    bufs = [torch.from_numpy(b).cuda() for b in _xbuckets(vt, rank)]
+    torch.cuda.synchronize()
+    g.push_exchange([b.data_ptr() for b in bufs], [b.numel() for b in bufs])
+    g.flush()
+    np.save(os.path.join(out_dir, f"data{rank}.npy"), g.store.values())
+    if vt == 1:
+        a, d = g.store.adagrad_state()
+        np.save(os.path.join(out_dir, f"alpha{rank}.npy"), a)
+        np.save(os.path.join(out_dir, f"delta{rank}.npy"), d)
+        np.save(os.path.join(out_dir, f"md{rank}.npy"), np.array(g.store.maxDelta(), np.float64))
+    g.store.close()
+    dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world,vt", [(2, 1), (3, 1), (2, 0)])
+def test_exchange_hip_multiprocess(tmp_path, oracle, world, vt):
+    """push_exchange with the real dml_shard_split and HIP stores (ranks share cuda:0,
+    all-to-all over gloo through the host): bit-exact against one oracle store fed
+    every rank's pushes in rank-major order; each shard's maxDelta against an oracle
+    shard fed the same pushes restricted to its keys."""
+    import torch.multiprocessing as mp
+    from distml_amd.datadesc import KeyRange
+    mp.spawn(_xworker, args=(world, _free_port(), vt, str(tmp_path)), nprocs=world, join=True)
+    init = _init(vt, XR, XC)
+    allb = [b for r in range(world) for b in _xbuckets(vt, r)]
+    o = oracle.OracleStore(1, 0, vt, 0, XR - 1, XC, 1, int(vt == 1))
+    if vt == 1:
+        o.set_alpha(*XADA)
+    o.data[:] = init
+    for b in allb:
+        assert o.push(b.tobytes()) == 0
+    got = np.concatenate([np.load(tmp_path / f"data{r}.npy") for r in range(world)]).reshape(XR, XC)
+    assert got.tobytes() == o.data.tobytes()
+    if vt != 1:
+        return
+    for name, ref in (("alpha", o.alpha), ("delta", o.delta)):
+        g = np.concatenate([np.load(tmp_path / f"{name}{r}.npy") for r in range(world)]).reshape(XR, XC)
+        assert g.tobytes() == ref.tobytes()
+    for r, sh in enumerate(KeyRange(0, XR - 1).linearSplit(world)):
+        so = oracle.OracleStore(1, 0, 1, sh.firstKey, sh.lastKey, XC, 1, 1)
+        so.set_alpha(*XADA)
+        so.data[:] = init[sh.firstKey:sh.lastKey + 1]
+        for b in allb:
+            rec = b.reshape(-1, 4 + 4 * XC)
+            k = rec[:, :4].copy().view("<i4").ravel()
+            assert so.push(rec[(k >= sh.firstKey) & (k <= sh.lastKey)].tobytes()) == 0
+        assert tuple(np.load(tmp_path / f"md{r}.npy").tolist()) == tuple(float(x) for x in so.max_delta())

@@ -681,3 +681,103 @@ def test_native_group_rccl_world1(oracle, vt):
         assert np.all(diff <= 2 * W * 2.0 ** -24 * terms)
     finally:
         g.close()
+
+
+def _np_split(recs_list, K, total_rows, world):
+    """Reference split for dml_shard_split: stable per-owner partition, dest-major."""
+    from distml_amd.datadesc import KeyRange
+    step = KeyRange(0, total_rows - 1).linearSplit(world)[0].size()
+    kdt = "<i4" if K == 4 else "<i8"
+    owners = []
+    for r in recs_list:
+        k = r[:, :K].copy().view(kdt).ravel().astype(np.int64)
+        o = np.where((k >= 0) & (k < total_rows), k // max(step, 1), world)
+        owners.append(np.minimum(o, world))
+    out = b"".join(r[o == d].tobytes() for d in range(world) for r, o in zip(recs_list, owners))
+    counts = [[int((o == d).sum()) for d in range(world)] for o in owners]
+    return out, counts
+
+
+@pytest.mark.parametrize("case", [
+    # (data_type, key_type, value_type, cols, total_rows, world, n, nrec)
+    (1, 0, 1, 200, 5000, 8, 3, 4000),   # config-4 record shape, 8 owners
+    (1, 0, 0, 1000, 1000, 3, 2, 700),   # int32 counts, short last shard
+    (1, 1, 3, 10, 784, 2, 4, 300),      # MLR DoubleMatrix (LONG keys)
+    (0, 1, 1, 1, 10**9, 5, 2, 20000),   # sparse float array, long keys
+    (1, 0, 1, 64, 100, 64, 1, 257),     # 64 owners, ragged last block
+])
+def test_shard_split_kernel(case):
+    """dml_shard_split against a numpy stable partition: counts and bytes equal; keys
+    outside [0, total_rows) dropped."""
+    from distml_amd import DataDesc
+    from distml_amd.group import HipOps
+    dtp, kt, vt, cols, total, world, n, nrec = case
+    fmt = DataDesc(dtp, kt, vt)
+    K, V = (4 if kt == 0 else 8), (4 if vt in (0, 1) else 8)
+    stride = K + (V * cols if dtp == 1 else V)
+    rng = np.random.default_rng(sum(case))
+    recs = []
+    for b in range(n):
+        r = rng.integers(0, 256, size=(nrec + b, stride), dtype=np.uint8)
+        keys = rng.integers(-3, total + 3, size=nrec + b).astype("<i4" if K == 4 else "<i8")
+        r[:, :K] = keys.view(np.uint8).reshape(-1, K)
+        recs.append(r)
+    dev = [torch.from_numpy(r.reshape(-1)).cuda() for r in recs]
+    cap = sum(d.numel() for d in dev)
+    out = torch.zeros(cap + 16, dtype=torch.uint8, device="cuda")
+    torch.cuda.synchronize()
+    counts = HipOps().split(fmt, cols, total, world, [d.data_ptr() for d in dev], [d.numel() for d in dev],
+                            out.data_ptr(), cap, torch.cuda.current_stream().cuda_stream)
+    exp, exp_counts = _np_split(recs, K, total, world)
+    assert counts == exp_counts
+    assert out[:len(exp)].cpu().numpy().tobytes() == exp
+
+
+def test_shard_split_rejects_partial_records():
+    from distml_amd import DataDesc, NativeError
+    from distml_amd.group import HipOps
+    d = torch.zeros(805, dtype=torch.uint8, device="cuda")
+    with pytest.raises(NativeError):
+        HipOps().split(DataDesc(1, 0, 1), 200, 100, 2, [d.data_ptr()], [805], d.data_ptr(), 805, 0)
+
+
+def test_exchange_rccl_world1_adagrad(oracle):
+    """ShardGroup.push_exchange at world 1 over RCCL: dml_shard_split, the all-to-all
+    and the ordered AdaGrad apply; bit-exact (data, alpha, delta, maxDelta)."""
+    import socket
+    import torch.distributed as dist
+    from distml_amd import DataDesc, encode_matrix_push
+    from distml_amd.group import ShardGroup
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    dist.init_process_group("nccl", init_method=f"tcp://127.0.0.1:{port}", rank=0, world_size=1,
+                            device_id=torch.device("cuda", 0))
+    try:
+        rows, cols, W = 3000, 200, 5
+        fmt = DataDesc(1, 0, 1, False, True, True)
+        g = ShardGroup(fmt, rows, cols, 0, 1, device=0)
+        g.store.setAlpha(0.025, 0.0001, 1.5)
+        rng = np.random.default_rng(77)
+        host = []
+        for b in range(W):
+            keys = rng.permutation(rows + 50)[: rows // 2] - 25  # some keys outside the matrix: dropped
+            vals = (rng.standard_normal((len(keys), cols)) * 0.6).astype(np.float32)
+            host.append(encode_matrix_push(keys, vals, 0, 1))
+        dev = [torch.frombuffer(bytearray(h), dtype=torch.uint8).cuda() for h in host]
+        torch.cuda.synchronize()
+        g.push_exchange([d.data_ptr() for d in dev], [d.numel() for d in dev])
+        g.flush()
+        o = oracle_store(oracle, fmt, 0, rows - 1, cols)
+        o.set_alpha(0.025, 0.0001, 1.5)
+        for h in host:  # the client's split: out-of-matrix keys never reach the server
+            r = np.frombuffer(h, np.uint8).reshape(-1, 4 + 4 * cols)
+            k = r[:, :4].copy().view("<i4").ravel()
+            assert o.push(r[(k >= 0) & (k < rows)].tobytes()) == 0
+        assert kat.bits_equal(g.store.values(), o.data)
+        a, d = g.store.adagrad_state()
+        assert kat.bits_equal(a, o.alpha) and kat.bits_equal(d, o.delta)
+        assert g.store.maxDelta() == o.max_delta()
+    finally:
+        dist.destroy_process_group()
