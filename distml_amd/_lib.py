@@ -68,6 +68,7 @@ SIGNATURES = {
     "dml_prereduce_stream_wait": (C.c_int, [_vp, _vp]),
     "dml_shard_split": (C.c_int, [_P(dml_desc), _i32, _i64, _i32, _P(_vp), _P(_i64), _i32, _vp, _i64, _P(_i64), _vp]),
     "dml_group_unique_id": (C.c_int, [_vp, _i32]),
+    "dml_group_push_exchange": (C.c_int, [_vp, _P(_vp), _P(_i64), _i32]),
     "dml_group_create": (C.c_int, [_vp, _i32, _i32, _i32, _P(dml_desc), _i64, _i32, _i32, _P(_vp)]),
     "dml_group_store": (C.c_int, [_vp, _P(_vp)]),
     "dml_group_push_full_range": (C.c_int, [_vp, _P(_vp), _P(_i64), _i32]),

@@ -17,6 +17,7 @@
 // unique id the caller distributes (the JVM's control plane).
 #include <rccl/rccl.h>
 
+#include <algorithm>
 #include <cstring>
 #include <deque>
 #include <string>
@@ -62,6 +63,13 @@ struct dml_group {
     hipEvent_t applied[2] = {nullptr, nullptr};
     std::deque<dml_prereduce*> pending;
     int k = 0;
+    bool plain = true;  // plain-sum dense matrix: the full-range pre-reduce path applies
+    // exchange path (dml_group_push_exchange): split output, receive buffer, count buffers
+    void* xsend = nullptr;
+    void* xrecv = nullptr;
+    int64_t xsend_cap = 0, xrecv_cap = 0;
+    int64_t* xcnt = nullptr;  // device [2][world * kMaxW]: counts sent / received
+    bool xpending = false;    // the store may still read xrecv (its pushes are asynchronous)
 };
 
 namespace {
@@ -81,6 +89,9 @@ void group_free(dml_group* g) {
     if (!g) return;
     (void)hipSetDevice(g->device);
     (void)end_pending(g, 0);
+    if (g->xsend) (void)hipFree(g->xsend);
+    if (g->xrecv) (void)hipFree(g->xrecv);
+    if (g->xcnt) (void)hipFree(g->xcnt);
     for (int i = 0; i < 2; ++i) {
         if (g->partial[i]) (void)hipFree(g->partial[i]);
         if (g->recv[i]) (void)hipFree(g->recv[i]);
@@ -112,17 +123,37 @@ int group_init(dml_group* g, const uint8_t* unique_id) {
     void* ss = nullptr;
     GRC(dml_store_stream(g->store, &ss));
     g->sstream = (hipStream_t)ss;
+    for (int i = 0; i < 2; ++i) {
+        GHIP(hipEventCreateWithFlags(&g->rs_done[i], hipEventDisableTiming));
+        GHIP(hipEventCreateWithFlags(&g->applied[i], hipEventDisableTiming));
+    }
+    GHIP(hipMalloc((void**)&g->xcnt, sizeof(int64_t) * 2 * (size_t)g->world * kMaxW));
+    ncclUniqueId id;
+    memcpy(&id, unique_id, sizeof id);
+    GNCCL(ncclCommInitRank(&g->comm, g->world, id, g->rank));
+    return DML_OK;
+}
+
+// Full-range buffers on first use (an exchange-only group never allocates them).
+int ensure_partials(dml_group* g) {
+    if (g->partial[0]) return DML_OK;
     const size_t part = (size_t)g->world * (size_t)g->step_rows * (size_t)g->cols * g->vbytes;
     const size_t rcv = (size_t)g->step_rows * (size_t)g->cols * g->vbytes;
     for (int i = 0; i < 2; ++i) {
         GHIP(hipMalloc(&g->partial[i], part));
         GHIP(hipMalloc(&g->recv[i], rcv));
-        GHIP(hipEventCreateWithFlags(&g->rs_done[i], hipEventDisableTiming));
-        GHIP(hipEventCreateWithFlags(&g->applied[i], hipEventDisableTiming));
     }
-    ncclUniqueId id;
-    memcpy(&id, unique_id, sizeof id);
-    GNCCL(ncclCommInitRank(&g->comm, g->world, id, g->rank));
+    return DML_OK;
+}
+
+int grow(void** p, int64_t* cap, int64_t need) {
+    if (*cap >= need) return DML_OK;
+    if (*p) GHIP(hipFree(*p));
+    *p = nullptr;
+    *cap = 0;
+    const int64_t n = std::max<int64_t>(need, 1) + (need >> 3);  // 12.5 % headroom for the next call
+    GHIP(hipMalloc(p, (size_t)n));
+    *cap = n;
     return DML_OK;
 }
 
@@ -143,8 +174,8 @@ int dml_group_create(const uint8_t* unique_id, int32_t world, int32_t rank, int3
     if (!unique_id || !desc || !out || world <= 0 || rank < 0 || rank >= world || total_rows <= 0 || cols <= 0 ||
         pieces <= 0)
         return set_error(DML_E_INVALID_ARG, "bad group arguments");
-    if (desc->data_type != DML_DATA_TYPE_MATRIX || !desc->dense_column || desc->ada_grad)
-        return set_error(DML_E_UNSUPPORTED, "the sharded path supports dense-column plain matrices");
+    if (desc->data_type == DML_DATA_TYPE_MATRIX && !desc->dense_column)
+        return set_error(DML_E_UNSUPPORTED, "sparse-column matrices are not supported");
     auto* g = new (std::nothrow) dml_group();
     if (!g) return set_error(DML_E_NOMEM, "out of host memory");
     g->world = world;
@@ -154,6 +185,8 @@ int dml_group_create(const uint8_t* unique_id, int32_t world, int32_t rank, int3
     g->total_rows = total_rows;
     g->cols = cols;
     g->pieces = pieces;
+    g->plain = desc->data_type == DML_DATA_TYPE_MATRIX && !desc->ada_grad;
+    if (desc->data_type != DML_DATA_TYPE_MATRIX) g->cols = 1;
     switch (desc->value_type) {
         case DML_ELEMENT_TYPE_FLOAT: g->dtype = ncclFloat32; g->vbytes = 4; break;
         case DML_ELEMENT_TYPE_INT: g->dtype = ncclInt32; g->vbytes = 4; break;  // exact: mod 2^32 like the JVM int
@@ -177,7 +210,10 @@ int dml_group_store(dml_group* g, dml_store** store) {
 int dml_group_push_full_range(dml_group* g, const void* const* dev_bufs, const int64_t* lens, int32_t n) {
     if (!g || n < 0 || n > kMaxW || (n > 0 && (!dev_bufs || !lens)))
         return set_error(DML_E_INVALID_ARG, "bad push arguments (n must be <= 64)");
+    if (!g->plain)
+        return set_error(DML_E_UNSUPPORTED, "the full-range pre-reduce path needs a plain-sum matrix (use dml_group_push_exchange)");
     GHIP(hipSetDevice(g->device));
+    GRC(ensure_partials(g));
     const int64_t S = g->step_rows, P = g->pieces;
     if (S % P) return set_error(DML_E_INVALID_ARG, "pieces must divide the linearSplit step");
     const int64_t blk = S / P, W = g->world, C = g->cols;
@@ -211,9 +247,85 @@ int dml_group_push_full_range(dml_group* g, const void* const* dev_bufs, const i
     return end_pending(g, 1);  // the previous call's errors
 }
 
+int dml_group_push_exchange(dml_group* g, const void* const* dev_bufs, const int64_t* lens, int32_t n) {
+    if (!g || n < 0 || n > kMaxW || (n > 0 && (!dev_bufs || !lens)))
+        return set_error(DML_E_INVALID_ARG, "bad push arguments (n must be <= 64)");
+    GHIP(hipSetDevice(g->device));
+    const int W = g->world;
+    const int64_t K = g->desc.key_type == 0 ? 4 : 8;
+    const int64_t stride = g->desc.data_type == DML_DATA_TYPE_MATRIX ? K + (int64_t)g->vbytes * g->cols
+                                                                      : K + (int64_t)g->vbytes;
+    // the previous exchange's slices may still be read by the store: finish them
+    // (their deferred errors surface here, like the store's own next call)
+    if (g->xpending) {
+        g->xpending = false;
+        GRC(dml_store_flush(g->store));
+    }
+    int64_t total = 0;
+    for (int b = 0; b < n; ++b) total += lens[b];
+    GRC(grow(&g->xsend, &g->xsend_cap, total));
+    std::vector<int64_t> cnt((size_t)n * W);  // [push][dest]
+    GRC(dml_shard_split(&g->desc, g->cols, g->total_rows, W, dev_bufs, lens, n, g->xsend, g->xsend_cap, cnt.data(),
+                        g->cstream));
+    // counts per destination, then per source: mine[d][b] out, theirs[q][b] in (n per peer)
+    std::vector<int64_t> mine((size_t)W * n), theirs((size_t)W * n);
+    for (int d = 0; d < W; ++d)
+        for (int b = 0; b < n; ++b) mine[(size_t)d * n + b] = cnt[(size_t)b * W + d];
+    int64_t* dmine = g->xcnt;
+    int64_t* dtheirs = g->xcnt + (size_t)W * kMaxW;
+    GHIP(hipMemcpyAsync(dmine, mine.data(), sizeof(int64_t) * mine.size(), hipMemcpyHostToDevice, g->rstream));
+    GNCCL(ncclGroupStart());
+    for (int q = 0; q < W; ++q) {
+        GNCCL(ncclSend(dmine + (size_t)q * n, (size_t)n, ncclInt64, q, g->comm, g->rstream));
+        GNCCL(ncclRecv(dtheirs + (size_t)q * n, (size_t)n, ncclInt64, q, g->comm, g->rstream));
+    }
+    GNCCL(ncclGroupEnd());
+    GHIP(hipMemcpyAsync(theirs.data(), dtheirs, sizeof(int64_t) * theirs.size(), hipMemcpyDeviceToHost, g->rstream));
+    GHIP(hipStreamSynchronize(g->rstream));
+    std::vector<int64_t> soff((size_t)W + 1, 0), roff((size_t)W + 1, 0);
+    for (int q = 0; q < W; ++q) {
+        int64_t sb = 0, rb = 0;
+        for (int b = 0; b < n; ++b) {
+            sb += mine[(size_t)q * n + b] * stride;
+            rb += theirs[(size_t)q * n + b] * stride;
+        }
+        soff[(size_t)q + 1] = soff[(size_t)q] + sb;
+        roff[(size_t)q + 1] = roff[(size_t)q] + rb;
+    }
+    GRC(grow(&g->xrecv, &g->xrecv_cap, roff[(size_t)W]));
+    uint8_t* sp = (uint8_t*)g->xsend;
+    uint8_t* rp = (uint8_t*)g->xrecv;
+    GNCCL(ncclGroupStart());
+    for (int q = 0; q < W; ++q) {
+        GNCCL(ncclSend(sp + soff[(size_t)q], (size_t)(soff[(size_t)q + 1] - soff[(size_t)q]), ncclUint8, q, g->comm,
+                       g->rstream));
+        GNCCL(ncclRecv(rp + roff[(size_t)q], (size_t)(roff[(size_t)q + 1] - roff[(size_t)q]), ncclUint8, q, g->comm,
+                       g->rstream));
+    }
+    GNCCL(ncclGroupEnd());
+    GHIP(hipStreamSynchronize(g->rstream));
+    // the owner's pushes, rank-major: rank 0's pushes in order, then rank 1's, ...
+    std::vector<const void*> ptrs;
+    std::vector<int64_t> ls;
+    int64_t off = 0;
+    for (int q = 0; q < W; ++q)
+        for (int b = 0; b < n; ++b) {
+            const int64_t ln = theirs[(size_t)q * n + b] * stride;
+            if (ln > 0) {
+                ptrs.push_back(rp + off);
+                ls.push_back(ln);
+            }
+            off += ln;
+        }
+    if (ptrs.empty()) return DML_OK;
+    g->xpending = true;
+    return dml_store_push_batch_device(g->store, ptrs.data(), ls.data(), (int32_t)ptrs.size());
+}
+
 int dml_group_flush(dml_group* g) {
     if (!g) return set_error(DML_E_INVALID_ARG, "null group");
     GHIP(hipSetDevice(g->device));
+    g->xpending = false;  // dml_store_flush below finishes the exchange's pushes too
     int rc = end_pending(g, 0);
     for (hipStream_t s : {g->cstream, g->rstream})
         if (hipStreamSynchronize(s) != hipSuccess && rc == DML_OK) rc = set_error(DML_E_HIP, "group stream sync");

@@ -308,8 +308,15 @@ class NativeShardGroup:
         ls = (C.c_int64 * max(n, 1))(*lens)
         check(self._L.dml_group_push_full_range(C.c_void_p(self._h), ptrs, ls, n))
 
+    def push_exchange(self, dev_ptrs: Sequence[int], lens: Sequence[int]) -> None:
+        """The exact split / all-to-all / ordered-owner-apply path (dml_group_push_exchange)."""
+        n = len(dev_ptrs)
+        ptrs = (C.c_void_p * max(n, 1))(*dev_ptrs)
+        ls = (C.c_int64 * max(n, 1))(*lens)
+        check(self._L.dml_group_push_exchange(C.c_void_p(self._h), ptrs, ls, n), self.store)
+
     def flush(self) -> None:
-        check(self._L.dml_group_flush(C.c_void_p(self._h)))
+        check(self._L.dml_group_flush(C.c_void_p(self._h)), self.store)
 
     def close(self) -> None:
         if self._h:

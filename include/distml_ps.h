@@ -255,6 +255,15 @@ int dml_group_create(const uint8_t* unique_id, int32_t world, int32_t rank, int3
 /* The rank's shard store (fetch / checkpoint / read), owned by the group. */
 int dml_group_store(dml_group* g, dml_store** store);
 int dml_group_push_full_range(dml_group* g, const void* const* dev_bufs, const int64_t* lens, int32_t n);
+/* The exact path (AdaGrad, int32-checked, arrays, key-subset pushes): each of the
+ * rank's n device-resident pushes is split by owner shard (dml_shard_split), the
+ * slices go to their owners in one grouped ncclSend/ncclRecv exchange, and every
+ * owner applies the slices it received in rank-major push order (rank 0's n
+ * pushes, then rank 1's, ...) through the store's ordered push — the reference's
+ * client-split + server-apply data flow, bit-exact with errors included. Every
+ * rank calls with the same n (<= 64). The owner's pushes are asynchronous: their
+ * errors surface at the next exchange call or at dml_group_flush. */
+int dml_group_push_exchange(dml_group* g, const void* const* dev_bufs, const int64_t* lens, int32_t n);
 int dml_group_flush(dml_group* g);
 void dml_group_destroy(dml_group* g);
 

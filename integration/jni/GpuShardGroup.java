@@ -25,7 +25,14 @@ public class GpuShardGroup implements AutoCloseable {
     }
 
     /** Device pointers (HBM, this GPU) and byte lengths of up to 64 full-range pushes. */
-    public void pushFullRange(long[] devPtrs, long[] lens) { nativeGroupPush(handle, devPtrs, lens); }
+    public void pushFullRange(long[] devPtrs, long[] lens) { nativeGroupPush(handle, devPtrs, lens, false); }
+
+    /**
+     * Exact path for AdaGrad, int32-checked, array or key-subset pushes: split by owner
+     * (SparseMatrix.push's per-partition split), exchanged with RCCL send/recv, applied by
+     * each owner in rank-major push order. Every rank passes the same number of pushes.
+     */
+    public void pushExchange(long[] devPtrs, long[] lens) { nativeGroupPush(handle, devPtrs, lens, true); }
 
     /** Every call applied; throws the first deferred key / repeated-row error. */
     public void flush() { nativeGroupFlush(handle); }
@@ -44,7 +51,7 @@ public class GpuShardGroup implements AutoCloseable {
     private static native long nativeGroupCreate(byte[] id, int world, int rank, int device, int dataType,
                                                  int keyType, int valueType, int denseRow, int denseColumn,
                                                  int adaGrad, long totalRows, int cols, int pieces);
-    private static native void nativeGroupPush(long g, long[] devPtrs, long[] lens);
+    private static native void nativeGroupPush(long g, long[] devPtrs, long[] lens, boolean exchange);
     private static native void nativeGroupFlush(long g);
     private static native long nativeGroupStore(long g);
     private static native void nativeGroupDestroy(long g);

@@ -187,7 +187,8 @@ JNIEXPORT jlong JNICALL GFN(nativeGroupCreate)(JNIEnv* env, jclass, jbyteArray i
     return reinterpret_cast<jlong>(g);
 }
 
-JNIEXPORT void JNICALL GFN(nativeGroupPush)(JNIEnv* env, jclass, jlong g, jlongArray ptrs, jlongArray lens) {
+JNIEXPORT void JNICALL GFN(nativeGroupPush)(JNIEnv* env, jclass, jlong g, jlongArray ptrs, jlongArray lens,
+                                             jboolean exchange) {
     const jsize n = env->GetArrayLength(ptrs);
     std::vector<jlong> p((size_t)n), l((size_t)n);
     env->GetLongArrayRegion(ptrs, 0, n, p.data());
@@ -198,7 +199,9 @@ JNIEXPORT void JNICALL GFN(nativeGroupPush)(JNIEnv* env, jclass, jlong g, jlongA
         dp[(size_t)i] = reinterpret_cast<const void*>(p[(size_t)i]);
         dl[(size_t)i] = l[(size_t)i];
     }
-    if (int rc = dml_group_push_full_range(G(g), dp.data(), dl.data(), (int32_t)n)) throw_for(env, rc);
+    const int rc = exchange ? dml_group_push_exchange(G(g), dp.data(), dl.data(), (int32_t)n)
+                            : dml_group_push_full_range(G(g), dp.data(), dl.data(), (int32_t)n);
+    if (rc) throw_for(env, rc);
 }
 
 JNIEXPORT void JNICALL GFN(nativeGroupFlush)(JNIEnv* env, jclass, jlong g) {

@@ -781,3 +781,60 @@ def test_exchange_rccl_world1_adagrad(oracle):
         assert g.store.maxDelta() == o.max_delta()
     finally:
         dist.destroy_process_group()
+
+
+def test_native_group_exchange_world1(oracle):
+    """dml_group_push_exchange at world 1 (native RCCL send/recv): two AdaGrad calls,
+    then flush — bit-exact data, alpha, delta, maxDelta; then an int32-checked group
+    whose second call drives a counter negative: the error surfaces at flush with the
+    reference's key/col, and the shard holds the state the sequential oracle stops in."""
+    from distml_amd import DataDesc, IllegalStateException, encode_matrix_push
+    from distml_amd.group import NativeShardGroup
+    rows, cols = 1500, 200
+    fmt = DataDesc(1, 0, 1, False, True, True)
+    g = NativeShardGroup(fmt, rows, cols, 0, 1, NativeShardGroup.unique_id(), device=0)
+    rng = np.random.default_rng(91)
+    try:
+        g.store.setAlpha(0.025, 0.0001, 1.5)
+        host = []
+        for b in range(6):
+            keys = rng.permutation(rows)[: rng.integers(100, rows)]
+            host.append(encode_matrix_push(keys, (rng.standard_normal((len(keys), cols)) * 0.6).astype(np.float32),
+                                           0, 1))
+        dev = [torch.frombuffer(bytearray(h), dtype=torch.uint8).cuda() for h in host]
+        torch.cuda.synchronize()
+        ptrs, lens = [d.data_ptr() for d in dev], [d.numel() for d in dev]
+        g.push_exchange(ptrs[:4], lens[:4])
+        g.push_exchange(ptrs[4:], lens[4:])
+        g.flush()
+        o = oracle_store(oracle, fmt, 0, rows - 1, cols)
+        o.set_alpha(0.025, 0.0001, 1.5)
+        for h in host:
+            assert o.push(h) == 0
+        assert kat.bits_equal(g.store.values(), o.data)
+        a, d = g.store.adagrad_state()
+        assert kat.bits_equal(a, o.alpha) and kat.bits_equal(d, o.delta)
+        assert g.store.maxDelta() == o.max_delta()
+    finally:
+        g.close()
+
+    ifmt = DataDesc(1, 0, 0)
+    g = NativeShardGroup(ifmt, rows, 16, 0, 1, NativeShardGroup.unique_id(), device=0)
+    try:
+        g.store.load_values(np.full((rows, 16), 3, np.int32))
+        ok = encode_matrix_push(np.arange(rows), np.full((rows, 16), -1, np.int32), 0, 0)
+        bad = encode_matrix_push(np.array([7, 5]), np.array([[0] * 16, [0] * 3 + [-9] + [0] * 12], np.int32), 0, 0)
+        dev = [torch.frombuffer(bytearray(h), dtype=torch.uint8).cuda() for h in (ok, bad)]
+        torch.cuda.synchronize()
+        g.push_exchange([dev[0].data_ptr()], [dev[0].numel()])
+        g.push_exchange([dev[1].data_ptr()], [dev[1].numel()])
+        with pytest.raises(IllegalStateException) as ei:
+            g.flush()
+        assert (ei.value.key, ei.value.col) == (5, 3)
+        o = oracle.OracleStore(1, 0, 0, 0, rows - 1, 16)
+        o.data[:] = 3
+        assert o.push(ok) == 0
+        assert o.push(bad) != 0
+        assert np.array_equal(g.store.values(), o.data)
+    finally:
+        g.close()
