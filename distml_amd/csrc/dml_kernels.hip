@@ -995,6 +995,25 @@ static hipError_t launch_auto(void* shard, int64_t rows, int32_t cols, const Bat
         // register-limited 12-24 waves (scripts/exp_variants.py)
         if (cols % (64 * VEC * 4) == 0) return DML_LF(1, 4, 2, 2);
         static const int nf_rpw = getenv("DML_NF_RPW") ? atoi(getenv("DML_NF_RPW")) : 4;  // A/B knob
+        // Non-temporal shard stores on the other shapes (the rows are written once per
+        // batch): config 5 460 -> 433 us; config 2's FULL shape measured no gain
+        // (variant 34). Pre-reduce partials are read back by RCCL right away: cached.
+        // DML_NF_SNT (A/B, read once): 0 plain stores for every mode.
+        static const bool nf_snt = !(getenv("DML_NF_SNT") && atoi(getenv("DML_NF_SNT")) == 0);
+        if (nf_snt && MODE != kPreReduce) {
+#define DML_LN(G, CPW, RPW) launch_reduce_t<T, MODE, G, true, 4, 1, CPW, RPW>(shard, rows, cols, bt, nb, stride, K, \
+                                                     slot, rowflag, ctrl, tail_cut, ada, st, nblocks_out, ev, rm)
+#define DML_LFN(G, CPW, RPW) launch_reduce_t<T, MODE, G, true, 4, 1, CPW, RPW, true>(shard, rows, cols, bt, nb, \
+                                                     stride, K, slot, rowflag, ctrl, tail_cut, ada, st, nblocks_out, ev, rm, 0)
+            if (nchunks >= 4 && nf_rpw == 2) return DML_LN(3, 4, 2);
+            if (nchunks >= 4) return pairs ? DML_LN(3, 4, 4) : DML_LN(1, 4, 4);
+            if (cols % (64 * VEC * 2) == 0) return DML_LFN(1, 2, 4);
+            if (nchunks >= 2) return pairs ? DML_LN(3, 2, 4) : DML_LN(1, 2, 4);
+            if (cols % (64 * VEC) == 0) return DML_LFN(1, 1, 4);
+            return pairs ? DML_LN(3, 1, 4) : DML_LN(1, 1, 4);
+#undef DML_LN
+#undef DML_LFN
+        }
         if (nchunks >= 4 && nf_rpw == 2) return DML_L(3, 4, 2);
         if (nchunks >= 4) return pairs ? DML_L(3, 4, 4) : DML_L(1, 4, 4);
         if (cols % (64 * VEC * 2) == 0) return DML_LF(1, 2, 4, 0);
