@@ -147,6 +147,129 @@ def stream_peaks(L, torch, nbytes: int = 1 << 31, reps: int = 5):
     return out
 
 
+# ---------------------------------------------------------------- configs 4 and 5
+# One GPU's shard of BASELINE.json configs 4 and 5 (8-GPU configs):
+# the rows linearSplit(8) gives one rank, device-resident pushes of the named
+# shapes, the store's ordered batch reduce. `python bench.py --config 5|4`.
+SHARD_CONFIGS = {
+    "5": dict(name="config5: LDA IntMatrixStore shard 125000x1000 int32 (negativity check), "
+                   "32 pushes x 8192 distinct rows ([int32][1000 x int32])",
+              rows=125_000, cols=1000, W=32, nrec=8192, vt=0, ada=None, seed0=4000, mult=331, init=11, steps=20),
+    "4": dict(name="config4: Word2Vec FloatMatrixStoreAdaGrad shard 1250000x200 fp32 (data + alpha + delta), "
+                   "8 full-range pushes ([int32][200 x f32])",
+              rows=1_250_000, cols=200, W=8, nrec=1_250_000, vt=1, ada=(0.025, 0.0001, 1.0), seed0=3000,
+              mult=7919, init=13, steps=5),
+}
+
+
+def _coprime(a, n):
+    import math
+    while math.gcd(a, n) != 1:
+        a += 1
+    return a
+
+
+def _shard_perms(c):
+    return [(_coprime((c["seed0"] + b) * 2654435761 % c["rows"] | 1, c["rows"]), b * c["mult"] % c["rows"])
+            for b in range(c["W"])]
+
+
+def shard_cpu_baseline(c, budget_s: float):
+    """The oracle (1 thread) on the first pushes of the same workload (int32: each push
+    alternating with its negation, as on the GPU, so counts stay >= 0)."""
+    import numpy as np
+    sys.path.insert(0, os.path.join(ROOT, "oracle"))
+    import pyoracle
+    perms = _shard_perms(c)
+    rows, cols, nrec = c["rows"], c["cols"], c["nrec"]
+    host = [pyoracle.synth_dense_bucket(0, c["vt"], 0, rows, nrec, cols, c["seed0"] + b, *perms[b]) for b in range(4)]
+    if c["vt"] == 0:
+        negs = []
+        for h in host:
+            t = h.view(np.int32).reshape(nrec, 1 + cols).copy()
+            t[:, 1:] = -t[:, 1:]
+            negs.append(t.view(np.uint8).reshape(-1))
+        host = [x for pair in zip(host, negs) for x in pair]
+    o = pyoracle.OracleStore(1, 0, c["vt"], 0, rows - 1, cols, ada_grad=1 if c["ada"] else 0)
+    if c["ada"]:
+        o.set_alpha(*c["ada"])
+    o.synth_fill(c["init"])
+    nb, t0 = 0, time.perf_counter()
+    while time.perf_counter() - t0 < budget_s:
+        assert o.push(host[nb % len(host)]) == 0
+        nb += 1
+    el = time.perf_counter() - t0
+    return {"value": round(nb * nrec * (4 + 4 * cols) / el / 2**30, 3), "unit": "GiB/s of push bytes", "cores": 1,
+            "kind": "port", "sample": f"{nb} pushes of the same shapes in {el:.1f} s, oracle/dml_oracle.c"}
+
+
+def run_shard_config(which: str, cpu_s: float, no_cpu: bool) -> dict:
+    import torch
+    from distml_amd import DataDesc, DataStore, KeyRange, _lib
+    c = SHARD_CONFIGS[which]
+    L = _lib.load()
+    rows, cols, W, nrec = c["rows"], c["cols"], c["W"], c["nrec"]
+    fmt = DataDesc(1, 0, c["vt"], False, True, c["ada"] is not None)
+    store = DataStore(fmt, KeyRange(0, rows - 1), cols)
+    if c["ada"]:
+        store.setAlpha(*c["ada"])
+    store.rand(c["init"])
+    st = torch.cuda.current_stream().cuda_stream
+    bufs = []
+    for b, (pa, pc) in enumerate(_shard_perms(c)):
+        t = torch.empty(nrec * (4 + 4 * cols), dtype=torch.uint8, device="cuda")
+        assert L.dml_synth_dense_bucket(t.data_ptr(), C.byref(fmt.to_c()), 0, rows, nrec, cols, c["seed0"] + b,
+                                        pa, pc, C.c_void_p(st)) == 0
+        bufs.append(t)
+    torch.cuda.synchronize()
+    sets = [([b.data_ptr() for b in bufs], [b.numel() for b in bufs])]
+    if c["vt"] == 0:  # alternate with the negated pushes: repeated steps keep the counts >= 0
+        neg = []
+        for b in bufs:
+            t = b.clone().view(torch.int32).view(nrec, 1 + cols)
+            t[:, 1:] = -t[:, 1:]
+            neg.append(t.view(torch.uint8).view(-1))
+        bufs = bufs + neg
+        sets.append(([b.data_ptr() for b in neg], [b.numel() for b in neg]))
+    torch.cuda.synchronize()
+    # SURVEY §8d: every push byte once + the touched shard rows read and written once
+    # (AdaGrad: alpha and delta too)
+    touched = rows if nrec >= rows else int(round(rows * (1 - (1 - nrec / rows) ** W)))
+    algo = W * nrec * (4 + 4 * cols) + 2 * (3 if c["ada"] else 1) * 4 * cols * touched
+    steps = c["steps"]
+    for i in range(max(4, steps)):
+        store.pushDevice(*sets[i % len(sets)])
+    store.flush()
+    store.set_timing(True)
+    store.kernel_time(reset=True)
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for i in range(steps):
+        store.pushDevice(*sets[i % len(sets)])
+    store.flush()
+    torch.cuda.synchronize()
+    el = time.perf_counter() - t0
+    k_ms, k_n = store.kernel_time(reset=True)
+    store.set_timing(False)
+    assert store.error_state()[0] == 0, store.error_state()
+    store.close()
+    del bufs, sets
+    torch.cuda.empty_cache()
+    k_s = k_ms / max(k_n, 1) / 1e3
+    line = {"metric": "device-resident push reduce GiB/s (one GPU's shard)", "value": round(steps * algo / el / 2**30, 1),
+            "unit": "GiB/s", "n_gpus": 1, "steps": steps, "ms_per_step": round(el / steps * 1e3, 3),
+            "higher_is_better": True, "dtype": "i32" if c["vt"] == 0 else "f32", "data": "synthetic",
+            "config": {"workload": c["name"], "rows": rows, "cols": cols, "pushes": W, "records_per_push": nrec,
+                       "algorithmic_bytes_per_step": algo},
+            "roofline": {"bound": "hbm", "achieved": round(algo / k_s / 1e9, 1) if k_n else None,
+                         "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                         "frac": round(algo / k_s / 1e9 / HBM_PEAK_GBS, 4) if k_n else None,
+                         "kernel_us_avg": round(k_s * 1e6, 1), "traffic": None}}
+    if not no_cpu:
+        line["cpu_baseline"] = shard_cpu_baseline(c, cpu_s)
+    return line
+
+
 def load_traffic():
     p = os.path.join(ROOT, "profiles", "pmc_traffic.json")
     if not os.path.exists(p):
@@ -171,7 +294,13 @@ def main():
     ap.add_argument("--pieces", type=int, default=4, help="pre-reduce row slices per call (sharded path)")
     ap.add_argument("--group", action="store_true",
                     help="use the sharded pre-reduce/reduce-scatter path even at N=1 (path check)")
+    ap.add_argument("--config", choices=["2", "4", "5"], default="2",
+                    help="2 = the headline (default); 4 / 5 = one GPU's shard of those 8-GPU configs")
+    ap.add_argument("--cpu-seconds", type=float, default=8.0, help="CPU baseline budget for --config 4/5")
     args = ap.parse_args()
+    if args.config != "2":
+        print(json.dumps(run_shard_config(args.config, args.cpu_seconds, args.no_cpu)), flush=True)
+        return
 
     import torch
     import torch.distributed as dist

@@ -9,18 +9,18 @@ import sys
 import time
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-sys.path[:0] = [ROOT, os.path.join(ROOT, "oracle")]
+sys.path[:0] = [ROOT]
 import numpy as np  # noqa: E402
 import torch  # noqa: E402
 
 import bench  # noqa: E402
-import pyoracle  # noqa: E402
-from distml_amd import DataDesc, DataStore, KeyRange  # noqa: E402
+from distml_amd import DataDesc, DataStore, KeyRange, _lib  # noqa: E402
 
 fmt = DataDesc(1, 0, 1)
 W = bench.W
-host = [pyoracle.synth_dense_bucket(0, 1, 0, bench.ROWS, bench.ROWS, bench.COLS, 1000 + b, *bench.perm_for(b))
-        for b in range(W)]
+# the same synthetic pushes as bench.py, generated on the GPU and copied to host memory
+host = [t.cpu().numpy() for t in bench.make_buckets(_lib.load(), torch, fmt, W, bench.ROWS)]
+torch.cuda.empty_cache()
 algo = W * bench.BUCKET + 2 * bench.SHARD
 res = {}
 store = DataStore(fmt, KeyRange(0, bench.ROWS - 1), bench.COLS)

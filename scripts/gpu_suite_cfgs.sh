@@ -1,9 +1,11 @@
-# GPU parity suite, then configs 5 and 4 per-GPU shard measurements.
+# GPU parity suite, then configs 5 and 4 (one GPU's shard) through bench.py --config.
 set -e
 cd $GRAFT_REPO_ROOT
 export TMPDIR=/tmp
 mkdir -p gpurun_out
 timeout -k 10 900 python -u -m pytest tests -m gpu -x -q --timeout 200 --timeout-method thread > gpurun_out/pytest_gpu.log 2>&1
 tail -2 gpurun_out/pytest_gpu.log
-timeout -k 10 300 python scripts/bench_configs.py 5 4 > gpurun_out/cfg45.log 2>&1
-grep config gpurun_out/cfg45.log
+timeout -k 10 300 python bench.py --config 5 > gpurun_out/cfg5.log 2>&1
+timeout -k 10 300 python bench.py --config 4 > gpurun_out/cfg4.log 2>&1
+tail -1 gpurun_out/cfg5.log
+tail -1 gpurun_out/cfg4.log

@@ -71,6 +71,20 @@ def main(tag):
             for r in csv.DictReader(open(sp)):
                 f.write(f"| `{r['Name'][:90]}` | {r['Calls']} | {float(r['AverageNs'])/1e3:.1f} | "
                         f"{float(r['Percentage']):.1f} |\n")
+    for cfg in ("5", "4"):
+        cs = os.path.join(OUT, f"prof_cfg{cfg}", "run_kernel_stats.csv")
+        if not os.path.exists(cs):
+            continue
+        shutil.copy(cs, os.path.join(PROF, f"{tag}_cfg{cfg}_kernel_stats.csv"))
+        lines = [l for l in open(os.path.join(OUT, f"prof_cfg{cfg}.log")) if l.startswith("{")]
+        with open(os.path.join(PROF, f"{tag}_summary.md"), "a") as f:
+            f.write(f"\n## Config {cfg}, one GPU's shard (`rocprofv3 --kernel-trace --stats -- python3 bench.py "
+                    f"--config {cfg} --cpu-seconds 2`)\n\n| kernel | calls | avg µs | % time |\n|---|---|---|---|\n")
+            for r in csv.DictReader(open(cs)):
+                f.write(f"| `{r['Name'][:90]}` | {r['Calls']} | {float(r['AverageNs'])/1e3:.1f} | "
+                        f"{float(r['Percentage']):.1f} |\n")
+            if lines:
+                f.write("\nbench line of the same run (under the profiler):\n\n```\n" + lines[-1] + "```\n")
     print(open(os.path.join(PROF, f"{tag}_summary.md")).read())
 
 
