@@ -155,10 +155,18 @@ SHARD_CONFIGS = {
     "5": dict(name="config5: LDA IntMatrixStore shard 125000x1000 int32 (negativity check), "
                    "32 pushes x 8192 distinct rows ([int32][1000 x int32])",
               rows=125_000, cols=1000, W=32, nrec=8192, vt=0, ada=None, seed0=4000, mult=331, init=11, steps=20),
-    "4": dict(name="config4: Word2Vec FloatMatrixStoreAdaGrad shard 1250000x200 fp32 (data + alpha + delta), "
-                   "8 full-range pushes ([int32][200 x f32])",
-              rows=1_250_000, cols=200, W=8, nrec=1_250_000, vt=1, ada=(0.025, 0.0001, 1.0), seed0=3000,
-              mult=7919, init=13, steps=5),
+    # config 4's metric is the plain sum (FloatMatrixStore), W = 8 and 32; AdaGrad is its variant
+    "4": dict(name="config4: Word2Vec rows, FloatMatrixStore shard 1250000x200 fp32, 8 full-range pushes "
+                   "([int32][200 x f32])",
+              rows=1_250_000, cols=200, W=8, nrec=1_250_000, vt=1, ada=None, seed0=3000, mult=7919, init=13,
+              steps=10),
+    "4-32": dict(name="config4 (W=32): Word2Vec rows, FloatMatrixStore shard 1250000x200 fp32, 32 full-range pushes",
+                 rows=1_250_000, cols=200, W=32, nrec=1_250_000, vt=1, ada=None, seed0=3000, mult=7919, init=13,
+                 steps=5),
+    "4-ada": dict(name="config4 AdaGrad variant: FloatMatrixStoreAdaGrad shard 1250000x200 fp32 (data + alpha + "
+                       "delta), 8 full-range pushes",
+                  rows=1_250_000, cols=200, W=8, nrec=1_250_000, vt=1, ada=(0.025, 0.0001, 1.0), seed0=3000,
+                  mult=7919, init=13, steps=5),
 }
 
 
@@ -294,8 +302,8 @@ def main():
     ap.add_argument("--pieces", type=int, default=4, help="pre-reduce row slices per call (sharded path)")
     ap.add_argument("--group", action="store_true",
                     help="use the sharded pre-reduce/reduce-scatter path even at N=1 (path check)")
-    ap.add_argument("--config", choices=["2", "4", "5"], default="2",
-                    help="2 = the headline (default); 4 / 5 = one GPU's shard of those 8-GPU configs")
+    ap.add_argument("--config", choices=["2", "4", "4-32", "4-ada", "5"], default="2",
+                    help="2 = the headline (default); 4, 4-32, 4-ada, 5 = one GPU's shard of those 8-GPU configs")
     ap.add_argument("--cpu-seconds", type=float, default=8.0, help="CPU baseline budget for --config 4/5")
     args = ap.parse_args()
     if args.config != "2":

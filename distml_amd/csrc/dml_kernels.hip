@@ -1032,7 +1032,7 @@ bool reduce_clears_slots(int vtype, int mode, int32_t cols) {
     if (cols < VEC) return false;  // k_reduce's generic path
     if (vtype == kF32 && mode == kAdd) {
         const int v = reduce_variant();
-        if (v == 10 || v == 13 || v == 14) return false;  // the one-row k_reduce variants
+        if (v == 10 || v == 13 || v == 14 || v == 40 || v == 41 || v == 44) return false;  // one-row k_reduce variants
     }
     return true;
 }
@@ -1071,6 +1071,12 @@ hipError_t launch_reduce(int vtype, int mode, void* shard, int64_t rows, int32_t
                 case 38: return launch_reduce_t<float, kAdd, 3, true, 4, 0, 4, 2, true>(shard, rows, cols, bt, nb, stride, K, slot, rowflag, ctrl, tail_cut, ada, st, nblocks_out, ev, {}, 2);
                 case 36: return launch_reduce_t<float, kAdd, 1, true, 4, false, 4, 1 + 1, true>(shard, rows, cols, bt, nb, stride, K, slot, rowflag, ctrl, tail_cut, ada, st, nblocks_out, ev, {}, 2);
                 case 29: return launch_reduce_t<float, kAdd, 1, true, 4, false, 4, 4, true>(shard, rows, cols, bt, nb, stride, K, slot, rowflag, ctrl, tail_cut, ada, st, nblocks_out, ev);
+                // narrow rows (config 4, 200 cols): one-row k_reduce with G pushes per load group, nt
+                case 40: return launch_reduce_t<float, kAdd, 8, true, 4, 1, 1, 1>(shard, rows, cols, bt, nb, stride, K, slot, rowflag, ctrl, tail_cut, ada, st, nblocks_out, ev);
+                case 41: return launch_reduce_t<float, kAdd, 4, true, 4, 1, 1, 1>(shard, rows, cols, bt, nb, stride, K, slot, rowflag, ctrl, tail_cut, ada, st, nblocks_out, ev);
+                case 42: return launch_reduce_t<float, kAdd, 1, true, 4, 1, 1, 4>(shard, rows, cols, bt, nb, stride, K, slot, rowflag, ctrl, tail_cut, ada, st, nblocks_out, ev);
+                case 43: return launch_reduce_t<float, kAdd, 3, true, 4, 1, 1, 2>(shard, rows, cols, bt, nb, stride, K, slot, rowflag, ctrl, tail_cut, ada, st, nblocks_out, ev);
+                case 44: return launch_reduce_t<float, kAdd, 16, true, 4, 1, 1, 1>(shard, rows, cols, bt, nb, stride, K, slot, rowflag, ctrl, tail_cut, ada, st, nblocks_out, ev);
                 default: return DML_A(float, kAdd);
             }
         }

@@ -16,6 +16,8 @@ timeout -s KILL 120 rocprofv3 --pmc FETCH_SIZE -d $R/gpurun_out/prof_fetch -o ru
 timeout -s KILL 120 rocprofv3 --pmc WRITE_SIZE -d $R/gpurun_out/prof_write -o run --output-format csv -- python3 bench.py --steps 10 --warmup 20 --no-cpu --sparse-steps 0 > gpurun_out/prof_write.log 2>&1
 timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $R/gpurun_out/prof_cfg5 -o run --output-format csv -- python3 bench.py --config 5 --cpu-seconds 2 > gpurun_out/prof_cfg5.log 2>&1
 timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $R/gpurun_out/prof_cfg4 -o run --output-format csv -- python3 bench.py --config 4 --cpu-seconds 2 > gpurun_out/prof_cfg4.log 2>&1
+timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $R/gpurun_out/prof_cfg4-ada -o run --output-format csv -- python3 bench.py --config 4-ada --cpu-seconds 2 > gpurun_out/prof_cfg4-ada.log 2>&1
 tail -1 gpurun_out/prof_cfg5.log
 tail -1 gpurun_out/prof_cfg4.log
+tail -1 gpurun_out/prof_cfg4-ada.log
 echo all-done

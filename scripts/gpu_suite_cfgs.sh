@@ -6,6 +6,7 @@ mkdir -p gpurun_out
 timeout -k 10 900 python -u -m pytest tests -m gpu -x -q --timeout 200 --timeout-method thread > gpurun_out/pytest_gpu.log 2>&1
 tail -2 gpurun_out/pytest_gpu.log
 timeout -k 10 300 python bench.py --config 5 > gpurun_out/cfg5.log 2>&1
-timeout -k 10 300 python bench.py --config 4 > gpurun_out/cfg4.log 2>&1
-tail -1 gpurun_out/cfg5.log
-tail -1 gpurun_out/cfg4.log
+for c in 4 4-32 4-ada; do
+timeout -k 10 300 python bench.py --config $c > gpurun_out/cfg$c.log 2>&1
+done
+for c in 5 4 4-32 4-ada; do tail -1 gpurun_out/cfg$c.log; done

@@ -71,7 +71,7 @@ def main(tag):
             for r in csv.DictReader(open(sp)):
                 f.write(f"| `{r['Name'][:90]}` | {r['Calls']} | {float(r['AverageNs'])/1e3:.1f} | "
                         f"{float(r['Percentage']):.1f} |\n")
-    for cfg in ("5", "4"):
+    for cfg in ("5", "4", "4-ada"):
         cs = os.path.join(OUT, f"prof_cfg{cfg}", "run_kernel_stats.csv")
         if not os.path.exists(cs):
             continue
