@@ -11,6 +11,11 @@ namespace dml {
 // One ordered batch chunk holds at most this many pushes (the slot table is
 // [rows][kMaxW] int32); longer batches run as consecutive chunks, in order.
 constexpr int kMaxW = 64;
+// Row stride of a chunk's slot table: its push count rounded up to 8 (scalar slot
+// loads read 8 entries at a time). [rows][stride] instead of [rows][64]: an
+// 8-push chunk of config 4's 1.25 M rows indexes into 40 MB (stays in the 256 MB
+// MALL) instead of 320 MB. Allocations stay rows x kMaxW.
+__host__ __device__ inline int slot_stride(int nb) { return (nb + 7) & ~7; }
 
 // Position of a byte in the batch, in reference processing order:
 // bucket-major, then byte offset inside the bucket (the order in which

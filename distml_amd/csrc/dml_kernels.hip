@@ -78,9 +78,9 @@ __global__ __launch_bounds__(256) void k_index(const Batch bt, int64_t stride, i
         return;
     }
     if constexpr (PLAIN) {
-        *(DML_GLOBAL int32_t*)&slot[idx * kMaxW + b] = (int32_t)r;
+        *(DML_GLOBAL int32_t*)&slot[idx * slot_stride((int)gridDim.y) + b] = (int32_t)r;
     } else {
-        const int32_t old = atomicExch(&slot[idx * kMaxW + b], (int32_t)r);
+        const int32_t old = atomicExch(&slot[idx * slot_stride((int)gridDim.y) + b], (int32_t)r);
         if (old != -1) {
             rowflag[idx] = 1u;
             ctrl->no_dup = 0u;  // benign race: every writer stores the same value
@@ -112,7 +112,7 @@ __global__ __launch_bounds__(256) void k_index_multi(const Batch bt, int64_t str
 #pragma unroll
     for (int j = 0; j < RPT; ++j) {
         old[j] = -1;
-        if (idx[j] >= 0) old[j] = atomicExch(&slot[idx[j] * kMaxW + b], (int32_t)(r0 + j * 256));
+        if (idx[j] >= 0) old[j] = atomicExch(&slot[idx[j] * slot_stride((int)gridDim.y) + b], (int32_t)(r0 + j * 256));
     }
 #pragma unroll
     for (int j = 0; j < RPT; ++j) {
@@ -135,7 +135,7 @@ __global__ __launch_bounds__(256) void k_verify(const Batch bt, int64_t stride, 
     if (r >= bt.nrec[b]) return;
     const int64_t idx = row_index(ld_key(bt.base[b] + r * stride, K), first, rows);
     if (idx < 0) return;
-    if (slot[idx * kMaxW + b] != (int32_t)r) {
+    if (slot[idx * slot_stride((int)gridDim.y) + b] != (int32_t)r) {
         rowflag[idx] = 1u;
         ctrl->no_dup = 0u;
     }
@@ -277,7 +277,7 @@ __global__ __launch_bounds__(64 * WPB) void k_reduce(T* __restrict__ shard, int6
             negcut = ctrl->neg_pos;
             if (negcut == kNoPos) break;
         }
-        const int32_t* srow = slot + row * kMaxW;
+        const int32_t* srow = slot + row * slot_stride(nb);
 
         T acc[CPW][VEC];
         // AdaGrad: delta; the delta after the last push that left it above 1 (0 =
@@ -438,7 +438,7 @@ __global__ __launch_bounds__(64 * WPB) void k_reduce(T* __restrict__ shard, int6
             // per row this wave is the row's only reader and its slot reads are done.
             if (ngroups == 1) {
                 const int nact = (cols + VEC - 1) / VEC < 64 ? (cols + VEC - 1) / VEC : 64;  // live lanes
-                for (int j = lane; j < nb; j += nact) const_cast<int32_t*>(slot)[row * kMaxW + j] = -1;
+                for (int j = lane; j < nb; j += nact) const_cast<int32_t*>(slot)[row * slot_stride(nb) + j] = -1;
             }
         }
         if (MODE == kPreReduce && !touched) {
@@ -591,7 +591,7 @@ __global__ __launch_bounds__(64 * WPB) void k_reduce_rows(T* __restrict__ shard,
             if (MODE == kPreReduce)
                 for (int c = 0; c < CPW; ++c)
                     for (int e = 0; e < nv[c]; ++e) rp[c0[c] + e] = T(0);
-            const int32_t* srow = slot + row[r] * kMaxW;
+            const int32_t* srow = slot + row[r] * slot_stride(nb);
             for (int b = 0; b < nb; ++b) {
                 const int gb = bt.bidx[b];
                 if (gb > cut_b) break;
@@ -637,14 +637,15 @@ __global__ __launch_bounds__(64 * WPB) void k_reduce_rows(T* __restrict__ shard,
     static_assert(kMaxW == 64, "one push per lane");
     int32_t vslot[RPW];
 #pragma unroll
-    for (int r = 0; r < RPW; ++r) vslot[r] = (live >> r & 1u) ? slot[row[r] * kMaxW + lane] : -1;
+    // lanes >= nb read past the row's entries (another row's): masked to -1
+    for (int r = 0; r < RPW; ++r) vslot[r] = ((live >> r & 1u) && lane < nb) ? slot[row[r] * slot_stride(nb) + lane] : -1;
     if constexpr (MODE != kAddCheckI32) {
         // Hand the slot rows back as the next batch's index expects them (-1 = no
         // record), so the host skips the slot-table memset (reduce_clears_slots). The
         // int32-check mode keeps them: its rollback re-reads the table.
 #pragma unroll
         for (int r = 0; r < RPW; ++r)
-            if ((live >> r & 1u) && lane < nb) slot[row[r] * kMaxW + lane] = -1;
+            if ((live >> r & 1u) && lane < nb) slot[row[r] * slot_stride(nb) + lane] = -1;
     }
     const uint64_t vbase = lane < nb ? (uint64_t)bt.base[lane] : 0ull;
     if constexpr (DEPTH == 2) {

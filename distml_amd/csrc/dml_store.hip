@@ -480,7 +480,7 @@ int replay_rows(dml_store* s, const Chunk& c, Workspace& W, Ctrl* ctl) {
             vc.bt.len[j] = c.bt.len[col.src_b];
             vc.bt.nrec[j] = c.bt.nrec[col.src_b];
             vc.bt.bidx[j] = c.bt.bidx[col.src_b];
-            for (auto& pr : col.rr) hslot[(size_t)pr.first * kMaxW + (size_t)j] = pr.second;
+            for (auto& pr : col.rr) hslot[(size_t)pr.first * (size_t)slot_stride(vc.nb) + (size_t)j] = pr.second;
         }
         HIPCHK(hipMemcpy(W.slot, hslot.data(), hslot.size() * sizeof(int32_t), hipMemcpyHostToDevice));
         return DML_OK;
