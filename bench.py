@@ -163,6 +163,10 @@ SHARD_CONFIGS = {
     "4-32": dict(name="config4 (W=32): Word2Vec rows, FloatMatrixStore shard 1250000x200 fp32, 32 full-range pushes",
                  rows=1_250_000, cols=200, W=32, nrec=1_250_000, vt=1, ada=None, seed0=3000, mult=7919, init=13,
                  steps=5),
+    "4-asc": dict(name="config4 with every push in ascending row order (Java HashMap<Integer> iteration): "
+                       "FloatMatrixStore shard 1250000x200 fp32, 8 full-range pushes",
+                  rows=1_250_000, cols=200, W=8, nrec=1_250_000, vt=1, ada=None, seed0=3000, mult=7919, init=13,
+                  steps=10, asc=True),
     "4-ada": dict(name="config4 AdaGrad variant: FloatMatrixStoreAdaGrad shard 1250000x200 fp32 (data + alpha + "
                        "delta), 8 full-range pushes",
                   rows=1_250_000, cols=200, W=8, nrec=1_250_000, vt=1, ada=(0.025, 0.0001, 1.0), seed0=3000,
@@ -178,6 +182,8 @@ def _coprime(a, n):
 
 
 def _shard_perms(c):
+    if c.get("asc"):
+        return [(1, 0)] * c["W"]
     return [(_coprime((c["seed0"] + b) * 2654435761 % c["rows"] | 1, c["rows"]), b * c["mult"] % c["rows"])
             for b in range(c["W"])]
 
@@ -302,7 +308,7 @@ def main():
     ap.add_argument("--pieces", type=int, default=4, help="pre-reduce row slices per call (sharded path)")
     ap.add_argument("--group", action="store_true",
                     help="use the sharded pre-reduce/reduce-scatter path even at N=1 (path check)")
-    ap.add_argument("--config", choices=["2", "4", "4-32", "4-ada", "5"], default="2",
+    ap.add_argument("--config", choices=["2", "4", "4-32", "4-asc", "4-ada", "5"], default="2",
                     help="2 = the headline (default); 4, 4-32, 4-ada, 5 = one GPU's shard of those 8-GPU configs")
     ap.add_argument("--cpu-seconds", type=float, default=8.0, help="CPU baseline budget for --config 4/5")
     args = ap.parse_args()
