@@ -838,3 +838,32 @@ def test_native_group_exchange_world1(oracle):
         assert np.array_equal(g.store.values(), o.data)
     finally:
         g.close()
+
+
+def test_native_group_exchange_float_array(oracle):
+    """The exact exchange path for a sparse FloatArrayStore (config 3's store type,
+    LONG keys) through the native group at world 1: repeated and out-of-matrix keys,
+    bit-exact against the oracle fed the in-matrix records in push order."""
+    from distml_amd import DataDesc, encode_array_push
+    from distml_amd.group import NativeShardGroup
+    dim = 1_000_000
+    fmt = DataDesc(0, 1, 1)
+    g = NativeShardGroup(fmt, dim, 1, 0, 1, NativeShardGroup.unique_id(), device=0)
+    rng = np.random.default_rng(123)
+    try:
+        host = []
+        for b in range(5):
+            keys = rng.integers(-10, dim + 10, size=50_000)  # repeats inside a push, some outside the matrix
+            host.append(encode_array_push(keys, rng.standard_normal(len(keys)).astype(np.float32), 1, 1))
+        dev = [torch.frombuffer(bytearray(h), dtype=torch.uint8).cuda() for h in host]
+        torch.cuda.synchronize()
+        g.push_exchange([d.data_ptr() for d in dev], [d.numel() for d in dev])
+        g.flush()
+        o = oracle_store(oracle, fmt, 0, dim - 1)
+        for h in host:
+            r = np.frombuffer(h, np.uint8).reshape(-1, 12)
+            k = r[:, :8].copy().view("<i8").ravel()
+            assert o.push(r[(k >= 0) & (k < dim)].tobytes()) == 0
+        assert kat.bits_equal(g.store.values(), o.data)
+    finally:
+        g.close()
