@@ -167,6 +167,9 @@ SHARD_CONFIGS = {
                        "FloatMatrixStore shard 1250000x200 fp32, 8 full-range pushes",
                   rows=1_250_000, cols=200, W=8, nrec=1_250_000, vt=1, ada=None, seed0=3000, mult=7919, init=13,
                   steps=10, asc=True),
+    "4-256": dict(name="config4 shape probe: FloatMatrixStore shard 1250000x256 fp32 (whole 1-KiB rows), 8 full-range "
+                       "pushes", rows=1_250_000, cols=256, W=8, nrec=1_250_000, vt=1, ada=None, seed0=3000, mult=7919,
+                  init=13, steps=10),
     "4-ada": dict(name="config4 AdaGrad variant: FloatMatrixStoreAdaGrad shard 1250000x200 fp32 (data + alpha + "
                        "delta), 8 full-range pushes",
                   rows=1_250_000, cols=200, W=8, nrec=1_250_000, vt=1, ada=(0.025, 0.0001, 1.0), seed0=3000,
@@ -308,7 +311,7 @@ def main():
     ap.add_argument("--pieces", type=int, default=4, help="pre-reduce row slices per call (sharded path)")
     ap.add_argument("--group", action="store_true",
                     help="use the sharded pre-reduce/reduce-scatter path even at N=1 (path check)")
-    ap.add_argument("--config", choices=["2", "4", "4-32", "4-asc", "4-ada", "5"], default="2",
+    ap.add_argument("--config", choices=["2", "4", "4-32", "4-asc", "4-256", "4-ada", "5"], default="2",
                     help="2 = the headline (default); 4, 4-32, 4-ada, 5 = one GPU's shard of those 8-GPU configs")
     ap.add_argument("--cpu-seconds", type=float, default=8.0, help="CPU baseline budget for --config 4/5")
     args = ap.parse_args()

@@ -252,6 +252,9 @@ class ShardGroup:
                     ls.append(ln)
                 off += ln
         if ptrs:
+            if len(self._xbufs) >= 2:  # bound the receive buffers held for the asynchronous store
+                self.store.flush()     # (a deferred error of an earlier call surfaces here)
+                self._xbufs.clear()
             self.store.pushDevice(ptrs, ls)
             self._xbufs.append(recv)  # alive until the store has consumed it (flush)
 
