@@ -18,7 +18,8 @@ except Exception:  # pragma: no cover - torch is optional for the C-ABI itself
     torch = None
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(_HERE, "libdistml_ps.so")
+# DML_LIB_PATH: an alternative build of the same library (A/B runs of build-time variants)
+LIB_PATH = os.environ.get("DML_LIB_PATH") or os.path.join(_HERE, "libdistml_ps.so")
 _lib = None
 
 

@@ -309,9 +309,12 @@ __global__ __launch_bounds__(256) void k_sp_bounds(const SpPlan pl, const SpMeta
 // owners of repeated rows walk their bucket in ascending comp order. Buckets
 // over kSpBucketMax records (adversarial keys) send the whole leaf to the exact
 // replay before any of its rows is written.
-constexpr int kSpLines = 1024;
+#ifndef DML_SP_LEAF_THREADS
+#define DML_SP_LEAF_THREADS 512  // 8 waves per leaf (A/B builds override)
+#endif
+constexpr int kSpLeafThreads = DML_SP_LEAF_THREADS;
+constexpr int kSpLines = 2 * kSpLeafThreads;
 constexpr int kSpBucketMax = 64;
-constexpr int kSpLeafThreads = 512;  // 8 waves per leaf
 
 template <typename T>
 __global__ __launch_bounds__(kSpLeafThreads) void k_sp_leaf(T* __restrict__ shard, const int64_t* __restrict__ bounds,
