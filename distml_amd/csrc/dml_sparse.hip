@@ -586,6 +586,11 @@ SpPlan sparse_plan(const Batch& bt, int nb, int64_t rows) {
     const double span = (double)(kSpLeafCap / 2) * (double)rows / (double)std::max<int64_t>(nrec, 1);
     int SL = 0;
     while (SL < 31 && (double)((int64_t)1 << (SL + 1)) <= span) ++SL;
+    static const int sl_bias = [] {  // A/B knob: leaves 2^bias times larger
+        const char* v = getenv("DML_SP_SL_BIAS");
+        return v ? atoi(v) : 0;
+    }();
+    SL = std::max(0, std::min(31, SL + sl_bias));
     while (SL < 31 && ((rows + ((int64_t)1 << SL) - 1) >> SL) > 65536) ++SL;
     pl.SL = SL;
     pl.nleaves = (rows + ((int64_t)1 << SL) - 1) >> SL;
