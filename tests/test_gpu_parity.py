@@ -867,3 +867,49 @@ def test_native_group_exchange_float_array(oracle):
         assert kat.bits_equal(g.store.values(), o.data)
     finally:
         g.close()
+
+
+@pytest.mark.parametrize("kind", ["f32_matrix", "i32_matrix", "adagrad", "f64_matrix", "f32_array", "i32_array",
+                                  "f64_array"])
+@pytest.mark.parametrize("api", ["batch", "sequential", "device"])
+def test_empty_and_single_record_pushes(oracle, kind, api):
+    """Zero-length pushes (handlePush's record loop never runs: a no-op in the reference,
+    e.g. FloatMatrixStore.java:200-208) at the start, middle and end of a batch, and
+    one-record pushes, leave exactly the oracle's state."""
+    from distml_amd import DataDesc, encode_array_push, encode_matrix_push
+    rng = np.random.default_rng(sum(map(ord, kind + api)))
+    vt = {"f32": 1, "i32": 0, "f64": 3, "adagrad": 1}[kind.split("_")[0]]
+    matrix = not kind.endswith("array")
+    cols = 6 if matrix else 1
+    first, rows = 50, 40
+    fmt = DataDesc(1 if matrix else 0, 0, vt, False, True, kind == "adagrad")
+    s, _ = mk_store(fmt, first, first + rows - 1, cols)
+    o = oracle_store(oracle, fmt, first, first + rows - 1, cols)
+    init = (rng.integers(100, 200, size=(rows, cols)).astype(np.int32) if vt == 0
+            else rng.standard_normal((rows, cols)).astype(s.dtype))
+    s.load_values(init)
+    o.data[:] = init
+
+    def push(keys):
+        v = (rng.integers(-3, 4, size=(len(keys), cols)) if vt == 0 else rng.standard_normal((len(keys), cols)))
+        if matrix:
+            return encode_matrix_push(first + keys, v, 0, vt)
+        return encode_array_push(first + keys, v[:, 0], 0, vt)
+
+    pushes = [b"", push(np.array([7])), b"", push(rng.choice(rows, 25, replace=False)), push(np.array([rows - 1])),
+              b""]
+    for p in pushes:
+        assert o.push(p) == 0
+    if api == "batch":
+        s.handlePushBatch(fmt, pushes)
+    elif api == "sequential":
+        for p in pushes:
+            s.handlePush(fmt, p)
+    else:
+        bufs = [torch.frombuffer(bytearray(p), dtype=torch.uint8).cuda() if p else
+                torch.empty(0, dtype=torch.uint8, device="cuda") for p in pushes]
+        torch.cuda.synchronize()
+        s.pushDevice([b.data_ptr() for b in bufs], [b.numel() for b in bufs])
+        s.flush()
+    assert kat.bits_equal(s.values(), o.data)
+    s.close()
