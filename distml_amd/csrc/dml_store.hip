@@ -118,6 +118,8 @@ struct dml_store {
     int64_t cand_n = 0;
     MaxDelta* md = nullptr;
     float initial_alpha = 0.f, min_alpha = 0.f, factor = 1.5f;  // :22, :26
+    uint32_t* mark = nullptr;   // int32 arrays: per-element token of the last push that added to it
+    uint32_t mark_tok = 0;
     Workspace ws[kRing];
     size_t slot_bytes = 0, ws_bytes = 0;
     int next_ws = 0;
@@ -356,8 +358,17 @@ int launch_apply(dml_store* s, Chunk& c, Workspace& W, const Ctrl* prev) {
                 ev = {p.first, p.second};
                 s->ev_used.push_back(p);
             }
+            uint32_t tok = 0;
+            if (s->mark) {
+                if (++s->mark_tok == 0) {  // tokens wrapped: forget every stamp
+                    HIPCHK(hipMemsetAsync(s->mark, 0, (size_t)s->rows * sizeof(uint32_t), s->stream));
+                    s->mark_tok = 1;
+                }
+                tok = s->mark_tok;
+            }
             HIPCHK(launch_array_apply(vtype_of(s->desc), s->data, s->rows, c.bt.base[b], c.bt.nrec[b], c.bt.bidx[b],
-                                      s->stride, s->K, s->first, W.ctrl, c.tail_cut, prev, s->stream, ev));
+                                      s->stride, s->K, s->first, W.ctrl, c.tail_cut, prev, s->stream, ev, s->mark,
+                                      tok));
         }
         HIPCHK(hipEventRecord(W.applied, s->stream));
     }
@@ -570,6 +581,15 @@ int retire_front(dml_store* s) {
     if (s->is_matrix && ctl.no_dup == 0u) {
         rc = replay_rows(s, c, W, &ctl);
         if (rc) return rc;
+    } else if (!s->is_matrix && ctl.no_dup == 0u && s->mark) {
+        // an int32 push repeated a key: the atomics' order decided which add saw a
+        // negative counter; re-run the chunk in record order for the exact first one
+        const uint64_t cut = std::min<uint64_t>(ctl.cutoff, c.tail_cut);
+        HIPCHK(launch_array_exact_i32((int32_t*)s->data, s->rows, c.bt, c.nb, s->stride, s->K, s->first, cut, W.ctrl,
+                                      s->stream));
+        HIPCHK(hipMemcpyAsync(&ctl.neg_pos, &W.ctrl->neg_pos, sizeof(ctl.neg_pos), hipMemcpyDeviceToHost,
+                              s->stream));
+        HIPCHK(hipStreamSynchronize(s->stream));
     } else if (!s->is_matrix && ctl.no_dup == 0u) {
         // leaves too large for the LDS sort were skipped by the leaf kernel: apply them exactly
         HIPCHK(sparse_replay(vtype_of(s->desc), s->data, c.sp, c.spl, W.sp, s->stream));
@@ -767,6 +787,11 @@ int dml_store_create_range(const dml_desc* desc, int64_t first_key, int64_t last
         if ((e = hipMalloc((void**)&s->md, sizeof(MaxDelta))) != hipSuccess) return fail(e, "md alloc");
         if ((e = hipMemsetAsync(s->md, 0, sizeof(MaxDelta), s->stream)) != hipSuccess) return fail(e, "md zero");
     }
+    if (!s->is_matrix && d.value_type == DML_ELEMENT_TYPE_INT) {
+        if ((e = hipMalloc((void**)&s->mark, (size_t)rows * sizeof(uint32_t))) != hipSuccess) return fail(e, "mark alloc");
+        if ((e = hipMemsetAsync(s->mark, 0, (size_t)rows * sizeof(uint32_t), s->stream)) != hipSuccess)
+            return fail(e, "mark zero");
+    }
     s->slot_bytes = s->is_matrix ? (size_t)rows * kMaxW * sizeof(int32_t) : 0;
     s->ws_bytes = sizeof(Ctrl) + s->slot_bytes + (s->is_matrix ? (size_t)rows * sizeof(uint32_t) : 0);
     if ((e = prio_mode ? hipStreamCreateWithPriority(&s->istream, hipStreamNonBlocking, prio_least)
@@ -817,6 +842,7 @@ void dml_store_destroy(dml_store* s) {
         (void)hipFree(s->delta);
         (void)hipFree(s->cand);
         (void)hipFree(s->md);
+        (void)hipFree(s->mark);
         (void)hipFree(s->dstage);
         if (s->hstage) (void)hipHostFree(s->hstage);
         (void)hipFree(s->dscr);

@@ -913,3 +913,59 @@ def test_empty_and_single_record_pushes(oracle, kind, api):
         s.flush()
     assert kat.bits_equal(s.values(), o.data)
     s.close()
+
+
+@pytest.mark.parametrize("case", ["no_error", "hidden_negative", "late_negative", "async_batches"])
+def test_int_array_repeated_keys_exact_error_state(oracle, case):
+    """IntArrayStore pushes that list a key several times (legal bytes, never produced by
+    SparseArray.writeMap): the reference adds in record order and throws after the first add
+    that leaves a counter negative (IntArrayStore.java:294-310). Per-push atomics get the sums
+    right but not that position — e.g. 1 + (-2) + 5 is negative after the first add in record
+    order, never in the order (+5, -2). The store detects the repeat (per-element push tokens)
+    and re-runs the chunk in record order: data, error key and the no-further-pushes state
+    all equal the oracle's."""
+    from distml_amd import DataDesc, DistMLException, encode_array_push
+    rng = np.random.default_rng(hash(case) % 1000)
+    first, rows = 10, 3000
+    fmt = DataDesc(0, 0, 0)
+    init = rng.integers(30, 40, size=(rows, 1)).astype(np.int32)  # random walks stay >= 0
+    pushes = []
+    for b in range(5):
+        k = rng.integers(0, 400, size=2000)  # ~5 repeats of each key in every push
+        v = rng.integers(-1, 2, size=len(k))
+        pushes.append(encode_array_push(first + k, v, 0, 0))
+    if case == "hidden_negative":
+        init[2500, 0] = 1
+        pushes[2] = pushes[2] + encode_array_push(first + np.array([2500, 2500]), np.array([-2, 5]), 0, 0)
+    elif case == "late_negative":
+        init[1500, 0] = 3
+        k = np.array([1500] * 6 + [1501])
+        pushes[4] = encode_array_push(first + k, np.array([-1, -1, -1, -1, -1, -1, -1]), 0, 0) + pushes[4]
+    apis = ["batch", "sequential"] if case != "async_batches" else ["async"]
+    o = oracle_store(oracle, fmt, first, first + rows - 1)
+    o.data[:] = init
+    rc = 0
+    for p in pushes:
+        rc = o.push(p)
+        if rc:
+            break
+    assert (rc != 0) == (case in ("hidden_negative", "late_negative"))
+    for api in apis:
+        s, _ = mk_store(fmt, first, first + rows - 1, async_push=(api == "async"))
+        s.load_values(init)
+        if rc:
+            with pytest.raises(DistMLException) as ei:
+                if api == "batch":
+                    s.handlePushBatch(fmt, pushes)
+                else:
+                    for p in pushes:
+                        s.handlePush(fmt, p)
+            assert (ei.value.code, ei.value.key, ei.value.col) == o.error()
+        elif api == "async":
+            for i in range(0, len(pushes), 2):
+                s.handlePushBatch(fmt, pushes[i:i + 2])
+            s.flush()
+        else:
+            s.handlePushBatch(fmt, pushes) if api == "batch" else [s.handlePush(fmt, p) for p in pushes]
+        assert kat.bits_equal(s.values(), o.data)
+        s.close()
