@@ -287,6 +287,14 @@ def run_shard_config(which: str, cpu_s: float, no_cpu: bool) -> dict:
     return line
 
 
+def _pre_time(L, enable: bool, reset: bool):
+    """Pre-reduce piece timing of the sharded path (dml_prereduce_timing / _kernel_time)."""
+    ms, n = C.c_double(0.0), C.c_int64(0)
+    assert L.dml_prereduce_kernel_time(C.byref(ms), C.byref(n), 1 if reset else 0) == 0
+    assert L.dml_prereduce_timing(1 if enable else 0) == 0
+    return ms.value, n.value
+
+
 def load_traffic():
     p = os.path.join(ROOT, "profiles", "pmc_traffic.json")
     if not os.path.exists(p):
@@ -373,11 +381,14 @@ def main():
         timed_store = group.store
         algo_per_rank = W * BUCKET + 2 * group.shard.size() * COLS * 4
 
+    sharded = not (world == 1 and not args.group)
     for _ in range(args.warmup):
         step()
     finish()
     timed_store.set_timing(not args.no_timing)
     timed_store.kernel_time(reset=True)
+    if sharded and not args.no_timing:
+        _pre_time(L, enable=True, reset=True)
     barrier()
     t0 = time.perf_counter()
     for _ in range(args.steps):
@@ -387,6 +398,7 @@ def main():
     el = time.perf_counter() - t0
     k_ms, k_n = timed_store.kernel_time(reset=True)
     timed_store.set_timing(False)
+    pre_ms, pre_n = _pre_time(L, enable=False, reset=True) if sharded else (0.0, 0)
     t = torch.tensor([el], dtype=torch.float64, device="cuda")
     if world > 1:
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
@@ -418,9 +430,18 @@ def main():
                                 "launches": k_n, "measured_read_peak": round(pk["read"], 1),
                                 "frac_of_measured_read": round(achieved / pk["read"], 4),
                                 "measured_copy_peak": round(pk["copy"], 1)}
-        elif k_n > 0:
-            line["roofline"] = {"bound": "hbm", "achieved": None, "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                                "frac": None, "traffic": None, "note": "apply kernel only timed at N>1"}
+        elif pre_n > 0:
+            # sharded path: the pre-reduce pieces (k_reduce_rows in pre-reduce mode) are the
+            # dominant kernel; per call they read the W pushes and write the full-model partial
+            pre_bytes = W * BUCKET + world * group.step_rows * COLS * 4
+            calls = pre_n / args.pieces
+            avg_s = pre_ms / calls / 1e3
+            achieved = pre_bytes / avg_s / 1e9
+            line["roofline"] = {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS,
+                                "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": None,
+                                "kernel": f"k_reduce_rows pre-reduce ({args.pieces} pieces per call, rank 0)",
+                                "avg_kernel_us": round(avg_s * 1e6, 2), "launches": pre_n,
+                                "algorithmic_bytes_per_call": pre_bytes}
         if world == 1 and not args.group and args.sparse_steps > 0:
             del bufs
             line["sparse"] = sparse_leg(L, torch, args.sparse_steps)

@@ -21,6 +21,7 @@
 #include <cstdlib>
 #include <cstring>
 #include <deque>
+#include <atomic>
 #include <mutex>
 #include <string>
 #include <unordered_map>
@@ -1372,7 +1373,22 @@ struct dml_prereduce {
     hipEvent_t last_ev = nullptr;  // piece stream: last piece enqueued so far
     hipStream_t last_st = nullptr;
     bool idx_waited = false;
+    bool timed = false;
+    hipEvent_t done_ev = nullptr;  // completion of the last piece: last_ev, or its timing stop event
+    std::vector<std::pair<hipEvent_t, hipEvent_t>> tev;  // per-piece start/stop of a timed call
 };
+
+// Pre-reduce kernel timing (dml_prereduce_timing): one call in kPreSample gets
+// start/stop events in its pieces' dispatch packets (events in every packet
+// cost ~10 us per launch: 4 pieces per call would move the step time itself);
+// _end adds their elapsed time to the totals. Events come from a pool.
+constexpr int64_t kPreSample = 16;
+static std::atomic<bool> g_pre_timing{false};
+static std::atomic<int64_t> g_pre_calls{0};
+static std::mutex g_pre_mu;
+static double g_pre_ms = 0.0;
+static int64_t g_pre_launches = 0;
+static std::vector<std::pair<hipEvent_t, hipEvent_t>> g_pre_pool;
 
 static void prereduce_free(dml_prereduce* p) {
     if (p->idx_ev) (void)hipEventDestroy(p->idx_ev);
@@ -1445,6 +1461,8 @@ int dml_prereduce_begin(const dml_desc* desc, int64_t first_key, int64_t rows, i
         prereduce_free(p);
         return set_err(DML_E_HIP, hipGetErrorString(e));
     }
+    p->timed = g_pre_timing.load(std::memory_order_relaxed) &&
+               g_pre_calls.fetch_add(1, std::memory_order_relaxed) % kPreSample == 0;
     *out = p;
     return DML_OK;
 }
@@ -1469,8 +1487,26 @@ int dml_prereduce_piece(dml_prereduce* p, int64_t row_block, int64_t row_stride,
     AdaArgs none{};
     if (!p->last_ev) HIPCHK(hipEventCreateWithFlags(&p->last_ev, hipEventDisableTiming));
     // the piece's completion event rides in its dispatch packet (no marker packet between pieces)
+    LaunchEv ev{nullptr, p->last_ev};
+    if (p->timed) {
+        std::pair<hipEvent_t, hipEvent_t> t{nullptr, nullptr};
+        {
+            std::lock_guard<std::mutex> lk(g_pre_mu);
+            if (!g_pre_pool.empty()) {
+                t = g_pre_pool.back();
+                g_pre_pool.pop_back();
+            }
+        }
+        if (!t.first) {
+            HIPCHK(hipEventCreate(&t.first));
+            HIPCHK(hipEventCreate(&t.second));
+        }
+        p->tev.push_back(t);
+        ev = LaunchEv{t.first, t.second};
+    }
     HIPCHK(launch_reduce(p->desc.value_type, kPreReduce, dev_out, ntask_rows, p->cols, p->bt, p->nb, p->stride, p->K,
-                         p->slot, nullptr, p->ctrl, kNoPos, none, st, nullptr, LaunchEv{nullptr, p->last_ev}, rm));
+                         p->slot, nullptr, p->ctrl, kNoPos, none, st, nullptr, ev, rm));
+    p->done_ev = ev.stop;
     // model rows this piece covered: blocks of row_block task rows at row_off + q*row_stride
     for (int64_t t0 = 0; t0 < ntask_rows; t0 += row_block) {
         const int64_t lo = (t0 / row_block) * row_stride + row_off;
@@ -1481,9 +1517,26 @@ int dml_prereduce_piece(dml_prereduce* p, int64_t row_block, int64_t row_stride,
     return DML_OK;
 }
 
+int dml_prereduce_timing(int32_t enable) {
+    g_pre_timing.store(enable != 0);
+    return DML_OK;
+}
+
+int dml_prereduce_kernel_time(double* ms, int64_t* launches, int32_t reset) {
+    if (!ms || !launches) return set_err(DML_E_INVALID_ARG, "null output");
+    std::lock_guard<std::mutex> lk(g_pre_mu);
+    *ms = g_pre_ms;
+    *launches = g_pre_launches;
+    if (reset) {
+        g_pre_ms = 0.0;
+        g_pre_launches = 0;
+    }
+    return DML_OK;
+}
+
 int dml_prereduce_stream_wait(dml_prereduce* p, void* stream) {
-    if (!p || !p->last_ev) return set_err(DML_E_INVALID_ARG, "no piece enqueued yet");
-    HIPCHK(hipStreamWaitEvent((hipStream_t)stream, p->last_ev, 0));
+    if (!p || !p->done_ev) return set_err(DML_E_INVALID_ARG, "no piece enqueued yet");
+    HIPCHK(hipStreamWaitEvent((hipStream_t)stream, p->done_ev, 0));
     return DML_OK;
 }
 
@@ -1492,7 +1545,21 @@ int dml_prereduce_end(dml_prereduce* p) {
     hipError_t e = hipEventSynchronize(p->idx_ev);  // index done, Ctrl copied out
     const Ctrl h = *p->hctrl;
     // the workspace is free once the last piece ran
-    if (e == hipSuccess && p->last_ev) e = hipEventSynchronize(p->last_ev);
+    if (e == hipSuccess && p->done_ev) e = hipEventSynchronize(p->done_ev);
+    if (!p->tev.empty()) {
+        double ms = 0.0;
+        for (auto& t : p->tev) {
+            float x = 0.f;
+            if (e == hipSuccess && hipEventElapsedTime(&x, t.first, t.second) == hipSuccess) ms += x;
+        }
+        std::lock_guard<std::mutex> lk(g_pre_mu);
+        if (e == hipSuccess) {
+            g_pre_ms += ms;
+            g_pre_launches += (int64_t)p->tev.size();
+        }
+        g_pre_pool.insert(g_pre_pool.end(), p->tev.begin(), p->tev.end());
+        p->tev.clear();
+    }
     int rc = DML_OK;
     if (e != hipSuccess) rc = set_err(DML_E_HIP, hipGetErrorString(e));
     else if (h.cutoff != kNoPos) rc = set_err(DML_E_KEY_OUT_OF_SHARD, "pre-reduce: key outside the matrix");

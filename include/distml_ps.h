@@ -220,6 +220,11 @@ int dml_prereduce_end(dml_prereduce* p);
 /* Make `stream` wait (device side) for the pieces enqueued so far, e.g. the
  * communication stream that reduce-scatters the piece just written. */
 int dml_prereduce_stream_wait(dml_prereduce* p, void* stream);
+/* Measurement: with timing on, each piece carries start/stop events in its
+ * dispatch packet and _end adds their elapsed time to a process-wide total
+ * (bench.py's roofline of the sharded path; no reference counterpart). */
+int dml_prereduce_timing(int32_t enable);
+int dml_prereduce_kernel_time(double* ms, int64_t* launches, int32_t reset);
 
 /* --- per-shard split of device-resident pushes (multi-GPU exchange path) -- */
 
