@@ -323,8 +323,13 @@ def main():
                     help="2 = the headline (default); 4, 4-32, 4-ada, 5 = one GPU's shard of those 8-GPU configs")
     ap.add_argument("--cpu-seconds", type=float, default=8.0, help="CPU baseline budget for --config 4/5")
     args = ap.parse_args()
+    # stdout carries exactly the one JSON line: RCCL and other native libraries print
+    # banners to fd 1 (e.g. "RCCL version : ..."), so fd 1 goes to stderr for the run
+    sys.stdout.flush()
+    out = os.fdopen(os.dup(1), "w")
+    os.dup2(2, 1)
     if args.config != "2":
-        print(json.dumps(run_shard_config(args.config, args.cpu_seconds, args.no_cpu)), flush=True)
+        print(json.dumps(run_shard_config(args.config, args.cpu_seconds, args.no_cpu)), file=out, flush=True)
         return
 
     import torch
@@ -447,7 +452,7 @@ def main():
             line["sparse"] = sparse_leg(L, torch, args.sparse_steps)
         if world == 1 and not args.no_cpu and not args.group:
             line["cpu_baseline"] = cpu_baseline()
-        print(json.dumps(line), flush=True)
+        print(json.dumps(line), file=out, flush=True)
     if dist.is_initialized():
         dist.destroy_process_group()
 
