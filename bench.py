@@ -1,30 +1,49 @@
 """Benchmark: device-resident gradient-bucket reduce GiB/s (BASELINE.json metric).
 
-N=1 (default) — config 2 of BASELINE.json: a 16 384 x 1 024 fp32 shard (64 MiB,
-DataDesc MATRIX/INT/FLOAT dense) receives 32 pushes of 64 MiB each
+Headline (every N) — config 2 of BASELINE.json: a 16 384 x 1 024 fp32 model
+(64 MiB, DataDesc MATRIX/INT/FLOAT dense) receives 32 pushes of 64 MiB per GPU
 ([int32 key][1 024 x f32] x 16 384 records = 67 174 400 B), resident in HBM.
-One step = dml_store_push_batch_device(32 pushes): slot-table reset, key
-index kernel (side stream, overlapping the previous batch's reduce), the
-ordered multi-push reduce kernel, the error check; the timed region ends with
-flush() (every batch applied and error-checked) and a device synchronize.
-Algorithmic bytes per step = 32 x 67 174 400 + 2 x 67 108 864 = 2 283 798 528.
+  N=1: one shard; one step = dml_store_push_batch_device(32 pushes): key index
+       (side stream, overlapping the previous batch's reduce), the ordered
+       multi-push reduce, the error check; the timed region ends with flush().
+       Algorithmic bytes per step = 32 x 67 174 400 + 2 x 67 108 864.
+  N>1: weak scaling, one process per GPU, RCCL: every rank holds 32 full-range
+       pushes of the same model, whose rows are linearSplit over the N ranks
+       (KeyRange.java:68-80); step = ordered pre-reduce of the 32 local pushes,
+       RCCL reduce-scatter of the partials (pipelined in row slices), owner apply.
 
-N>1 (torchrun, one rank per GPU, RCCL) — weak scaling: every rank holds 32
-full-range pushes of the same 64 MiB model, whose rows are linearSplit over
-the N ranks; step = ordered pre-reduce of the 32 local pushes, RCCL
-reduce-scatter of the partials, owner apply.
+Legs reported in the same JSON line (same N, same process group):
+  "config4": BASELINE config 4, Word2Vec rows 10M x 200 fp32 (8 GB model),
+             W full-range pushes per GPU ([int32][200 x f32] = 804 B records);
+             N=1 one store, N>1 linearSplit + pre-reduce + reduce-scatter
+             (weak scaling: W pushes per GPU at every N).
+  "config5": BASELINE config 5, LDA IntMatrixStore 1M x 1000 int32 (4 GB),
+             32 pushes of 65 536 distinct vocabulary rows, split per shard the
+             way the reference's client splits them (SparseMatrix.java:46-60),
+             each shard's part applied by its owner with the negativity check
+             (strong scaling: the model and the pushes are fixed, N shards).
+  "sparse":  (N=1) config 3, 1e9-dim fp32 FloatArrayStore, 32 x 1e6 keys.
+  "cpu_baseline": (N=1, rank 0) the oracle's restatement of
+             FloatMatrixStore.updateRow on the same pushes, on this host's
+             cores: one thread (the reference's one selector thread per PS)
+             and all usable cores (row-partitioned).
 
-Also reported: the dominant kernel's HBM roofline (achieved from HIP events
-around every k_reduce launch, on the store's stream) and the CPU baseline
-(the oracle's restatement of FloatMatrixStore.updateRow, 1 thread, timed on
-this host on the same pushes).
+Without a launcher (`python bench.py --gpus N`, WORLD_SIZE unset) the script
+starts its N rank processes itself before any GPU call and prints rank 0's
+line; under torchrun it reads RANK / LOCAL_RANK / WORLD_SIZE.
+
+`--config 4|4-32|4-asc|4-256|4-ada|5` measures one GPU's shard of configs 4
+and 5 (the per-shard kernel numbers DESIGN.md §7 quotes), N=1 only.
 """
 from __future__ import annotations
 
 import argparse
 import ctypes as C
 import json
+import math
 import os
+import socket
+import subprocess
 import sys
 import time
 
@@ -36,11 +55,119 @@ sys.path.insert(0, ROOT)
 # (measured on the --group path: the next call's key index queued behind the pieces).
 os.environ.setdefault("GPU_MAX_HW_QUEUES", "8")
 
+METRIC = "device-resident gradient-bucket reduce GiB/s (dense fp32 + sparse scatter-add)"
 ROWS, COLS, W = 16384, 1024, 32
 REC = 4 + 4 * COLS
 BUCKET = ROWS * REC                      # 67 174 400 B
 SHARD = ROWS * COLS * 4                  # 67 108 864 B
 HBM_PEAK_GBS = 8000.0                    # MI355X_MICROARCH.md: HBM3E 8.0 TB/s (spec)
+
+C4_ROWS, C4_COLS = 10_000_000, 200       # Word2Vec rows (BASELINE config 4)
+C5_ROWS, C5_COLS, C5_W, C5_NNZ = 1_000_000, 1000, 32, 65536  # LDA word-topic counts (config 5)
+
+
+# ---------------------------------------------------------------- launcher
+def _free_port() -> int:
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def launch_ranks(n: int, argv) -> int:
+    """Start n rank processes of this script (one per GPU) when no launcher set
+    WORLD_SIZE. Nothing here touches the GPU. Rank 0's stdout (the JSON line)
+    passes through; the other ranks' stdout goes to stderr. If a rank fails, the
+    others are terminated (they may be blocked in a collective)."""
+    port = os.environ.get("MASTER_PORT") or str(_free_port())
+    procs = []
+    for r in range(n):
+        env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(n), LOCAL_WORLD_SIZE=str(n),
+                   GROUP_RANK="0", MASTER_ADDR="127.0.0.1", MASTER_PORT=port)
+        procs.append(subprocess.Popen([sys.executable, os.path.abspath(__file__)] + list(argv), env=env,
+                                      stdout=None if r == 0 else sys.stderr.fileno()))
+    rc = 0
+    alive = list(procs)
+    while alive:
+        for p in list(alive):
+            c = p.poll()
+            if c is None:
+                continue
+            alive.remove(p)
+            if c != 0 and rc == 0:
+                rc = c if c > 0 else 128 - c
+                for q in alive:
+                    q.terminate()
+        time.sleep(0.05)
+    return rc
+
+
+class Ctx:
+    """Rank context: barrier, max over ranks, rank 0 output."""
+
+    def __init__(self, torch, dist, world: int, rank: int, local: int):
+        self.torch, self.dist, self.world, self.rank, self.local = torch, dist, world, rank, local
+
+    def barrier(self):
+        if self.world > 1:
+            self.dist.barrier()
+        self.torch.cuda.synchronize()
+
+    def max(self, x: float) -> float:
+        if self.world == 1:
+            return x
+        t = self.torch.tensor([x], dtype=self.torch.float64, device="cuda")
+        self.dist.all_reduce(t, op=self.dist.ReduceOp.MAX)
+        return float(t.item())
+
+
+def timed_steps(ctx: Ctx, step, finish, steps: int, warmup: int, ramp_s: float = 0.0, reset=None) -> float:
+    """W untimed warmup steps (plus, if they took less than ramp_s, as many more as
+    fill it: a GPU that sat idle through start-up runs ~5 % slow for the first
+    milliseconds), then EXACTLY `steps` steps between barrier + synchronize pairs.
+    `reset` (e.g. the kernel-timing counters) runs right before the timed region.
+    Returns the max over ranks of the timed region's wall time."""
+    t0 = time.perf_counter()
+    for _ in range(warmup):
+        step()
+    finish()
+    ctx.torch.cuda.synchronize()
+    el = time.perf_counter() - t0
+    extra = 0
+    if ramp_s > el:
+        per = el / max(warmup, 1)
+        extra = int(min(ctx.max(math.ceil((ramp_s - el) / max(per, 1e-6))), 100_000))
+    for _ in range(extra):
+        step()
+    finish()
+    if reset is not None:
+        reset()
+    ctx.barrier()
+    t0 = time.perf_counter()
+    for _ in range(steps):
+        step()
+    finish()
+    ctx.barrier()
+    return ctx.max(time.perf_counter() - t0)
+
+
+# ---------------------------------------------------------------- host / CPU baseline
+def host_info() -> dict:
+    model = "unknown"
+    try:
+        for ln in open("/proc/cpuinfo"):
+            if ln.startswith("model name"):
+                model = ln.split(":", 1)[1].strip()
+                break
+    except OSError:
+        pass
+    usable = len(os.sched_getaffinity(0)) if hasattr(os, "sched_getaffinity") else os.cpu_count()
+    # the GPU box gives one GPU's job a 16-CPU share (OMP_NUM_THREADS), while nproc shows the machine
+    share = int(os.environ.get("OMP_NUM_THREADS", "0") or 0)
+    threads = min(usable, share) if share > 0 else usable
+    return {"cpu_model": model, "nproc": os.cpu_count(), "usable_cpus": usable, "omp_num_threads": share or None,
+            "threads_used_all_cores": threads}
 
 
 def perm_for(b: int):
@@ -48,6 +175,52 @@ def perm_for(b: int):
     return (1, 0) if b % 2 == 0 else (((2 * b + 1) * 2654435761) % ROWS | 1, (b * 7919) % ROWS)
 
 
+def cpu_baseline(budget_s: float = 8.0, all_s: float = 4.0):
+    """Oracle (C restatement of FloatMatrixStore.updateRow) on the same 32 x 64 MiB
+    pushes: one thread until `budget_s`, then all usable cores (row-partitioned, each
+    thread scanning every record in push order) until `all_s`."""
+    sys.path.insert(0, os.path.join(ROOT, "oracle"))
+    import pyoracle
+    bufs = [pyoracle.synth_dense_bucket(0, 1, 0, ROWS, ROWS, COLS, 1000 + b, *perm_for(b)) for b in range(W)]
+    o = pyoracle.OracleStore(1, 0, 1, 0, ROWS - 1, COLS)
+    o.synth_fill(7)
+    algo = W * BUCKET + 2 * SHARD
+    host = host_info()
+
+    def run(threads, budget):
+        reps, t0 = 0, time.perf_counter()
+        while True:
+            assert o.push_many(bufs, threads=threads) == 0
+            reps += 1
+            el = time.perf_counter() - t0
+            if el >= budget or reps >= 50:
+                return reps, el
+
+    reps, el = run(1, budget_s)
+    nt = host["threads_used_all_cores"]
+    reps_a, el_a = run(nt, all_s)
+    return {"value": round(reps * algo / el / 2**30, 3), "unit": "GiB/s", "cores": 1, "kind": "port",
+            "sample": f"full config-2 workload (32 x 64 MiB pushes -> 16384x1024 fp32 shard) x{reps} reps, "
+                      f"{el:.1f} s, oracle/dml_oracle.c single thread",
+            "all_cores": {"value": round(reps_a * algo / el_a / 2**30, 3), "unit": "GiB/s", "cores": nt,
+                          "sample": f"same workload x{reps_a} reps, {el_a:.1f} s, rows partitioned over {nt} threads"},
+            "host": host}
+
+
+def _coprime(a, n):
+    while math.gcd(a, n) != 1:
+        a += 1
+    return a
+
+
+def _sparse_perm(b, dim):
+    pa = (2 * b + 3) * 999_999_937 % dim
+    while pa % 2 == 0 or pa % 5 == 0:
+        pa += 1
+    return pa, (b * 12_345_701) % dim
+
+
+# ---------------------------------------------------------------- config 2
 def make_buckets(L, torch, fmt, n, rows_total):
     st = torch.cuda.current_stream().cuda_stream
     bufs = []
@@ -62,69 +235,125 @@ def make_buckets(L, torch, fmt, n, rows_total):
     return bufs
 
 
-def cpu_baseline(budget_s: float = 12.0):
-    """Oracle (C restatement of FloatMatrixStore.updateRow, single thread) on the
-    same 32 x 64 MiB pushes, repeated until `budget_s` of CPU work."""
-    sys.path.insert(0, os.path.join(ROOT, "oracle"))
-    import pyoracle
-    bufs = [pyoracle.synth_dense_bucket(0, 1, 0, ROWS, ROWS, COLS, 1000 + b, *perm_for(b)) for b in range(W)]
-    o = pyoracle.OracleStore(1, 0, 1, 0, ROWS - 1, COLS)
-    o.synth_fill(7)
-    reps, t0 = 0, time.perf_counter()
-    while True:
-        assert o.push_many(bufs, threads=1) == 0
-        reps += 1
-        el = time.perf_counter() - t0
-        if el >= budget_s or reps >= 50:
-            break
-    algo = W * BUCKET + 2 * SHARD
-    return {"value": round(reps * algo / el / 2**30, 3), "unit": "GiB/s", "cores": 1, "kind": "port",
-            "sample": f"full config-2 workload (32 x 64 MiB pushes -> 16384x1024 fp32 shard) x{reps} reps, "
-                      f"{el:.1f} s, oracle/dml_oracle.c single thread"}
+def _pre_time(L, enable: bool, reset: bool):
+    """Pre-reduce piece timing of the sharded path (dml_prereduce_timing / _kernel_time)."""
+    ms, n = C.c_double(0.0), C.c_int64(0)
+    assert L.dml_prereduce_kernel_time(C.byref(ms), C.byref(n), 1 if reset else 0) == 0
+    assert L.dml_prereduce_timing(1 if enable else 0) == 0
+    return ms.value, n.value
 
 
-def sparse_leg(L, torch, steps: int):
-    """Config 3 (reported beside the headline): 1e9-dim fp32 FloatArrayStore shard
-    (4 GB), 32 device-resident pushes x 1e6 unique keys ([int64 key][f32] = 12 B),
-    ordered per-push scatter-add. Algorithmic bytes per step = 32 x 12e6 + 2 x 4 x 32e6."""
+def load_traffic(key: str = "config2"):
+    p = os.path.join(ROOT, "profiles", "pmc_traffic.json")
+    if not os.path.exists(p):
+        return None
+    try:
+        d = json.load(open(p))
+    except Exception:
+        return None
+    if key == "config2":
+        return d.get("hbm_bytes_per_launch")
+    return (d.get("per_config") or {}).get(key, {}).get("hbm_bytes_per_launch")
+
+
+def prereduce_roofline(L, ctx, pieces, pre_ms, pre_n, pre_bytes, label):
+    calls = pre_n / pieces
+    avg_s = pre_ms / calls / 1e3
+    achieved = pre_bytes / avg_s / 1e9
+    return {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+            "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": None,
+            "kernel": f"k_reduce_rows pre-reduce ({pieces} pieces per call, rank {ctx.rank}; {label})",
+            "avg_kernel_us": round(avg_s * 1e6, 2), "launches": pre_n, "algorithmic_bytes_per_call": pre_bytes}
+
+
+def headline(ctx: Ctx, L, args, out_line: dict):
+    torch = ctx.torch
     from distml_amd import DataDesc, DataStore, KeyRange
+    from distml_amd.group import ShardGroup
     from distml_amd.store import DeviceBatch
-    dim, nnz, w = 10**9, 10**6, 32
-    fmt = DataDesc(DataDesc.DATA_TYPE_ARRAY, DataDesc.KEY_TYPE_LONG, DataDesc.ELEMENT_TYPE_FLOAT)
-    store = DataStore(fmt, KeyRange(0, dim - 1))
-    bufs = []
-    st = torch.cuda.current_stream().cuda_stream
-    for b in range(w):
-        pa = (2 * b + 3) * 999_999_937 % dim
-        while pa % 2 == 0 or pa % 5 == 0:
-            pa += 1
-        t = torch.empty(nnz * 12, dtype=torch.uint8, device="cuda")
-        assert L.dml_synth_sparse_bucket(t.data_ptr(), C.byref(fmt.to_c()), 0, dim, nnz, 2000 + b, pa,
-                                         (b * 12_345_701) % dim, C.c_void_p(st)) == 0
-        bufs.append(t)
-    torch.cuda.synchronize()
-    batch = DeviceBatch([b.data_ptr() for b in bufs], [b.numel() for b in bufs])
-    for _ in range(max(2, steps)):  # warmup: as many untimed steps as timed ones
-        store.pushDevice(batch)
-    store.flush()
-    store.set_timing(True)
-    store.kernel_time(reset=True)
-    torch.cuda.synchronize()
+    world, rank = ctx.world, ctx.rank
+    fmt = DataDesc(DataDesc.DATA_TYPE_MATRIX, DataDesc.KEY_TYPE_INT, DataDesc.ELEMENT_TYPE_FLOAT)
+    sharded = world > 1 or args.group
+    group = None
+    if not sharded:
+        store = DataStore(fmt, KeyRange(0, ROWS - 1), COLS, device=ctx.local)
+        store.rand(7)
+        bufs = make_buckets(L, torch, fmt, W, ROWS)
+        batch = DeviceBatch([b.data_ptr() for b in bufs], [b.numel() for b in bufs])
+
+        def step():
+            # async: ack once captured; the store keeps <= 2 batches in flight and the
+            # key index of batch k+1 overlaps the reduce of batch k
+            store.pushDevice(batch)
+
+        finish = store.flush  # every pushed batch applied and error-checked
+        timed_store = store
+        algo_per_rank = W * BUCKET + 2 * SHARD
+    else:
+        group = ShardGroup(fmt, ROWS, COLS, rank, world, device=ctx.local, pieces=args.pieces)
+        bufs = make_buckets(L, torch, fmt, W, ROWS)
+        ptrs, lens = [b.data_ptr() for b in bufs], [b.numel() for b in bufs]
+        st = torch.cuda.current_stream().cuda_stream
+
+        def step():
+            group.push_full_range(ptrs, lens, st)
+
+        finish = group.flush
+        timed_store = group.store
+        algo_per_rank = W * BUCKET + 2 * group.shard.size() * COLS * 4
+
+    timing = not args.no_timing
+    timed_store.set_timing(timing and not sharded)
     t0 = time.perf_counter()
-    for _ in range(steps):
-        store.pushDevice(batch)
-    store.flush()
-    torch.cuda.synchronize()
-    el = time.perf_counter() - t0
-    k_ms, k_n = store.kernel_time(reset=True)
-    algo = w * nnz * 12 + 2 * 4 * w * nnz
-    out = {"workload": "config3: 1e9-dim fp32 array shard, 32 pushes x 1e6 unique int64 keys, ordered scatter-add",
-           "value": round(steps * algo / el / 2**30, 2), "unit": "GiB/s (algorithmic)", "steps": steps,
-           "ms_per_step": round(el / steps * 1e3, 3), "algorithmic_bytes_per_step": algo,
-           "apply_kernel_us_avg": round(k_ms / max(k_n, 1) * 1e3, 2), "apply_launches": k_n}
-    store.close()
+    for _ in range(args.warmup):
+        step()
+    finish()
+
+    def reset():
+        timed_store.kernel_time(reset=True)
+        if sharded and timing:
+            _pre_time(L, enable=True, reset=True)
+
+    el = timed_steps(ctx, step, finish, args.steps, 0, ramp_s=max(0.0, 0.3 - (time.perf_counter() - t0)),
+                     reset=reset)
+    k_ms, k_n = timed_store.kernel_time(reset=True)
+    timed_store.set_timing(False)
+    pre_ms, pre_n = _pre_time(L, enable=False, reset=True) if sharded else (0.0, 0)
+    value = algo_per_rank * world * args.steps / el / 2**30
+    out_line.update({
+        "metric": METRIC, "value": round(value, 2), "unit": "GiB/s", "n_gpus": world, "steps": args.steps,
+        "warmup": args.warmup, "ms_per_step": round(el / args.steps * 1e3, 4), "higher_is_better": True,
+        "scaling": "weak", "vs_baseline": None, "dtype": "f32", "data": "synthetic",
+        "config": {"workload": "config2: dense fp32 reduce, 32 device-resident pushes x 64 MiB "
+                               "([int32 key][1024 x f32] x 16384) -> 16384x1024 fp32 model per GPU",
+                   "pushes_per_gpu": W, "push_bytes": BUCKET, "model_rows": ROWS, "cols": COLS,
+                   "parallelism": ("single shard" if not sharded else f"linearSplit({world}) + RCCL reduce-scatter"),
+                   "algorithmic_bytes_per_step_per_gpu": algo_per_rank},
+    })
+    if not sharded and k_n > 0:
+        avg_s = k_ms / k_n / 1e3
+        achieved = algo_per_rank / avg_s / 1e9
+        pk = stream_peaks(L, torch)
+        out_line["roofline"] = {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS,
+                                "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4),
+                                "traffic": load_traffic("config2"),
+                                "kernel": "k_reduce_rows<float,kAdd> (2 rows x 4 KiB per wave)",
+                                "avg_kernel_us": round(avg_s * 1e6, 2), "launches": k_n,
+                                "measured_read_peak": round(pk["read"], 1),
+                                "frac_of_measured_read": round(achieved / pk["read"], 4),
+                                "measured_copy_peak": round(pk["copy"], 1)}
+    elif pre_n > 0:
+        # the pre-reduce pieces (k_reduce_rows in pre-reduce mode) are the dominant
+        # kernel; per call they read the W pushes and write the full-model partial
+        out_line["roofline"] = prereduce_roofline(L, ctx, args.pieces, pre_ms, pre_n,
+                                                  W * BUCKET + world * group.step_rows * COLS * 4, "config 2")
+    if group is not None:
+        group.close()
+    else:
+        store.close()
     del bufs
-    return out
+    torch.cuda.synchronize()
+    torch.cuda.empty_cache()
 
 
 def stream_peaks(L, torch, nbytes: int = 1 << 31, reps: int = 5):
@@ -147,7 +376,230 @@ def stream_peaks(L, torch, nbytes: int = 1 << 31, reps: int = 5):
     return out
 
 
-# ---------------------------------------------------------------- configs 4 and 5
+# ---------------------------------------------------------------- config 3 (N=1)
+def sparse_leg(ctx: Ctx, L, steps: int, cpu: bool):
+    """Config 3 (reported beside the headline): 1e9-dim fp32 FloatArrayStore shard
+    (4 GB), 32 device-resident pushes x 1e6 unique keys ([int64 key][f32] = 12 B),
+    ordered per-push scatter-add. Algorithmic bytes per step = 32 x 12e6 + 2 x 4 x 32e6."""
+    torch = ctx.torch
+    from distml_amd import DataDesc, DataStore, KeyRange
+    from distml_amd.store import DeviceBatch
+    dim, nnz, w = 10**9, 10**6, 32
+    fmt = DataDesc(DataDesc.DATA_TYPE_ARRAY, DataDesc.KEY_TYPE_LONG, DataDesc.ELEMENT_TYPE_FLOAT)
+    store = DataStore(fmt, KeyRange(0, dim - 1), device=ctx.local)
+    bufs = []
+    st = torch.cuda.current_stream().cuda_stream
+    for b in range(w):
+        t = torch.empty(nnz * 12, dtype=torch.uint8, device="cuda")
+        assert L.dml_synth_sparse_bucket(t.data_ptr(), C.byref(fmt.to_c()), 0, dim, nnz, 2000 + b,
+                                         *_sparse_perm(b, dim), C.c_void_p(st)) == 0
+        bufs.append(t)
+    torch.cuda.synchronize()
+    batch = DeviceBatch([b.data_ptr() for b in bufs], [b.numel() for b in bufs])
+    store.set_timing(True)
+
+    def step():
+        store.pushDevice(batch)
+
+    for _ in range(max(2, steps)):  # warmup: as many untimed steps as timed ones
+        step()
+    store.flush()
+    store.kernel_time(reset=True)
+    el = timed_steps(ctx, step, store.flush, steps, 0)
+    k_ms, k_n = store.kernel_time(reset=True)
+    algo = w * nnz * 12 + 2 * 4 * w * nnz
+    out = {"workload": "config3: 1e9-dim fp32 array shard, 32 pushes x 1e6 unique int64 keys, ordered scatter-add",
+           "value": round(steps * algo / el / 2**30, 2), "unit": "GiB/s (algorithmic)", "steps": steps,
+           "ms_per_step": round(el / steps * 1e3, 3), "algorithmic_bytes_per_step": algo,
+           "apply_kernel_us_avg": round(k_ms / max(k_n, 1) * 1e3, 2), "apply_launches": k_n}
+    store.close()
+    del bufs
+    torch.cuda.empty_cache()
+    if cpu:
+        sys.path.insert(0, os.path.join(ROOT, "oracle"))
+        import pyoracle
+        o = pyoracle.OracleStore(0, 1, 1, 0, dim - 1)
+        n, spent = 0, 0.0
+        while n < w and spent < 6.0:
+            buf = pyoracle.synth_sparse_bucket(1, 1, 0, dim, nnz, 2000 + n, *_sparse_perm(n, dim))
+            t1 = time.perf_counter()
+            assert o.push(buf) == 0
+            spent += time.perf_counter() - t1
+            n += 1
+        o.close()
+        out["cpu_baseline"] = {"value": round(n * (nnz * 12 + 2 * 4 * nnz) / spent / 2**30, 3),
+                               "unit": "GiB/s (algorithmic)", "cores": 1, "kind": "port",
+                               "sample": f"first {n} of the 32 pushes into the 4 GB host array in {spent:.1f} s, "
+                                         f"oracle/dml_oracle.c FloatArrayStore restatement, single thread"}
+    return out
+
+
+# ---------------------------------------------------------------- config 4 (model level)
+def leg_config4(ctx: Ctx, L, args) -> dict:
+    """BASELINE config 4: Word2Vec rows 10M x 200 fp32, W full-range pushes per GPU.
+    N=1: one store, the ordered batch reduce. N>1: linearSplit(N) shards, ordered
+    pre-reduce of the W local pushes, RCCL reduce-scatter, owner apply (plain
+    FloatMatrixStore sum, the config's metric; weak scaling: W pushes per GPU)."""
+    torch = ctx.torch
+    from distml_amd import DataDesc, DataStore, KeyRange
+    from distml_amd.group import ShardGroup
+    from distml_amd.store import DeviceBatch
+    world, rank = ctx.world, ctx.rank
+    rows, cols, w = C4_ROWS, C4_COLS, args.c4_pushes
+    rec = 4 + 4 * cols
+    fmt = DataDesc(DataDesc.DATA_TYPE_MATRIX, DataDesc.KEY_TYPE_INT, DataDesc.ELEMENT_TYPE_FLOAT)
+    st = torch.cuda.current_stream().cuda_stream
+    bufs = []
+    for b in range(w):
+        t = torch.empty(rows * rec, dtype=torch.uint8, device="cuda")
+        seed = 3000 + 64 * rank + b
+        pa = _coprime(seed * 2654435761 % rows | 1, rows)
+        assert L.dml_synth_dense_bucket(t.data_ptr(), C.byref(fmt.to_c()), 0, rows, rows, cols, seed, pa,
+                                        b * 7919 % rows, C.c_void_p(st)) == 0
+        bufs.append(t)
+    torch.cuda.synchronize()
+    ptrs, lens = [b.data_ptr() for b in bufs], [b.numel() for b in bufs]
+    group = None
+    sharded = world > 1 or args.group
+    if not sharded:
+        store = DataStore(fmt, KeyRange(0, rows - 1), cols, device=ctx.local)
+        store.rand(13)
+        batch = DeviceBatch(ptrs, lens)
+
+        def step():
+            store.pushDevice(batch)
+
+        finish = store.flush
+        shard_rows = rows
+        store.set_timing(True)
+    else:
+        group = ShardGroup(fmt, rows, cols, rank, world, device=ctx.local, pieces=args.pieces)
+        group.store.rand(13)
+
+        def step():
+            group.push_full_range(ptrs, lens, st)
+
+        finish = group.flush
+        shard_rows = group.shard.size()
+        store = group.store
+    for _ in range(args.c4_warmup):
+        step()
+    finish()
+
+    def reset():
+        store.kernel_time(reset=True)
+        if sharded:
+            _pre_time(L, enable=True, reset=True)
+
+    el = timed_steps(ctx, step, finish, args.c4_steps, 0, reset=reset)
+    k_ms, k_n = store.kernel_time(reset=True)
+    store.set_timing(False)
+    pre_ms, pre_n = _pre_time(L, enable=False, reset=True) if sharded else (0.0, 0)
+    algo = w * rows * rec + 2 * shard_rows * cols * 4
+    out = {"workload": f"config4: Word2Vec rows {rows}x{cols} fp32 model, {w} full-range pushes per GPU "
+                       f"([int32][{cols} x f32], rows permuted per push)",
+           "value": round(algo * world * args.c4_steps / el / 2**30, 2), "unit": "GiB/s", "n_gpus": world,
+           "pushes_per_gpu": w, "steps": args.c4_steps, "ms_per_step": round(el / args.c4_steps * 1e3, 3),
+           "scaling": "weak", "dtype": "f32",
+           "parallelism": "single shard" if not sharded else f"linearSplit({world}) + RCCL reduce-scatter",
+           "algorithmic_bytes_per_step_per_gpu": algo}
+    if not sharded and k_n:
+        k_s = k_ms / k_n / 1e3
+        out["roofline"] = {"bound": "hbm", "achieved": round(algo / k_s / 1e9, 1), "peak": HBM_PEAK_GBS,
+                           "unit": "GB/s", "frac": round(algo / k_s / 1e9 / HBM_PEAK_GBS, 4),
+                           "traffic": None, "kernel": "k_reduce_rows<float,kAdd> (200-col rows)",
+                           "avg_kernel_us": round(k_s * 1e6, 1), "launches": k_n}
+    elif pre_n:
+        out["roofline"] = prereduce_roofline(L, ctx, args.pieces, pre_ms, pre_n,
+                                             w * rows * rec + world * group.step_rows * cols * 4, "config 4")
+    if group is not None:
+        group.close()
+    else:
+        store.close()
+    del bufs, ptrs
+    torch.cuda.synchronize()
+    torch.cuda.empty_cache()
+    return out
+
+
+# ---------------------------------------------------------------- config 5 (model level)
+def leg_config5(ctx: Ctx, L, args) -> dict:
+    """BASELINE config 5: LDA word-topic counts, IntMatrixStore 1M x 1000 int32,
+    32 pushes x 65 536 distinct vocabulary rows. The reference's client splits
+    each push by server partition (SparseMatrix.java:46-60) and every shard
+    applies its part with the negativity check (IntMatrixStore.java:164-178):
+    rank r holds shard r of linearSplit(N) and its parts of the 32 pushes
+    (65 536 x |shard| / 1M rows each). No data-path collective; strong scaling.
+    Successive steps alternate the pushes with their negations (counts stay >= 0)."""
+    torch = ctx.torch
+    from distml_amd import DataDesc, DataStore, KeyRange
+    from distml_amd.store import DeviceBatch
+    world, rank = ctx.world, ctx.rank
+    cols = C5_COLS
+    shard = KeyRange(0, C5_ROWS - 1).linearSplit(world)[rank]
+    S = shard.size()
+    nrec = int(round(C5_NNZ * S / C5_ROWS))
+    rec = 4 + 4 * cols
+    fmt = DataDesc(DataDesc.DATA_TYPE_MATRIX, DataDesc.KEY_TYPE_INT, DataDesc.ELEMENT_TYPE_INT)
+    store = DataStore(fmt, shard, cols, device=ctx.local)
+    store.rand(11)
+    st = torch.cuda.current_stream().cuda_stream
+    pos, neg = [], []
+    for b in range(C5_W):
+        t = torch.empty(nrec * rec, dtype=torch.uint8, device="cuda")
+        seed = 4000 + b
+        pa = _coprime((seed * 2654435761 + rank) % S | 1, S)
+        assert L.dml_synth_dense_bucket(t.data_ptr(), C.byref(fmt.to_c()), shard.firstKey, S, nrec, cols, seed,
+                                        pa, (b * 331 + rank) % S, C.c_void_p(st)) == 0
+        pos.append(t)
+        n = t.clone().view(torch.int32).view(nrec, 1 + cols)
+        n[:, 1:] = -n[:, 1:]
+        neg.append(n.view(torch.uint8).view(-1))
+    torch.cuda.synchronize()
+    sets = [DeviceBatch([b.data_ptr() for b in s], [b.numel() for b in s]) for s in (pos, neg)]
+    k = [0]
+
+    def step():
+        store.pushDevice(sets[k[0] & 1])
+        k[0] += 1
+
+    store.set_timing(True)
+    for _ in range(args.c5_warmup):
+        step()
+    store.flush()
+    store.kernel_time(reset=True)
+    steps = args.c5_steps + (args.c5_steps & 1)  # even: the counts return to their start
+    el = timed_steps(ctx, step, store.flush, steps, 0)
+    k_ms, k_n = store.kernel_time(reset=True)
+    store.set_timing(False)
+    assert store.error_state()[0] == 0, store.error_state()
+    touched = int(round(S * (1 - (1 - nrec / S) ** C5_W)))
+    algo = C5_W * nrec * rec + 2 * 4 * cols * touched
+    algo_all = algo
+    if world > 1:
+        t = torch.tensor([float(algo)], dtype=torch.float64, device="cuda")
+        ctx.dist.all_reduce(t)
+        algo_all = float(t.item())
+    out = {"workload": f"config5: LDA IntMatrixStore {C5_ROWS}x{cols} int32 (negativity check), {C5_W} pushes x "
+                       f"{C5_NNZ} distinct rows split per shard; this rank: shard of {S} rows, {nrec} records per push",
+           "value": round(algo_all * steps / el / 2**30, 2), "unit": "GiB/s", "n_gpus": world,
+           "pushes": C5_W, "steps": steps, "ms_per_step": round(el / steps * 1e3, 3), "scaling": "strong",
+           "dtype": "i32", "parallelism": "single shard" if world == 1 else f"linearSplit({world}), client-split pushes",
+           "algorithmic_bytes_per_step_per_gpu": algo, "algorithmic_bytes_per_step": int(algo_all)}
+    if k_n:
+        k_s = k_ms / k_n / 1e3
+        out["roofline"] = {"bound": "hbm", "achieved": round(algo / k_s / 1e9, 1), "peak": HBM_PEAK_GBS,
+                           "unit": "GB/s", "frac": round(algo / k_s / 1e9 / HBM_PEAK_GBS, 4), "traffic": None,
+                           "kernel": f"k_reduce_rows<int,kAddCheckI32> (rank {rank})",
+                           "avg_kernel_us": round(k_s * 1e6, 1), "launches": k_n}
+    store.close()
+    del pos, neg, sets
+    torch.cuda.synchronize()
+    torch.cuda.empty_cache()
+    return out
+
+
+# ---------------------------------------------------------------- configs 4 and 5, one shard
 # One GPU's shard of BASELINE.json configs 4 and 5 (8-GPU configs; SURVEY.md §8d):
 # the rows linearSplit(8) gives one rank, device-resident pushes of the named
 # shapes, the store's ordered batch reduce. `python bench.py --config 5|4`.
@@ -175,13 +627,6 @@ SHARD_CONFIGS = {
                   rows=1_250_000, cols=200, W=8, nrec=1_250_000, vt=1, ada=(0.025, 0.0001, 1.0), seed0=3000,
                   mult=7919, init=13, steps=5),
 }
-
-
-def _coprime(a, n):
-    import math
-    while math.gcd(a, n) != 1:
-        a += 1
-    return a
 
 
 def _shard_perms(c):
@@ -217,7 +662,8 @@ def shard_cpu_baseline(c, budget_s: float):
         nb += 1
     el = time.perf_counter() - t0
     return {"value": round(nb * nrec * (4 + 4 * cols) / el / 2**30, 3), "unit": "GiB/s of push bytes", "cores": 1,
-            "kind": "port", "sample": f"{nb} pushes of the same shapes in {el:.1f} s, oracle/dml_oracle.c"}
+            "kind": "port", "sample": f"{nb} pushes of the same shapes in {el:.1f} s, oracle/dml_oracle.c",
+            "host": host_info()}
 
 
 def run_shard_config(which: str, cpu_s: float, no_cpu: bool) -> dict:
@@ -225,7 +671,7 @@ def run_shard_config(which: str, cpu_s: float, no_cpu: bool) -> dict:
     from distml_amd import DataDesc, DataStore, KeyRange, _lib
     c = SHARD_CONFIGS[which]
     L = _lib.load()
-    rows, cols, W, nrec = c["rows"], c["cols"], c["W"], c["nrec"]
+    rows, cols, W_, nrec = c["rows"], c["cols"], c["W"], c["nrec"]
     fmt = DataDesc(1, 0, c["vt"], False, True, c["ada"] is not None)
     store = DataStore(fmt, KeyRange(0, rows - 1), cols)
     if c["ada"]:
@@ -251,8 +697,8 @@ def run_shard_config(which: str, cpu_s: float, no_cpu: bool) -> dict:
     torch.cuda.synchronize()
     # every push byte once + the touched shard rows read and written once
     # (AdaGrad: alpha and delta too)
-    touched = rows if nrec >= rows else int(round(rows * (1 - (1 - nrec / rows) ** W)))
-    algo = W * nrec * (4 + 4 * cols) + 2 * (3 if c["ada"] else 1) * 4 * cols * touched
+    touched = rows if nrec >= rows else int(round(rows * (1 - (1 - nrec / rows) ** W_)))
+    algo = W_ * nrec * (4 + 4 * cols) + 2 * (3 if c["ada"] else 1) * 4 * cols * touched
     steps = c["steps"]
     for i in range(max(4, steps)):
         store.pushDevice(*sets[i % len(sets)])
@@ -276,67 +722,77 @@ def run_shard_config(which: str, cpu_s: float, no_cpu: bool) -> dict:
     line = {"metric": "device-resident push reduce GiB/s (one GPU's shard)", "value": round(steps * algo / el / 2**30, 1),
             "unit": "GiB/s", "n_gpus": 1, "steps": steps, "ms_per_step": round(el / steps * 1e3, 3),
             "higher_is_better": True, "dtype": "i32" if c["vt"] == 0 else "f32", "data": "synthetic",
-            "config": {"workload": c["name"], "rows": rows, "cols": cols, "pushes": W, "records_per_push": nrec,
+            "config": {"workload": c["name"], "rows": rows, "cols": cols, "pushes": W_, "records_per_push": nrec,
                        "algorithmic_bytes_per_step": algo},
             "roofline": {"bound": "hbm", "achieved": round(algo / k_s / 1e9, 1) if k_n else None,
                          "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": round(algo / k_s / 1e9 / HBM_PEAK_GBS, 4) if k_n else None,
-                         "kernel_us_avg": round(k_s * 1e6, 1), "traffic": None}}
+                         "kernel_us_avg": round(k_s * 1e6, 1), "traffic": load_traffic(which)}}
     if not no_cpu:
         line["cpu_baseline"] = shard_cpu_baseline(c, cpu_s)
     return line
 
 
-def _pre_time(L, enable: bool, reset: bool):
-    """Pre-reduce piece timing of the sharded path (dml_prereduce_timing / _kernel_time)."""
-    ms, n = C.c_double(0.0), C.c_int64(0)
-    assert L.dml_prereduce_kernel_time(C.byref(ms), C.byref(n), 1 if reset else 0) == 0
-    assert L.dml_prereduce_timing(1 if enable else 0) == 0
-    return ms.value, n.value
-
-
-def load_traffic():
-    p = os.path.join(ROOT, "profiles", "pmc_traffic.json")
-    if not os.path.exists(p):
-        return None
-    try:
-        d = json.load(open(p))
-        return d.get("hbm_bytes_per_launch")
-    except Exception:
-        return None
+# ---------------------------------------------------------------- main
+def launcher_check(args, out):
+    """CPU-only rehearsal of the multi-rank plumbing (tests/test_bench_launcher.py):
+    the same env / rendezvous / max-over-ranks / rank-0 line, over gloo, no GPU."""
+    import torch
+    import torch.distributed as dist
+    world, rank = int(os.environ["WORLD_SIZE"]), int(os.environ["RANK"])
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    t0 = time.perf_counter()
+    time.sleep(0.02 * (rank + 1))
+    dist.barrier()
+    t = torch.tensor([time.perf_counter() - t0], dtype=torch.float64)
+    dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    if rank == 0:
+        print(json.dumps({"metric": "launcher-check", "value": float(t.item()), "n_gpus": world,
+                          "ranks_seen": world, "local_rank": int(os.environ["LOCAL_RANK"])}), file=out, flush=True)
+    dist.destroy_process_group()
 
 
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    # ~0.2 s of warmup and ~0.4 s timed at N=1: a few-ms window on a GPU that sat idle
-    # through process start-up measured 5 % slow (clocks still ramping; DESIGN.md §7)
+    # ~0.2 s of warmup and ~0.4 s timed at N=1 by default
     ap.add_argument("--steps", type=int, default=1000)
     ap.add_argument("--warmup", type=int, default=500)
-    ap.add_argument("--no-cpu", action="store_true", help="skip the CPU baseline leg")
+    ap.add_argument("--no-cpu", action="store_true", help="skip the CPU baseline legs")
     ap.add_argument("--no-timing", action="store_true", help="no kernel timing events in the timed region")
-    ap.add_argument("--sparse-steps", type=int, default=20, help="config-3 sparse leg steps (0 = skip)")
+    ap.add_argument("--sparse-steps", type=int, default=20, help="config-3 sparse leg steps (0 = skip; N=1 only)")
     ap.add_argument("--pieces", type=int, default=4, help="pre-reduce row slices per call (sharded path)")
     ap.add_argument("--group", action="store_true",
                     help="use the sharded pre-reduce/reduce-scatter path even at N=1 (path check)")
+    ap.add_argument("--legs", default="4,5", help="model-level config legs in the line ('' = none)")
+    ap.add_argument("--c4-pushes", type=int, default=16, help="config-4 full-range pushes per GPU (8.04 GB each)")
+    ap.add_argument("--c4-steps", type=int, default=5)
+    ap.add_argument("--c4-warmup", type=int, default=2)
+    ap.add_argument("--c5-steps", type=int, default=20)
+    ap.add_argument("--c5-warmup", type=int, default=4)
     ap.add_argument("--config", choices=["2", "4", "4-32", "4-asc", "4-256", "4-ada", "5"], default="2",
-                    help="2 = the headline (default); 4, 4-32, 4-ada, 5 = one GPU's shard of those 8-GPU configs")
+                    help="2 = the headline line (default); 4, 4-32, 4-ada, 5 = one GPU's shard of those configs")
     ap.add_argument("--cpu-seconds", type=float, default=8.0, help="CPU baseline budget for --config 4/5")
+    ap.add_argument("--launcher-check", action="store_true", help=argparse.SUPPRESS)
     args = ap.parse_args()
+    if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
+        sys.exit(launch_ranks(args.gpus, sys.argv[1:]))
     # stdout carries exactly the one JSON line: RCCL and other native libraries print
     # banners to fd 1 (e.g. "RCCL version : ..."), so fd 1 goes to stderr for the run
     sys.stdout.flush()
     out = os.fdopen(os.dup(1), "w")
     os.dup2(2, 1)
+    if args.launcher_check:
+        launcher_check(args, out)
+        return
     if args.config != "2":
+        assert args.gpus == 1, "--config 4/5 measure one GPU's shard; the N-GPU legs run in the default line"
         print(json.dumps(run_shard_config(args.config, args.cpu_seconds, args.no_cpu)), file=out, flush=True)
         return
 
     import torch
     import torch.distributed as dist
-    from distml_amd import DataDesc, DataStore, KeyRange, _lib
-    from distml_amd.group import ShardGroup
-    from distml_amd.store import DeviceBatch
+    from distml_amd import _lib
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
@@ -347,113 +803,26 @@ def main():
         dist.init_process_group("nccl", device_id=torch.device("cuda", local))
     elif args.group:
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
-        os.environ.setdefault("MASTER_PORT", "29533")
+        os.environ.setdefault("MASTER_PORT", str(_free_port()))
         dist.init_process_group("nccl", rank=0, world_size=1, device_id=torch.device("cuda", local))
     L = _lib.load()
-    fmt = DataDesc(DataDesc.DATA_TYPE_MATRIX, DataDesc.KEY_TYPE_INT, DataDesc.ELEMENT_TYPE_FLOAT)
+    ctx = Ctx(torch, dist, world, rank, local)
 
-    def barrier():
-        if world > 1:
-            dist.barrier()
-        torch.cuda.synchronize()
-
-    if world == 1 and not args.group:
-        store = DataStore(fmt, KeyRange(0, ROWS - 1), COLS, device=local)
-        store.rand(7)
-        bufs = make_buckets(L, torch, fmt, W, ROWS)
-        batch = DeviceBatch([b.data_ptr() for b in bufs], [b.numel() for b in bufs])
-
-        def step():
-            # async: ack once captured; the store keeps <= 2 batches in flight and the
-            # key index of batch k+1 overlaps the reduce of batch k
-            store.pushDevice(batch)
-
-        def finish():
-            store.flush()  # every pushed batch applied and error-checked
-        timed_store = store
-        algo_per_rank = W * BUCKET + 2 * SHARD
-    else:
-        group = ShardGroup(fmt, ROWS, COLS, rank, world, device=local, pieces=args.pieces)
-        bufs = make_buckets(L, torch, fmt, W, ROWS)
-        ptrs, lens = [b.data_ptr() for b in bufs], [b.numel() for b in bufs]
-        st = torch.cuda.current_stream().cuda_stream
-
-        def step():
-            group.push_full_range(ptrs, lens, st)
-
-        def finish():
-            group.flush()
-        timed_store = group.store
-        algo_per_rank = W * BUCKET + 2 * group.shard.size() * COLS * 4
-
-    sharded = not (world == 1 and not args.group)
-    for _ in range(args.warmup):
-        step()
-    finish()
-    timed_store.set_timing(not args.no_timing)
-    timed_store.kernel_time(reset=True)
-    if sharded and not args.no_timing:
-        _pre_time(L, enable=True, reset=True)
-    barrier()
-    t0 = time.perf_counter()
-    for _ in range(args.steps):
-        step()
-    finish()
-    barrier()
-    el = time.perf_counter() - t0
-    k_ms, k_n = timed_store.kernel_time(reset=True)
-    timed_store.set_timing(False)
-    pre_ms, pre_n = _pre_time(L, enable=False, reset=True) if sharded else (0.0, 0)
-    t = torch.tensor([el], dtype=torch.float64, device="cuda")
-    if world > 1:
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-    el = float(t.item())
-
-    total_bytes = algo_per_rank * world * args.steps
-    value = total_bytes / el / 2**30
-    line = {
-        "metric": "device-resident gradient-bucket reduce GiB/s (dense fp32 + sparse scatter-add)",
-        "value": round(value, 2), "unit": "GiB/s", "n_gpus": world, "steps": args.steps,
-        "warmup": args.warmup, "ms_per_step": round(el / args.steps * 1e3, 4), "higher_is_better": True,
-        "scaling": "weak", "vs_baseline": None, "dtype": "f32", "data": "synthetic",
-        "config": {"workload": "config2: dense fp32 reduce, 32 device-resident pushes x 64 MiB "
-                               "([int32 key][1024 x f32] x 16384) -> 16384x1024 fp32 shard per model",
-                   "pushes_per_gpu": W, "push_bytes": BUCKET, "model_rows": ROWS, "cols": COLS,
-                   "parallelism": ("single shard" if world == 1 and not args.group
-                                   else f"linearSplit({world}) + RCCL reduce-scatter"),
-                   "algorithmic_bytes_per_step_per_gpu": algo_per_rank},
-    }
+    line: dict = {}
+    headline(ctx, L, args, line)
+    legs = [x for x in args.legs.split(",") if x]
+    if "4" in legs:
+        line["config4"] = leg_config4(ctx, L, args)
+    if "5" in legs:
+        line["config5"] = leg_config5(ctx, L, args)
+    if world == 1 and not args.group and args.sparse_steps > 0:
+        line["sparse"] = sparse_leg(ctx, L, args.sparse_steps, cpu=not args.no_cpu)
+    if rank == 0 and world == 1 and not args.no_cpu and not args.group:
+        line["cpu_baseline"] = cpu_baseline()
     if rank == 0:
-        if world == 1 and k_n > 0 and not args.group:
-            avg_s = k_ms / k_n / 1e3
-            achieved = algo_per_rank / avg_s / 1e9
-            traffic = load_traffic()
-            pk = stream_peaks(L, torch)
-            line["roofline"] = {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS,
-                                "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic,
-                                "kernel": "k_reduce_rows<float,kAdd> (2 rows x 4 KiB per wave)", "avg_kernel_us": round(avg_s * 1e6, 2),
-                                "launches": k_n, "measured_read_peak": round(pk["read"], 1),
-                                "frac_of_measured_read": round(achieved / pk["read"], 4),
-                                "measured_copy_peak": round(pk["copy"], 1)}
-        elif pre_n > 0:
-            # sharded path: the pre-reduce pieces (k_reduce_rows in pre-reduce mode) are the
-            # dominant kernel; per call they read the W pushes and write the full-model partial
-            pre_bytes = W * BUCKET + world * group.step_rows * COLS * 4
-            calls = pre_n / args.pieces
-            avg_s = pre_ms / calls / 1e3
-            achieved = pre_bytes / avg_s / 1e9
-            line["roofline"] = {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS,
-                                "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": None,
-                                "kernel": f"k_reduce_rows pre-reduce ({args.pieces} pieces per call, rank 0)",
-                                "avg_kernel_us": round(avg_s * 1e6, 2), "launches": pre_n,
-                                "algorithmic_bytes_per_call": pre_bytes}
-        if world == 1 and not args.group and args.sparse_steps > 0:
-            del bufs
-            line["sparse"] = sparse_leg(L, torch, args.sparse_steps)
-        if world == 1 and not args.no_cpu and not args.group:
-            line["cpu_baseline"] = cpu_baseline()
         print(json.dumps(line), file=out, flush=True)
     if dist.is_initialized():
+        dist.barrier()
         dist.destroy_process_group()
 
 

@@ -129,6 +129,8 @@ hipError_t launch_array_rollback_i32(int32_t* shard, int64_t rows, const uint8_t
 hipError_t launch_fill(int vtype, void* p, int64_t n, double v, hipStream_t st);
 hipError_t launch_fill_f32(float* p, int64_t n, float v, hipStream_t st);
 hipError_t launch_apply_dense(int vtype, void* shard, const void* src, int64_t n, hipStream_t st);
+hipError_t launch_apply_dense_i32chk(int32_t* shard, const int32_t* src, int64_t n, unsigned long long* neg,
+                                     hipStream_t st);
 hipError_t launch_fetch(int vtype, const void* shard, const float* alpha, int32_t cols, const int64_t* keys,
                         int64_t key_lo, int64_t n, int64_t first, uint8_t* out, int64_t rec, int K, int value_slot,
                         hipStream_t st);

@@ -1372,6 +1372,43 @@ __global__ __launch_bounds__(256) void k_apply_dense(T* __restrict__ shard, cons
     const int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (t < n - nvec * VEC) shard[nvec * VEC + t] = Elem<T>::add(shard[nvec * VEC + t], src[nvec * VEC + t]);
 }
+// int32 owner apply with IntMatrixStore's negativity check on the final counters
+// (IntMatrixStore.java:174-176): the first negative element (row-major) of the
+// first failing apply is kept in *neg (sticky: kNoPos until then); once it is
+// set, later applies are no-ops (the reference store stops at its exception).
+__global__ __launch_bounds__(256) void k_apply_dense_i32chk(int32_t* __restrict__ shard, const int32_t* __restrict__ src,
+                                                            int64_t n, unsigned long long* neg) {
+    if (__atomic_load_n(neg, __ATOMIC_RELAXED) != kNoPos) return;
+    const int64_t nvec = n / 4;
+    unsigned long long first = kNoPos;
+    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < nvec; i += (int64_t)gridDim.x * blockDim.x) {
+        int32_t a[4], b[4];
+        unpack<int32_t>(((const u32x4*)shard)[i], a);
+        unpack<int32_t>(((const u32x4*)src)[i], b);
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+            a[e] = Elem<int32_t>::add(a[e], b[e]);
+            if (a[e] < 0 && first == kNoPos) first = (unsigned long long)(4 * i + e);
+        }
+        ((u32x4*)shard)[i] = pack<int32_t>(a);
+    }
+    const int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (t < n - nvec * 4) {
+        const int64_t j = nvec * 4 + t;
+        const int32_t v = Elem<int32_t>::add(shard[j], src[j]);
+        shard[j] = v;
+        if (v < 0 && first == kNoPos) first = (unsigned long long)j;
+    }
+    if (first != kNoPos) atomicMin(neg, first);
+}
+
+hipError_t launch_apply_dense_i32chk(int32_t* shard, const int32_t* src, int64_t n, unsigned long long* neg,
+                                     hipStream_t st) {
+    if (n <= 0) return hipSuccess;
+    hipLaunchKernelGGL(k_apply_dense_i32chk, dim3(256 * 8), dim3(256), 0, st, shard, src, n, neg);
+    return hipGetLastError();
+}
+
 hipError_t launch_apply_dense(int vtype, void* shard, const void* src, int64_t n, hipStream_t st) {
     if (n <= 0) return hipSuccess;
     const unsigned g = 256 * 8;

@@ -139,6 +139,11 @@ struct dml_store {
     int err = 0;
     int64_t err_key = 0;
     int32_t err_col = -1;
+    // int32 owner apply (dml_store_apply_dense_device): first negative final counter
+    unsigned long long* neg_dev = nullptr;   // sticky, kNoPos until an apply leaves a negative
+    unsigned long long* neg_host = nullptr;  // pinned copy, DMA'd behind every checked apply
+    hipEvent_t neg_ev = nullptr;
+    bool neg_pending = false;
     // timing of the dominant kernel
     bool timing = false;
     std::vector<std::pair<hipEvent_t, hipEvent_t>> ev_used, ev_free;
@@ -656,7 +661,10 @@ int retire_all(dml_store* s) {
 
 // Run `n` device-resident pushes (global indices 0..n-1) as ordered chunks of
 // <= kMaxW; up to two chunks stay in flight (retired later, in order).
+int collect_apply_check(dml_store* s, bool block);
+
 int run_batch(dml_store* s, const uint8_t* const* dptr, const int64_t* lens, int n) {
+    if (int rc = collect_apply_check(s, false)) return rc;  // an int32 owner apply failed earlier
     for (int c0 = 0; c0 < n; c0 += kMaxW) {
         Chunk c;
         c.nb = std::min(kMaxW, n - c0);
@@ -695,9 +703,27 @@ int check_store(dml_store* s) {
     return DML_OK;
 }
 
+// Result of the int32 owner applies (dml_store_apply_dense_device): the first
+// negative counter becomes the store's IllegalStateException. `block` waits for
+// the last apply; otherwise only a finished one is read.
+int collect_apply_check(dml_store* s, bool block) {
+    if (!s->neg_pending) return DML_OK;
+    if (!block && hipEventQuery(s->neg_ev) == hipErrorNotReady) return DML_OK;
+    HIPCHK(hipEventSynchronize(s->neg_ev));
+    s->neg_pending = false;
+    const unsigned long long idx = *s->neg_host;
+    if (idx == kNoPos) return DML_OK;
+    return record_error(s, DML_E_NEGATIVE_COUNTER, s->first + (int64_t)(idx / (unsigned long long)s->cols),
+                        (int32_t)(idx % (unsigned long long)s->cols));
+}
+
 // Entry of every reading / non-push call: all accepted pushes applied and
 // checked (read-your-writes).
-int begin_call(dml_store* s) { return retire_all(s); }
+int begin_call(dml_store* s) {
+    int rc = retire_all(s);
+    int rc2 = collect_apply_check(s, true);
+    return rc ? rc : rc2;
+}
 
 }  // namespace
 
@@ -844,6 +870,9 @@ void dml_store_destroy(dml_store* s) {
         (void)hipFree(s->cand);
         (void)hipFree(s->md);
         (void)hipFree(s->mark);
+        (void)hipFree(s->neg_dev);
+        if (s->neg_host) (void)hipHostFree(s->neg_host);
+        if (s->neg_ev) (void)hipEventDestroy(s->neg_ev);
         (void)hipFree(s->dstage);
         if (s->hstage) (void)hipHostFree(s->hstage);
         (void)hipFree(s->dscr);
@@ -932,7 +961,7 @@ int dml_store_flush(dml_store* s) {
     if (int rc = check_store(s)) return rc;
     std::lock_guard<std::mutex> lk(s->mu);
     DeviceGuard g(s->device);
-    int rc = retire_all(s);
+    int rc = begin_call(s);
     if (rc) return rc;
     HIPCHK(hipStreamSynchronize(s->stream));
     return DML_OK;
@@ -952,6 +981,13 @@ void dml_store_clear_error(dml_store* s) {
     s->err = 0;
     s->err_key = 0;
     s->err_col = -1;
+    if (s->neg_dev) {  // int32 owner applies resume
+        DeviceGuard g(s->device);
+        (void)hipStreamSynchronize(s->stream);
+        s->neg_pending = false;
+        (void)hipMemsetAsync(s->neg_dev, 0xFF, sizeof(unsigned long long), s->stream);
+        (void)hipStreamSynchronize(s->stream);
+    }
 }
 
 int dml_store_shape(dml_store* s, int64_t* rows, int32_t* cols) {
@@ -1240,7 +1276,23 @@ int dml_store_apply_dense_device(dml_store* s, const void* dev_src, int64_t elem
         ev = ev_pair(s);
         HIPCHK(hipEventRecord(ev.first, s->stream));
     }
-    HIPCHK(launch_apply_dense(vtype_of(s->desc), s->data, dev_src, elems, s->stream));
+    if (vtype_of(s->desc) == kI32) {
+        // IntMatrixStore: check the final counters (IntMatrixStore.java:174-176)
+        if (int rc = collect_apply_check(s, false)) return rc;
+        if (s->err) return set_err(s->err, "store is in a failed state (see dml_store_error_state)");
+        if (!s->neg_dev) {
+            HIPCHK(hipMalloc((void**)&s->neg_dev, sizeof(unsigned long long)));
+            HIPCHK(hipMemsetAsync(s->neg_dev, 0xFF, sizeof(unsigned long long), s->stream));
+            HIPCHK(hipHostMalloc((void**)&s->neg_host, sizeof(unsigned long long), hipHostMallocDefault));
+            HIPCHK(hipEventCreateWithFlags(&s->neg_ev, hipEventDisableTiming));
+        }
+        HIPCHK(launch_apply_dense_i32chk((int32_t*)s->data, (const int32_t*)dev_src, elems, s->neg_dev, s->stream));
+        HIPCHK(hipMemcpyAsync(s->neg_host, s->neg_dev, sizeof(unsigned long long), hipMemcpyDeviceToHost, s->stream));
+        HIPCHK(hipEventRecord(s->neg_ev, s->stream));
+        s->neg_pending = true;
+    } else {
+        HIPCHK(launch_apply_dense(vtype_of(s->desc), s->data, dev_src, elems, s->stream));
+    }
     if (s->timing) {
         HIPCHK(hipEventRecord(ev.second, s->stream));
         s->ev_used.push_back(ev);

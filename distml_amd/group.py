@@ -14,8 +14,21 @@ fp32 results differ from the single-shard ordered sum only by summation order
 (bound stated in tests/test_group_gloo.py); int32 is exact.
 
 Pushes that are already split per shard (SparseMatrix.push splits by partition,
-SparseMatrix.java:124-138) need no exchange: push_local() applies them on the
+SparseMatrix.java:46-60) need no exchange: push_local() applies them on the
 owner with the exact ordered reduce.
+
+int32 matrices (IntMatrixStore): the owner apply checks the final counters
+(IntMatrixStore.java:174-176) and reports the first negative element of the
+first failing call (row-major) at the next call or flush(); the store then
+refuses later applies. A counter that dips below zero only between two pushes
+of one pre-reduced sum is not seen (the reference would throw there) — the
+divergence SURVEY.md §8c names for batched reduces. push_exchange() applies
+int32 pushes exactly, intermediates included.
+
+Buffer contract of the asynchronous paths (push_full_range, push_exchange,
+push_local): the push buffers must stay allocated and unmodified until flush()
+— the same contract as dml_store_push_batch_device. The group orders its own
+reads after the work the caller's current stream enqueued before the call.
 """
 from __future__ import annotations
 
@@ -136,6 +149,9 @@ class ShardGroup:
         if (self.partial.is_cuda and hasattr(self.ops, "begin") and len(dev_ptrs) <= 64
                 and self.step_rows % self.pieces == 0):
             return self._push_pipelined(dev_ptrs, lens)
+        if self.partial.is_cuda:
+            # the one-shot path reuses buffer set 0: drain the pipelined calls that may still use it
+            self._drain()
         # rows past the matrix end (linearSplit's last shard may be short) stay zero
         self.ops.prereduce(self.fmt, 0, self.total_rows, self.cols, dev_ptrs, lens,
                            self.partial.data_ptr(), stream)
@@ -163,6 +179,8 @@ class ShardGroup:
         # stream has enqueued (the producers of the pushes)
         self._ready.record(torch.cuda.current_stream())
         self.cstream.wait_event(self._ready)
+        # the key index reads the push keys too: it orders after the producers as well
+        self.istream.wait_event(self._ready)
         st = self.cstream.cuda_stream
         partial, recv = self._partials[k], self._recvs[k]
         h = self.ops.begin(self.fmt, 0, self.total_rows, cols, dev_ptrs, lens, self.istream.cuda_stream)
@@ -262,17 +280,34 @@ class ShardGroup:
         """Pushes already split to this shard: exact ordered apply, no exchange."""
         self.store.pushDevice(dev_ptrs, lens)
 
-    def flush(self):
-        """Every pushed call applied; raises the first deferred pre-reduce error."""
+    def _drain(self) -> None:
+        """Every pipelined call's pieces, reduce-scatters and applies have finished."""
         try:
             self._end_pending(0)
         finally:
             if self.partial.is_cuda:
+                self.istream.synchronize()
                 self.cstream.synchronize()
                 self.comm.synchronize()
                 for ev in self._applied:
                     ev.synchronize()
+
+    def flush(self):
+        """Every pushed call applied; raises the first deferred pre-reduce error."""
+        try:
+            self._drain()
+        finally:
             self.store.flush()
+            self._xbufs.clear()
+
+    def close(self) -> None:
+        """Flush, then release the shard store and the partial / receive buffers."""
+        try:
+            self.flush()
+        finally:
+            self.store.close()
+            self._partials = self._recvs = []
+            self.partial = self.recv = None
             self._xbufs.clear()
 
 

@@ -1,0 +1,39 @@
+"""bench.py's own rank launcher: `python bench.py --gpus N` with no
+WORLD_SIZE starts its N rank processes itself and prints rank 0's one JSON line.
+Rehearsed on CPU with --launcher-check: the same env, 127.0.0.1 rendezvous, barrier
+and max-over-ranks as the GPU run, over gloo (no GPU call)."""
+import json
+import os
+import subprocess
+import sys
+
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def _run(n):
+    env = {k: v for k, v in os.environ.items()
+           if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK", "MASTER_ADDR", "MASTER_PORT")}
+    return subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", str(n), "--launcher-check"],
+                          env=env, capture_output=True, text=True, timeout=240)
+
+
+@pytest.mark.parametrize("n", [2, 3])
+def test_bench_self_launch_ranks(n):
+    r = _run(n)
+    assert r.returncode == 0, r.stderr[-2000:]
+    lines = [ln for ln in r.stdout.splitlines() if ln.strip()]
+    assert len(lines) == 1, r.stdout
+    d = json.loads(lines[0])
+    assert d["n_gpus"] == n and d["ranks_seen"] == n and d["local_rank"] == 0
+    # max over ranks: the slowest rank sleeps 0.02 * n s before the barrier
+    assert d["value"] >= 0.02 * n - 1e-3
+
+
+def test_bench_launcher_propagates_failure():
+    """A failing rank fails the launch (non-zero exit) instead of hanging."""
+    env = {k: v for k, v in os.environ.items() if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK")}
+    r = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "2", "--config", "4"],
+                       env=env, capture_output=True, text=True, timeout=240)
+    assert r.returncode != 0

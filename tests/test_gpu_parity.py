@@ -683,6 +683,85 @@ def test_native_group_rccl_world1(oracle, vt):
         g.close()
 
 
+def test_native_group_int32_negative_final_counter():
+    """IntMatrixStore's negativity check on the sharded full-range path:
+    the owner apply checks the final counters (IntMatrixStore.java:174-176); the
+    first negative element (row-major) of the failing call becomes the store's
+    IllegalStateException at flush(), with its key and column, and the store
+    refuses later calls."""
+    from distml_amd import DataDesc, IllegalStateException, encode_matrix_push
+    from distml_amd.group import NativeShardGroup
+    rows, cols = 64, 8
+    fmt = DataDesc(1, 0, 0)
+    g = NativeShardGroup(fmt, rows, cols, 0, 1, NativeShardGroup.unique_id(), device=0, pieces=4)
+    try:
+        g.store.set("3")
+        vals = np.zeros((rows, cols), np.int32)
+        vals[40, 5] = -4   # final 3 - 4 = -1: the first negative in row-major order
+        vals[41, 0] = -9
+        vals[10, 2] = -3   # final 0: fine
+        push = np.frombuffer(encode_matrix_push(np.arange(rows), vals, 0, 0), np.uint8).copy()
+        dev = torch.from_numpy(push).cuda()
+        torch.cuda.synchronize()
+        g.push_full_range([dev.data_ptr()], [dev.numel()])
+        with pytest.raises(IllegalStateException) as ei:
+            g.flush()
+        assert (ei.value.key, ei.value.col) == (40, 5)
+        got = g.store.values()
+        want = np.full((rows, cols), 3, np.int32) + vals
+        assert np.array_equal(got, want)
+        with pytest.raises(Exception):
+            g.push_full_range([dev.data_ptr()], [dev.numel()])
+            g.flush()
+    finally:
+        g.close()
+
+
+def test_shard_group_orders_after_producer_stream(oracle):
+    """ShardGroup.push_full_range right after the producers ran on the caller's
+    stream, with no host synchronize: the key index (side stream) and the pieces
+    must both order after them. Two back-to-back calls, bit-exact at
+    world 1 for int32 (the reduce-scatter is a copy, the sum exact)."""
+    import socket
+    import torch.distributed as dist
+    from distml_amd import DataDesc, _lib
+    from distml_amd.group import ShardGroup
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    dist.init_process_group("nccl", init_method=f"tcp://127.0.0.1:{port}", rank=0, world_size=1,
+                            device_id=torch.device("cuda", 0))
+    try:
+        rows, cols, W = 4096, 1000, 6
+        fmt = DataDesc(1, 0, 0)
+        L = _lib.load()
+        g = ShardGroup(fmt, rows, cols, 0, 1, device=0)
+        g.store.rand(5)
+        # a large first kernel on the caller's stream delays the producers behind it
+        big = torch.empty(1 << 30, dtype=torch.uint8, device="cuda")
+        bufs = [torch.empty(rows * (4 + 4 * cols), dtype=torch.uint8, device="cuda") for _ in range(2 * W)]
+        torch.cuda.synchronize()
+        st = torch.cuda.current_stream().cuda_stream
+        pas = [1, 3, 5, 7, 9, 11, 13, 15, 17, 19, 21, 23]
+        for call in range(2):
+            big.fill_(call)
+            for b in range(W):
+                j = call * W + b
+                assert L.dml_synth_dense_bucket(bufs[j].data_ptr(), C.byref(fmt.to_c()), 0, rows, rows, cols, 90 + j,
+                                                pas[j], 7 * j, C.c_void_p(st)) == 0
+            g.push_full_range([bufs[call * W + b].data_ptr() for b in range(W)], [bufs[0].numel()] * W, st)
+        g.flush()
+        o = oracle_store(oracle, fmt, 0, rows - 1, cols)
+        o.synth_fill(5)
+        for j in range(2 * W):
+            assert o.push(oracle.synth_dense_bucket(0, 0, 0, rows, rows, cols, 90 + j, pas[j], 7 * j).tobytes()) == 0
+        assert np.array_equal(g.store.values(), o.data)
+        g.close()
+    finally:
+        dist.destroy_process_group()
+
+
 def _np_split(recs_list, K, total_rows, world):
     """Reference split for dml_shard_split: stable per-owner partition, dest-major."""
     from distml_amd.datadesc import KeyRange
