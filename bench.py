@@ -235,11 +235,12 @@ def make_buckets(L, torch, fmt, n, rows_total):
     return bufs
 
 
-def _pre_time(L, enable: bool, reset: bool):
-    """Pre-reduce piece timing of the sharded path (dml_prereduce_timing / _kernel_time)."""
+def _pre_time(L, every: int, reset: bool):
+    """Pre-reduce piece timing of the sharded path (dml_prereduce_timing / _kernel_time):
+    returns the totals so far, then samples one call in `every` (0 = off)."""
     ms, n = C.c_double(0.0), C.c_int64(0)
     assert L.dml_prereduce_kernel_time(C.byref(ms), C.byref(n), 1 if reset else 0) == 0
-    assert L.dml_prereduce_timing(1 if enable else 0) == 0
+    assert L.dml_prereduce_timing(every) == 0
     return ms.value, n.value
 
 
@@ -277,7 +278,7 @@ def headline(ctx: Ctx, L, args, out_line: dict):
     group = None
     if not sharded:
         store = DataStore(fmt, KeyRange(0, ROWS - 1), COLS, device=ctx.local)
-        store.rand(7)
+        store.synth_fill(7)
         bufs = make_buckets(L, torch, fmt, W, ROWS)
         batch = DeviceBatch([b.data_ptr() for b in bufs], [b.numel() for b in bufs])
 
@@ -312,13 +313,13 @@ def headline(ctx: Ctx, L, args, out_line: dict):
     def reset():
         timed_store.kernel_time(reset=True)
         if sharded and timing:
-            _pre_time(L, enable=True, reset=True)
+            _pre_time(L, every=16, reset=True)
 
     el = timed_steps(ctx, step, finish, args.steps, 0, ramp_s=max(0.0, 0.3 - (time.perf_counter() - t0)),
                      reset=reset)
     k_ms, k_n = timed_store.kernel_time(reset=True)
     timed_store.set_timing(False)
-    pre_ms, pre_n = _pre_time(L, enable=False, reset=True) if sharded else (0.0, 0)
+    pre_ms, pre_n = _pre_time(L, every=0, reset=True) if sharded else (0.0, 0)
     value = algo_per_rank * world * args.steps / el / 2**30
     out_line.update({
         "metric": METRIC, "value": round(value, 2), "unit": "GiB/s", "n_gpus": world, "steps": args.steps,
@@ -463,7 +464,7 @@ def leg_config4(ctx: Ctx, L, args) -> dict:
     sharded = world > 1 or args.group
     if not sharded:
         store = DataStore(fmt, KeyRange(0, rows - 1), cols, device=ctx.local)
-        store.rand(13)
+        store.synth_fill(13)
         batch = DeviceBatch(ptrs, lens)
 
         def step():
@@ -474,7 +475,7 @@ def leg_config4(ctx: Ctx, L, args) -> dict:
         store.set_timing(True)
     else:
         group = ShardGroup(fmt, rows, cols, rank, world, device=ctx.local, pieces=args.pieces)
-        group.store.rand(13)
+        group.store.synth_fill(13)
 
         def step():
             group.push_full_range(ptrs, lens, st)
@@ -489,12 +490,12 @@ def leg_config4(ctx: Ctx, L, args) -> dict:
     def reset():
         store.kernel_time(reset=True)
         if sharded:
-            _pre_time(L, enable=True, reset=True)
+            _pre_time(L, every=1, reset=True)
 
     el = timed_steps(ctx, step, finish, args.c4_steps, 0, reset=reset)
     k_ms, k_n = store.kernel_time(reset=True)
     store.set_timing(False)
-    pre_ms, pre_n = _pre_time(L, enable=False, reset=True) if sharded else (0.0, 0)
+    pre_ms, pre_n = _pre_time(L, every=0, reset=True) if sharded else (0.0, 0)
     algo = w * rows * rec + 2 * shard_rows * cols * 4
     out = {"workload": f"config4: Word2Vec rows {rows}x{cols} fp32 model, {w} full-range pushes per GPU "
                        f"([int32][{cols} x f32], rows permuted per push)",
@@ -542,7 +543,7 @@ def leg_config5(ctx: Ctx, L, args) -> dict:
     rec = 4 + 4 * cols
     fmt = DataDesc(DataDesc.DATA_TYPE_MATRIX, DataDesc.KEY_TYPE_INT, DataDesc.ELEMENT_TYPE_INT)
     store = DataStore(fmt, shard, cols, device=ctx.local)
-    store.rand(11)
+    store.synth_fill(11)
     st = torch.cuda.current_stream().cuda_stream
     pos, neg = [], []
     for b in range(C5_W):
@@ -676,7 +677,7 @@ def run_shard_config(which: str, cpu_s: float, no_cpu: bool) -> dict:
     store = DataStore(fmt, KeyRange(0, rows - 1), cols)
     if c["ada"]:
         store.setAlpha(*c["ada"])
-    store.rand(c["init"])
+    store.synth_fill(c["init"])
     st = torch.cuda.current_stream().cuda_stream
     bufs = []
     for b, (pa, pc) in enumerate(_shard_perms(c)):

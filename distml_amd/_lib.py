@@ -36,7 +36,7 @@ SIGNATURES = {
     "dml_store_create_range": (C.c_int, [_P(dml_desc), _i64, _i64, _i32, _i32, _u32, _P(_vp)]),
     "dml_store_destroy": (None, [_vp]),
     "dml_linear_split": (C.c_int, [_i64, _i64, _i32, _P(_i64), _P(_i64)]),
-    "dml_store_push": (C.c_int, [_vp, C.c_char_p, _i64]),
+    "dml_store_push": (C.c_int, [_vp, _vp, _i64]),
     "dml_store_push_batch": (C.c_int, [_vp, _P(_vp), _P(_i64), _i32]),
     "dml_store_push_batch_device": (C.c_int, [_vp, _P(_vp), _P(_i64), _i32]),
     "dml_store_flush": (C.c_int, [_vp]),
@@ -80,6 +80,7 @@ SIGNATURES = {
     "dml_synth_dense_bucket": (C.c_int, [_vp, _P(dml_desc), _i64, _i64, _i64, _i32, _u64, _u64, _u64, _vp]),
     "dml_synth_sparse_bucket": (C.c_int, [_vp, _P(dml_desc), _i64, _i64, _i64, _u64, _u64, _u64, _vp]),
     "dml_synth_fill_store": (C.c_int, [_vp, _u64]),
+    "dml_store_rand": (C.c_int, [_vp, _u64]),
     "dml_diag_stream": (C.c_int, [_i32, _vp, _vp, _i64, _vp, _P(C.c_float)]),
     "dml_last_error": (C.c_char_p, []),
     "dml_version": (C.c_char_p, []),

@@ -11,7 +11,7 @@
 //                   the row (FloatMatrixStore.java:210-222, IntMatrixStore.java:164-178,
 //                   DoubleMatrixStore.java:163-175, FloatMatrixStoreAdaGrad.java:249-284)
 //   k_array_*       ordered sparse scatter-add for the array stores
-//                   (FloatArrayStore.java:380-392, IntArrayStore.java:294-310,
+//                   (FloatArrayStore.java:110-122, IntArrayStore.java:97-113,
 //                   DoubleArrayStore.java:115-127), one launch per push
 //   k_fetch, k_bswap, k_fill, k_apply_dense, k_synth_*  — fetch / checkpoint /
 //                   init / owner-apply / synthetic data.
@@ -1274,7 +1274,7 @@ __global__ __launch_bounds__(256) void k_array_rollback(int32_t* __restrict__ sh
 // Exact int32 array re-run (a push repeated a key, see k_array_apply): undo
 // every add the chunk's atomics made (positions before `cut`), then apply the
 // pushes in record order on one lane, stopping after the first add that leaves
-// a counter negative (IntArrayStore.java:294-310: the throw follows the add).
+// a counter negative (IntArrayStore.java:97-113: the throw follows the add).
 __global__ __launch_bounds__(256) void k_array_undo_i32(int32_t* __restrict__ shard, int64_t rows,
                                                         const uint8_t* __restrict__ base, int64_t nrec, int b_global,
                                                         int64_t stride, int K, int64_t first, uint64_t cut) {
@@ -1589,6 +1589,41 @@ hipError_t launch_stream(bool copy, void* dst, const void* src, int64_t n16, hip
     else
         hipExtLaunchKernelGGL(k_stream<false>, dim3(grid), dim3(256), 0, st, ev.start, ev.stop, 0, (uint8_t*)dst,
                               (const uint8_t*)src, n16);
+    return hipGetLastError();
+}
+
+// DataStore.rand() distributions (dml_store_rand). f32: (a/100f - 0.5f)/cols,
+// a uniform in 0..99, float arithmetic as in FloatMatrixStore.java:46-47.
+// f64: one thread per row, |N(0,1)| (Box-Muller) then the row over its L2 norm
+// (DoubleMatrixStore.java:196-206).
+__global__ void k_rand_f32(float* p, int64_t n, int32_t cols, uint64_t s0) {
+    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
+        const int a = (int)(splitmix64_dev(s0 + (uint64_t)i) % 100u);
+        p[i] = __fdiv_rn(__fsub_rn(__fdiv_rn((float)a, 100.0f), 0.5f), (float)cols);
+    }
+}
+__device__ inline double rand_abs_gauss(uint64_t h) {
+    const double u1 = (double)((h >> 11) + 1) * 0x1p-53;                   // (0, 1]
+    const double u2 = (double)(splitmix64_dev(h) >> 11) * 0x1p-53;          // [0, 1)
+    return fabs(sqrt(-2.0 * log(u1)) * cos(6.283185307179586 * u2));
+}
+__global__ void k_rand_f64_rows(double* p, int64_t rows, int32_t cols, uint64_t s0) {
+    for (int64_t r = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; r < rows; r += (int64_t)gridDim.x * blockDim.x) {
+        double* row = p + r * cols;
+        double sum = 0.0;
+        for (int32_t j = 0; j < cols; ++j) {
+            const double g = rand_abs_gauss(splitmix64_dev(s0 + (uint64_t)(r * cols + j)));
+            row[j] = g;
+            sum = __dadd_rn(sum, __dmul_rn(g, g));
+        }
+        sum = sqrt(sum);
+        for (int32_t j = 0; j < cols; ++j) row[j] = __ddiv_rn(row[j], sum);
+    }
+}
+hipError_t launch_rand(int vtype, void* p, int64_t rows, int32_t cols, uint64_t s0, hipStream_t st) {
+    if (rows <= 0) return hipSuccess;
+    if (vtype == kF32) hipLaunchKernelGGL(k_rand_f32, dim3(grid_for(rows * cols)), dim3(256), 0, st, (float*)p, rows * cols, cols, s0);
+    else if (vtype == kF64) hipLaunchKernelGGL(k_rand_f64_rows, dim3(grid_for(rows)), dim3(256), 0, st, (double*)p, rows, cols, s0);
     return hipGetLastError();
 }
 

@@ -1,5 +1,5 @@
 // dml_sparse.hip — ordered sparse scatter-add for the float / double array stores
-// (FloatArrayStore.java:380-392, DoubleArrayStore.java:115-127) over a chunk of
+// (FloatArrayStore.java:110-122, DoubleArrayStore.java:115-127) over a chunk of
 // pushes, without atomics on the shard.
 //
 // The reference adds record after record: per shard element, the adds land in

@@ -1430,12 +1430,13 @@ struct dml_prereduce {
     std::vector<std::pair<hipEvent_t, hipEvent_t>> tev;  // per-piece start/stop of a timed call
 };
 
-// Pre-reduce kernel timing (dml_prereduce_timing): one call in kPreSample gets
-// start/stop events in its pieces' dispatch packets (events in every packet
-// cost ~10 us per launch: 4 pieces per call would move the step time itself);
-// _end adds their elapsed time to the totals. Events come from a pool.
-constexpr int64_t kPreSample = 16;
-static std::atomic<bool> g_pre_timing{false};
+// Pre-reduce kernel timing (dml_prereduce_timing(every)): one call in `every`
+// gets start/stop events in its pieces' dispatch packets (events in every packet
+// cost ~10 us per launch: at config 2's 0.4 ms calls, 4 pieces per call would
+// move the step time itself, so bench.py samples 1 in 16 there and every call of
+// config 4's 40 ms calls); _end adds their elapsed time to the totals. Events
+// come from a pool.
+static std::atomic<int32_t> g_pre_timing{0};  // sample one call in g_pre_timing (0 = off)
 static std::atomic<int64_t> g_pre_calls{0};
 static std::mutex g_pre_mu;
 static double g_pre_ms = 0.0;
@@ -1513,8 +1514,8 @@ int dml_prereduce_begin(const dml_desc* desc, int64_t first_key, int64_t rows, i
         prereduce_free(p);
         return set_err(DML_E_HIP, hipGetErrorString(e));
     }
-    p->timed = g_pre_timing.load(std::memory_order_relaxed) &&
-               g_pre_calls.fetch_add(1, std::memory_order_relaxed) % kPreSample == 0;
+    const int32_t every = g_pre_timing.load(std::memory_order_relaxed);
+    p->timed = every > 0 && g_pre_calls.fetch_add(1, std::memory_order_relaxed) % every == 0;
     *out = p;
     return DML_OK;
 }
@@ -1569,8 +1570,9 @@ int dml_prereduce_piece(dml_prereduce* p, int64_t row_block, int64_t row_stride,
     return DML_OK;
 }
 
-int dml_prereduce_timing(int32_t enable) {
-    g_pre_timing.store(enable != 0);
+int dml_prereduce_timing(int32_t every) {
+    g_pre_timing.store(every > 0 ? every : 0);
+    g_pre_calls.store(0);
     return DML_OK;
 }
 
@@ -1663,6 +1665,18 @@ int dml_diag_stream(int32_t copy, void* dev_dst, const void* dev_src, int64_t by
     if (e1) (void)hipEventDestroy(e1);
     if (e != hipSuccess) return set_err(DML_E_HIP, hipGetErrorString(e));
     if (ms) *ms = t;
+    return DML_OK;
+}
+
+int dml_store_rand(dml_store* s, uint64_t seed) {
+    if (int rc = check_store(s)) return rc;
+    std::lock_guard<std::mutex> lk(s->mu);
+    DeviceGuard g(s->device);
+    if (int rc = begin_call(s)) return rc;
+    const int vt = vtype_of(s->desc);
+    if (!s->is_matrix || vt == kI32) return DML_OK;  // DataStore.rand(): no-op (DataStore.java:22)
+    HIPCHK(launch_rand(vt, s->data, s->rows, s->cols, splitmix64(seed ^ 0x5241'4e44ull), s->stream));
+    HIPCHK(hipStreamSynchronize(s->stream));
     return DML_OK;
 }
 

@@ -134,9 +134,17 @@ class DataStore:
     def rowSize(self) -> int:
         return self._cols
 
-    def rand(self, seed: int = 7):
-        """Random init. The reference draws java.util.Random (FloatMatrixStore.java:39-51);
-        this store uses the counter-based generator of DESIGN.md §Synthetic data."""
+    def rand(self, seed: int = 1):
+        """DataStore.rand (dml_store_rand): the reference's distributions, drawn from a
+        counter-based generator instead of java.util.Random — float matrices
+        (a/100f - 0.5f)/rowSize with a uniform in 0..99 (FloatMatrixStore.java:39-51,
+        FloatMatrixStoreAdaGrad.java:55-66), double matrices |N(0,1)| rows scaled to unit
+        norm (DoubleMatrixStore.java:192-207); the other stores keep DataStore's no-op."""
+        check(_lib.load().dml_store_rand(self._h, seed), self)
+
+    def synth_fill(self, seed: int = 7):
+        """Test/bench init with the counter-based generator the oracle restates
+        (DESIGN.md §Synthetic data; pyoracle.OracleStore.synth_fill)."""
         check(_lib.load().dml_synth_fill_store(self._h, seed), self)
 
     def zero(self):
@@ -146,20 +154,34 @@ class DataStore:
         # FloatMatrixStore.set -> setValue(Float.parseFloat(value)) (:53-71)
         check(_lib.load().dml_store_fill(self._h, float(value)), self)
 
-    def handlePush(self, format: DataDesc, data: bytes):
-        """Apply one push (FloatMatrixStore.java:200-238 and the other typed stores)."""
-        self._check_format(format)
-        buf = data if isinstance(data, (bytes, bytearray)) else bytes(data)
-        check(_lib.load().dml_store_push(self._h, bytes(buf), len(buf)), self)
+    @staticmethod
+    def _host_view(data):
+        """(pointer, length, keep-alive) of a push's bytes. A contiguous numpy uint8
+        array (e.g. pinned_empty(), the wire-ingest buffer) is passed as is: the
+        library DMAs pinned memory without staging. Anything else is copied to bytes."""
+        if isinstance(data, np.ndarray) and data.dtype == np.uint8 and data.flags.c_contiguous:
+            return data.ctypes.data, data.nbytes, data
+        b = data if isinstance(data, bytes) else bytes(data)
+        return C.cast(C.c_char_p(b), C.c_void_p).value, len(b), b
 
-    def handlePushBatch(self, format: DataDesc, datas: Sequence[bytes]):
+    def handlePush(self, format: DataDesc, data):
+        """Apply one push (FloatMatrixStore.java:200-238 and the other typed stores).
+        `data` is borrowed for the call (the reference's byte[]); with async_push the
+        call returns once the bytes are captured."""
+        self._check_format(format)
+        p, n, keep = self._host_view(data)
+        check(_lib.load().dml_store_push(self._h, C.c_void_p(p), n), self)
+        del keep
+
+    def handlePushBatch(self, format: DataDesc, datas: Sequence):
         """n sequential handlePush calls applied as one ordered multi-push reduce."""
         self._check_format(format)
-        bufs = [bytes(d) for d in datas]
-        n = len(bufs)
-        ptrs = (C.c_void_p * n)(*[C.cast(C.c_char_p(b), C.c_void_p).value for b in bufs])
-        lens = (C.c_int64 * n)(*[len(b) for b in bufs])
+        views = [self._host_view(d) for d in datas]
+        n = len(views)
+        ptrs = (C.c_void_p * max(n, 1))(*[v[0] for v in views])
+        lens = (C.c_int64 * max(n, 1))(*[v[1] for v in views])
         check(_lib.load().dml_store_push_batch(self._h, ptrs, lens, n), self)
+        del views
 
     def pushDevice(self, dev_ptrs, lens=None):
         """Device-resident pushes (pointers on this store's device), applied in order,
@@ -393,7 +415,7 @@ class Model:
 # ---- record codec: the byte layout of the reference's writers ---------------
 def encode_matrix_push(keys, values, key_type: int, value_type: int) -> bytes:
     """[key LE][cols x value LE] per row — SparseMatrix.writeMap dense branch
-    (SparseMatrix.java:174-204). `values` is (n, cols)."""
+    (SparseMatrix.java:96-148). `values` is (n, cols)."""
     keys = np.asarray(keys, dtype=np.int64)
     vals = np.ascontiguousarray(values, dtype=VALUE_DTYPE[value_type])
     kdt = np.dtype("<i4") if key_type == DataDesc.KEY_TYPE_INT else np.dtype("<i8")

@@ -97,7 +97,7 @@ int dml_linear_split(int64_t first_key, int64_t last_key, int32_t n,
 /* --- the hot path: handlePush ------------------------------------------ */
 
 /* == store.handlePush(format, data) (DataStore.java:30; FloatMatrixStore.java:200-238,
- * FloatArrayStore.java:380-392, IntMatrixStore.java:154-195, IntArrayStore.java:294-310,
+ * FloatArrayStore.java:110-122, IntMatrixStore.java:154-195, IntArrayStore.java:97-113,
  * FloatMatrixStoreAdaGrad.java:239-306, DoubleArrayStore.java:115-127,
  * DoubleMatrixStore.java:153-190). `data` is a host buffer BORROWED for the
  * call only (the JVM byte[]). Records use the store's own DataDesc
@@ -137,6 +137,14 @@ int dml_store_device_ptr(dml_store* s, void** dev_ptr);
 /* AdaGrad side arrays (FloatMatrixStoreAdaGrad.java:23-24), f32 row-major. */
 int dml_store_read_adagrad(dml_store* s, float* alpha_dst, float* delta_dst, int64_t elems);
 
+/* DataStore.rand() (DataStore.java:22; PSActor OP_RAND, PSActor.java:181-201):
+ * the reference's distributions from a counter-based generator seeded by `seed`
+ * (java.util.Random's stream is not reproduced): float matrices, AdaGrad
+ * included, (a/100f - 0.5f)/rowSize with a uniform in 0..99 in float arithmetic
+ * (FloatMatrixStore.java:39-51, FloatMatrixStoreAdaGrad.java:55-66); double
+ * matrices |N(0,1)| per element, each row divided by its L2 norm
+ * (DoubleMatrixStore.java:192-207); other stores: no-op (DataStore.java:22). */
+int dml_store_rand(dml_store* s, uint64_t seed);
 /* set(String)/zero()/setValue (FloatMatrixStore.java:53-71): fill every value. */
 int dml_store_fill(dml_store* s, double v);
 /* FloatMatrixStoreAdaGrad.setAlpha(initialAlpha, minAlpha, factor) (:77-82). */
@@ -145,7 +153,7 @@ int dml_store_set_alpha(dml_store* s, float initial_alpha, float min_alpha, floa
 int dml_store_max_delta(dml_store* s, float* max_delta, int32_t* row, int32_t* col);
 
 /* == handleFetch(format, rows), dense-column layout (FloatMatrixStore.java:113-174,
- * IntMatrixStore.java:81-140, FloatArrayStore.java:358-378, IntArrayStore.java:274-292,
+ * IntMatrixStore.java:81-140, FloatArrayStore.java:88-108, IntArrayStore.java:78-95,
  * DoubleArrayStore.java handleFetch, FloatMatrixStoreAdaGrad.java:146-213).
  * `keys` are the intersected keys in the caller's iteration order; every key
  * must lie in the shard. Writes the reference byte layout to `out`. */
@@ -220,10 +228,11 @@ int dml_prereduce_end(dml_prereduce* p);
 /* Make `stream` wait (device side) for the pieces enqueued so far, e.g. the
  * communication stream that reduce-scatters the piece just written. */
 int dml_prereduce_stream_wait(dml_prereduce* p, void* stream);
-/* Measurement: with timing on, each piece carries start/stop events in its
- * dispatch packet and _end adds their elapsed time to a process-wide total
- * (bench.py's roofline of the sharded path; no reference counterpart). */
-int dml_prereduce_timing(int32_t enable);
+/* Measurement: with every > 0, the pieces of one call in `every` carry
+ * start/stop events in their dispatch packets and _end adds their elapsed time
+ * to a process-wide total (bench.py's roofline of the sharded path; no
+ * reference counterpart). 0 turns timing off. */
+int dml_prereduce_timing(int32_t every);
 int dml_prereduce_kernel_time(double* ms, int64_t* launches, int32_t reset);
 
 /* --- per-shard split of device-resident pushes (multi-GPU exchange path) -- */

@@ -36,6 +36,10 @@ public class GpuDataStore extends DataStore {
     public KeyCollection rows() { return localRows; }
     public int rowSize() { return rowSize; }
 
+    /** DataStore.rand() / PSActor OP_RAND (PSActor.java:181-201): FloatMatrixStore's
+     *  (nextInt(100)/100f - 0.5f)/rowSize (FloatMatrixStore.java:39-51), DoubleMatrixStore's
+     *  unit-norm |gaussian| rows (DoubleMatrixStore.java:192-207); a no-op for the others. */
+    public void rand() { nativeRand(handle, System.nanoTime()); }
     public void zero() { nativeFill(handle, 0.0); }
     public void set(String value) { nativeFill(handle, Float.parseFloat(value)); }
     public void setAlpha(float initialAlpha, float minAlpha, float factor) {
@@ -99,6 +103,7 @@ public class GpuDataStore extends DataStore {
     private static native void nativeHostFree(java.nio.ByteBuffer b);
     private static native void nativePushDirect(long h, java.nio.ByteBuffer b, int offset, int len);
     private static native void nativeFill(long h, double v);
+    private static native void nativeRand(long h, long seed);
     private static native void nativeSetAlpha(long h, float a, float min, float factor);
     private static native void nativeDestroy(long h);
 }

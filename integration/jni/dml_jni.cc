@@ -1,10 +1,13 @@
 // dml_jni.cc — JNI shim: com.intel.distml.util.store.GpuDataStore -> include/distml_ps.h.
 // Build (where a JDK provides jni.h):
-//   g++ -O2 -fPIC -shared -I$JAVA_HOME/include -I$JAVA_HOME/include/linux -I../../include \
+//   g++ -O2 -fPIC -shared -I$JAVA_HOME/include -I$JAVA_HOME/include/linux -I../../include
 //       dml_jni.cc -L../../distml_amd -ldistml_ps -Wl,-rpath,'$ORIGIN' -o libdistml_jni.so
 // Status codes become the exceptions the reference throws (DataStore.java:91,
 // IntMatrixStore.java:175, array bounds): see include/distml_ps.h.
 #include <jni.h>
+
+#include <cstddef>
+#include <cstdint>
 
 #include <vector>
 
@@ -36,15 +39,55 @@ JNIEXPORT jlong JNICALL FN(nativeCreate)(JNIEnv* env, jclass, jint dt, jint kt, 
     return reinterpret_cast<jlong>(s);
 }
 
-// The byte[] is borrowed for the call only: GetPrimitiveArrayCritical pins it,
-// dml_store_push copies it into pinned staging / HBM, JNI_ABORT releases
-// without copy-back. Nothing retains the pointer after return.
-JNIEXPORT void JNICALL FN(nativePush)(JNIEnv* env, jclass, jlong h, jbyteArray a) {
+// Per-thread pinned staging for JVM-heap byte[]s: GetByteArrayRegion copies the
+// array into it (no GC-blocking critical section across the GPU work), and the
+// library DMAs pinned memory without a further staging copy. The push is
+// synchronous, so the buffer is free again when dml_store_push returns.
+namespace {
+struct PinnedStage {
+    void* p = nullptr;
+    int64_t cap = 0;
+    ~PinnedStage() { if (p) dml_host_free(p); }
+    uint8_t* get(int64_t n) {
+        if (n > cap) {
+            if (p) dml_host_free(p);
+            p = nullptr;
+            cap = 0;
+            const int64_t want = n < (1 << 20) ? (1 << 20) : n;
+            if (dml_host_alloc(want, &p) != DML_OK) return nullptr;
+            cap = want;
+        }
+        return static_cast<uint8_t*>(p);
+    }
+};
+thread_local PinnedStage t_stage;
+
+// Copy a byte[] into the thread's pinned stage; nullptr (exception pending) on failure.
+const uint8_t* stage_array(JNIEnv* env, jbyteArray a, jsize* n_out) {
     const jsize n = env->GetArrayLength(a);
-    void* p = env->GetPrimitiveArrayCritical(a, nullptr);
-    int rc = dml_store_push(H(h), static_cast<const uint8_t*>(p), n);
-    env->ReleasePrimitiveArrayCritical(a, p, JNI_ABORT);
-    if (rc) throw_for(env, rc);
+    uint8_t* p = t_stage.get(n);
+    if (!p) {
+        throw_for(env, DML_E_NOMEM);
+        return nullptr;
+    }
+    env->GetByteArrayRegion(a, 0, n, reinterpret_cast<jbyte*>(p));
+    *n_out = n;
+    return p;
+}
+}  // namespace
+
+// The byte[] is borrowed for the call only (PSAgent.java:278-281): its bytes are
+// copied into pinned staging first; nothing retains the array after return.
+JNIEXPORT void JNICALL FN(nativePush)(JNIEnv* env, jclass, jlong h, jbyteArray a) {
+    jsize n = 0;
+    const uint8_t* p = stage_array(env, a, &n);
+    if (!p) return;
+    if (int rc = dml_store_push(H(h), p, n)) throw_for(env, rc);
+}
+
+// DataStore.rand() (PSActor OP_RAND): the reference's distributions (dml_store_rand).
+JNIEXPORT void JNICALL FN(nativeRand)(JNIEnv* env, jclass, jlong h, jlong seed) {
+    if (int rc = dml_store_rand(H(h), (uint64_t)seed)) throw_for(env, rc);
 }
 
 static jbyteArray fetch_common(JNIEnv* env, dml_store* s, const int64_t* keys, int64_t n, bool range, int64_t f,
@@ -92,11 +135,10 @@ JNIEXPORT jbyteArray JNICALL FN(nativeWriteAll)(JNIEnv* env, jclass, jlong h) {
 }
 
 JNIEXPORT void JNICALL FN(nativeReadAll)(JNIEnv* env, jclass, jlong h, jbyteArray a) {
-    const jsize n = env->GetArrayLength(a);
-    void* p = env->GetPrimitiveArrayCritical(a, nullptr);
-    int rc = dml_store_read_all(H(h), static_cast<const uint8_t*>(p), n);
-    env->ReleasePrimitiveArrayCritical(a, p, JNI_ABORT);
-    if (rc) throw_for(env, rc);
+    jsize n = 0;
+    const uint8_t* p = stage_array(env, a, &n);
+    if (!p) return;
+    if (int rc = dml_store_read_all(H(h), p, n)) throw_for(env, rc);
 }
 
 // syncTo / syncFrom (PSSync.java:131,160): local rows from..to, big-endian.
@@ -117,11 +159,10 @@ JNIEXPORT jbyteArray JNICALL FN(nativeSyncTo)(JNIEnv* env, jclass, jlong h, jint
 }
 
 JNIEXPORT void JNICALL FN(nativeSyncFrom)(JNIEnv* env, jclass, jlong h, jint from, jint to, jbyteArray a) {
-    const jsize n = env->GetArrayLength(a);
-    void* p = env->GetPrimitiveArrayCritical(a, nullptr);
-    const int rc = dml_store_sync_from(H(h), from, to, static_cast<const uint8_t*>(p), n);
-    env->ReleasePrimitiveArrayCritical(a, p, JNI_ABORT);
-    if (rc) throw_for(env, rc);
+    jsize n = 0;
+    const uint8_t* p = stage_array(env, a, &n);
+    if (!p) return;
+    if (int rc = dml_store_sync_from(H(h), from, to, p, n)) throw_for(env, rc);
 }
 
 // Pinned host memory as a DirectByteBuffer: PSAgent's NIO channel reads a

@@ -246,8 +246,8 @@ static int push_matrix(orc_store* s, const uint8_t* data, int64_t len) {
 }
 
 /* Array stores:
- *   FloatArrayStore.handlePush   FloatArrayStore.java:380-392 (VALUE_SIZE :15)
- *   IntArrayStore.handlePush     IntArrayStore.java:294-310
+ *   FloatArrayStore.handlePush   FloatArrayStore.java:110-122 (VALUE_SIZE :15)
+ *   IntArrayStore.handlePush     IntArrayStore.java:97-113
  *   DoubleArrayStore.handlePush  DoubleArrayStore.java:115-127
  * Java evaluation order: key read, value read, then the array index. */
 static int push_array(orc_store* s, const uint8_t* data, int64_t len) {
@@ -356,7 +356,7 @@ int orc_push_many(orc_store* s, const uint8_t* const* bufs, const int64_t* lens,
  *          DoubleMatrixStore handleFetch); AdaGrad: [key][cols x (value, alpha)]
  *          (FloatMatrixStoreAdaGrad.java:173-190).
  * Array:   [key][value] with the store's VALUE_SIZE stride; FloatArrayStore writes
- *          4 value bytes into an 8-byte zeroed slot (FloatArrayStore.java:362-376).
+ *          4 value bytes into an 8-byte zeroed slot (FloatArrayStore.java:92-105).
  * Returns bytes written or -1 (key outside shard / capacity). */
 int64_t orc_fetch(orc_store* s, const int64_t* keys, int64_t n, uint8_t* out, int64_t cap) {
     const int K = s->key_size, V = s->value_size;

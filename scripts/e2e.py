@@ -24,7 +24,7 @@ torch.cuda.empty_cache()
 algo = W * bench.BUCKET + 2 * bench.SHARD
 res = {}
 store = DataStore(fmt, KeyRange(0, bench.ROWS - 1), bench.COLS)
-store.rand(7)
+store.synth_fill(7)
 for kind in ("pageable", "pinned"):
     if kind == "pinned":
         pinned = [torch.from_numpy(h).pin_memory() for h in host]

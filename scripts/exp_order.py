@@ -20,7 +20,7 @@ def main():
     L = _lib.load()
     fmt = DataDesc(1, 0, 1)
     store = DataStore(fmt, KeyRange(0, bench.ROWS - 1), bench.COLS)
-    store.rand(7)
+    store.synth_fill(7)
     st = torch.cuda.current_stream().cuda_stream
     algo = bench.W * bench.BUCKET + 2 * bench.SHARD
     orders = {"ascending": lambda b: (1, 0), "permuted": lambda b: bench.perm_for(2 * b + 1), "mixed": bench.perm_for}

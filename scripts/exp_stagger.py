@@ -20,7 +20,7 @@ def main():
     L = _lib.load()
     fmt = DataDesc(1, 0, 1)
     store = DataStore(fmt, KeyRange(0, bench.ROWS - 1), bench.COLS)
-    store.rand(7)
+    store.synth_fill(7)
     st = torch.cuda.current_stream().cuda_stream
     span = (bench.BUCKET + (4 << 20) + (2 << 20) - 1) // (2 << 20) * (2 << 20)
     pool = torch.empty(span * bench.W, dtype=torch.uint8, device="cuda")

@@ -19,7 +19,7 @@ def main():
     L = _lib.load()
     fmt = DataDesc(1, 0, 1)
     store = DataStore(fmt, KeyRange(0, bench.ROWS - 1), bench.COLS)
-    store.rand(7)
+    store.synth_fill(7)
     bufs = bench.make_buckets(L, torch, fmt, bench.W, bench.ROWS)
     ptrs, lens = [b.data_ptr() for b in bufs], [b.numel() for b in bufs]
     algo = bench.W * bench.BUCKET + 2 * bench.SHARD

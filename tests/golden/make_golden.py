@@ -171,8 +171,8 @@ def case(name, ref, dt, kt, vt, first, last, pushes, cols=1, init=None, ada=None
 
 FMS = "FloatMatrixStore.java:200-222"
 IMS = "IntMatrixStore.java:154-178"
-FAS = "FloatArrayStore.java:380-392"
-IAS = "IntArrayStore.java:294-310"
+FAS = "FloatArrayStore.java:110-122"
+IAS = "IntArrayStore.java:97-113"
 DAS = "DoubleArrayStore.java:115-127"
 DMS = "DoubleMatrixStore.java:153-175"
 ADA = "FloatMatrixStoreAdaGrad.java:239-284"

@@ -480,7 +480,7 @@ def test_config2_dense_fp32_full_size_bit_exact(oracle):
     rows, cols, W = 16384, 1024, 32
     fmt = DataDesc(1, 0, 1)
     s, _ = mk_store(fmt, 0, rows - 1, cols)
-    s.rand(7)
+    s.synth_fill(7)
     o = oracle_store(oracle, fmt, 0, rows - 1, cols)
     o.synth_fill(7)
     assert kat.bits_equal(s.values(), o.data)
@@ -528,7 +528,7 @@ def test_config5_lda_int32_shard_bit_exact(oracle):
     rows, cols, W, nrec = 125_000, 1000, 32, 8192
     fmt = DataDesc(1, 0, 0)
     s, _ = mk_store(fmt, 0, rows - 1, cols)
-    s.rand(11)
+    s.synth_fill(11)
     o = oracle_store(oracle, fmt, 0, rows - 1, cols)
     o.synth_fill(11)
     L = _lib.load()
@@ -587,7 +587,7 @@ def test_shard_group_rccl_world1(oracle):
         rows, cols, W = 1000, 256, 6
         fmt = DataDesc(1, 0, 1)
         g = ShardGroup(fmt, rows, cols, 0, 1, device=0)
-        g.store.rand(3)
+        g.store.synth_fill(3)
         pas = [1, 3, 7, 9, 11, 13]  # coprime with 1000: each push lists every row once
         host = [oracle.synth_dense_bucket(0, 1, 0, rows, rows, cols, 50 + b, pas[b], b) for b in range(W)]
         dev = [torch.from_numpy(h).cuda() for h in host]
@@ -655,7 +655,7 @@ def test_native_group_rccl_world1(oracle, vt):
     fmt = DataDesc(1, 0, vt)
     g = NativeShardGroup(fmt, rows, cols, 0, 1, NativeShardGroup.unique_id(), device=0, pieces=4)
     try:
-        g.store.rand(3)
+        g.store.synth_fill(3)
         pas = [1, 3, 7, 9, 11]  # coprime with 1000: each push lists every row once
         host = [oracle.synth_dense_bucket(0, vt, 0, rows, rows, cols, 70 + b, pas[b], 3 * b) for b in range(W)]
         dev = [torch.from_numpy(h).cuda() for h in host]
@@ -737,7 +737,7 @@ def test_shard_group_orders_after_producer_stream(oracle):
         fmt = DataDesc(1, 0, 0)
         L = _lib.load()
         g = ShardGroup(fmt, rows, cols, 0, 1, device=0)
-        g.store.rand(5)
+        g.store.synth_fill(5)
         # a large first kernel on the caller's stream delays the producers behind it
         big = torch.empty(1 << 30, dtype=torch.uint8, device="cuda")
         bufs = [torch.empty(rows * (4 + 4 * cols), dtype=torch.uint8, device="cuda") for _ in range(2 * W)]
@@ -998,7 +998,7 @@ def test_empty_and_single_record_pushes(oracle, kind, api):
 def test_int_array_repeated_keys_exact_error_state(oracle, case):
     """IntArrayStore pushes that list a key several times (legal bytes, never produced by
     SparseArray.writeMap): the reference adds in record order and throws after the first add
-    that leaves a counter negative (IntArrayStore.java:294-310). Per-push atomics get the sums
+    that leaves a counter negative (IntArrayStore.java:97-113). Per-push atomics get the sums
     right but not that position — e.g. 1 + (-2) + 5 is negative after the first add in record
     order, never in the order (+5, -2). The store detects the repeat (per-element push tokens)
     and re-runs the chunk in record order: data, error key and the no-further-pushes state
@@ -1048,3 +1048,138 @@ def test_int_array_repeated_keys_exact_error_state(oracle, case):
             s.handlePushBatch(fmt, pushes) if api == "batch" else [s.handlePush(fmt, p) for p in pushes]
         assert kat.bits_equal(s.values(), o.data)
         s.close()
+
+
+@pytest.mark.parametrize("async_push", [False, True])
+def test_pinned_push_matches_oracle(oracle, async_push):
+    """Row f2 (wire ingest into pinned memory): pushes that sit in pinned host
+    buffers (pinned_empty = dml_host_alloc, what the JNI DirectByteBuffer wraps) are
+    DMA'd without staging, one at a time and as a batch, synchronous and
+    DML_FLAG_ASYNC; bit-exact vs the oracle. The buffers are overwritten right
+    after each call returns: the bytes are borrowed for the call only
+    (PSAgent.java:278-281), so the store must have captured them by then."""
+    from distml_amd import DataDesc, DataStore, KeyRange, encode_matrix_push, encode_array_push
+    from distml_amd.store import pinned_empty
+    rng = np.random.default_rng(11)
+    for fmt, cols in ((DataDesc(1, 0, 1), 300), (DataDesc(0, 1, 0), 1)):
+        rows = 777
+        st = DataStore(fmt, KeyRange(0, rows - 1), cols, async_push=async_push)
+        o = oracle_store(oracle, fmt, 0, rows - 1, cols)
+        if fmt.valueType == 0:
+            init = rng.integers(100, 200, size=(rows, cols)).astype(np.int32)
+        else:
+            init = rng.standard_normal((rows, cols)).astype(np.float32)
+        st.load_values(init)
+        o.data[:] = init
+        pushes = []
+        for b in range(5):
+            keys = rng.permutation(rows)[: rows - 50 * b]
+            if fmt.dataType == 1:
+                v = (rng.standard_normal((len(keys), cols)) * 1e-3).astype(np.float32)
+                pushes.append(encode_matrix_push(keys, v, fmt.keyType, fmt.valueType))
+            else:
+                v = rng.integers(-3, 4, size=len(keys)).astype(np.int32)
+                pushes.append(encode_array_push(keys, v, fmt.keyType, fmt.valueType))
+        pin = [pinned_empty(len(p)) for p in pushes]
+        # one at a time
+        for p, buf in zip(pushes[:2], pin[:2]):
+            buf[:] = np.frombuffer(p, np.uint8)
+            st.handlePush(fmt, buf)
+            buf[:] = 0xAB  # the caller reuses its buffer at once
+            assert o.push(p) == 0
+        # as one batch
+        for p, buf in zip(pushes[2:], pin[2:]):
+            buf[:] = np.frombuffer(p, np.uint8)
+        st.handlePushBatch(fmt, pin[2:])
+        for buf in pin[2:]:
+            buf[:] = 0xCD
+        for p in pushes[2:]:
+            assert o.push(p) == 0
+        st.flush()
+        assert st.values().tobytes() == o.data.tobytes()
+        st.close()
+
+
+def test_rand_reference_distributions():
+    """DataStore.rand (dml_store_rand): FloatMatrixStore's (nextInt(100)/100f - 0.5f)
+    / rowSize values (FloatMatrixStore.java:39-51; AdaGrad :55-66) — every value one of
+    the 100 float results, each a near-uniform share; DoubleMatrixStore's |gaussian|
+    rows of unit norm (DoubleMatrixStore.java:192-207); int / array stores unchanged
+    (DataStore.rand is a no-op, DataStore.java:22). Seeded: same seed, same values."""
+    from distml_amd import DataDesc, DataStore, KeyRange
+    rows, cols = 2000, 50
+    allowed = {((np.float32(a) / np.float32(100.0)) - np.float32(0.5)) / np.float32(cols) for a in range(100)}
+    for ada in (False, True):
+        st = DataStore(DataDesc(1, 0, 1, False, True, ada), KeyRange(0, rows - 1), cols)
+        st.rand(5)
+        v = st.values()
+        st2 = DataStore(DataDesc(1, 0, 1, False, True, ada), KeyRange(0, rows - 1), cols)
+        st2.rand(5)
+        assert v.tobytes() == st2.values().tobytes()
+        uniq, cnt = np.unique(v, return_counts=True)
+        assert set(uniq.tolist()) <= {float(x) for x in allowed} and len(uniq) == 100
+        assert cnt.min() > 0.8 * v.size / 100 and cnt.max() < 1.2 * v.size / 100
+        st.close()
+        st2.close()
+    st = DataStore(DataDesc(1, 1, 3), KeyRange(0, rows - 1), 10)
+    st.rand(9)
+    v = st.values()
+    assert np.all(v >= 0)
+    assert np.allclose(np.sqrt((v * v).sum(axis=1)), 1.0, rtol=1e-12)
+    assert 0.2 < np.median(v) < 0.3  # median of |N(0,1)| / sqrt(10 E[g^2]) ~ 0.674 / 3.16
+    st.close()
+    for fmt, c in ((DataDesc(1, 0, 0), 7), (DataDesc(0, 1, 1), 1), (DataDesc(0, 0, 0), 1)):
+        st = DataStore(fmt, KeyRange(0, 99), c)
+        st.rand(1)
+        assert not st.values().any()
+        st.close()
+
+
+@pytest.mark.parametrize("ada", [False, True])
+def test_config4_full_shard_bit_exact(oracle, ada):
+    """BASELINE config 4 at the full per-GPU shard bench.py --config 4 times:
+    1 250 000 x 200 fp32 (linearSplit(8) of 10M rows), full-range pushes with every
+    row permuted per push, device-resident, one batch — bit-exact against the oracle
+    (VERDICT r1 #10). Plain sum: W = 8, oracle row-partitioned over 16 threads (each
+    thread still applies its rows' adds in push order). AdaGrad (data, alpha, delta,
+    maxDelta): W = 4, oracle single thread."""
+    import ctypes as C
+    import math
+    from distml_amd import DataDesc, DataStore, KeyRange, _lib
+    rows, cols = 1_250_000, 200
+    W = 4 if ada else 8
+    fmt = DataDesc(1, 0, 1, False, True, ada)
+    L = _lib.load()
+    st = DataStore(fmt, KeyRange(0, rows - 1), cols)
+    o = oracle_store(oracle, fmt, 0, rows - 1, cols)
+    if ada:
+        st.setAlpha(0.025, 0.0001, 1.0)
+        o.set_alpha(0.025, 0.0001, 1.0)
+    st.synth_fill(13)
+    o.synth_fill(13)
+
+    def perm(b):
+        a = (3000 + b) * 2654435761 % rows | 1
+        while math.gcd(a, rows) != 1:
+            a += 1
+        return a, b * 7919 % rows
+
+    dev, host = [], []
+    s0 = torch.cuda.current_stream().cuda_stream
+    for b in range(W):
+        pa, pc = perm(b)
+        t = torch.empty(rows * (4 + 4 * cols), dtype=torch.uint8, device="cuda")
+        assert L.dml_synth_dense_bucket(t.data_ptr(), C.byref(fmt.to_c()), 0, rows, rows, cols, 3000 + b, pa, pc,
+                                        C.c_void_p(s0)) == 0
+        dev.append(t)
+        host.append(oracle.synth_dense_bucket(0, 1, 0, rows, rows, cols, 3000 + b, pa, pc))
+    torch.cuda.synchronize()
+    st.pushDevice([t.data_ptr() for t in dev], [t.numel() for t in dev])
+    st.flush()
+    assert o.push_many(host, threads=1 if ada else 16) == 0
+    assert st.values().tobytes() == o.data.tobytes()
+    if ada:
+        a, d = st.adagrad_state()
+        assert a.tobytes() == o.alpha.tobytes() and d.tobytes() == o.delta.tobytes()
+        assert st.maxDelta() == o.max_delta()
+    st.close()

@@ -57,7 +57,7 @@ def test_oracle_fetch_and_checkpoint_layout(oracle):
             np.array([10], "<i4").tobytes() + np.array([1.0, -2.0], "<f4").tobytes())
     assert out == want
     assert s.write_all() == s.data.astype(">f4").tobytes()
-    # FloatArrayStore fetch: 4 value bytes in an 8-byte zeroed slot (FloatArrayStore.java:362-376)
+    # FloatArrayStore fetch: 4 value bytes in an 8-byte zeroed slot (FloatArrayStore.java:92-105)
     a = oracle.OracleStore(0, 1, 1, 0, 3)
     a.data[:] = np.array([[1.0], [2.0], [3.0], [4.0]], np.float32)
     assert a.fetch([2]) == np.array([2], "<i8").tobytes() + np.array([3.0], "<f4").tobytes() + b"\0" * 4
