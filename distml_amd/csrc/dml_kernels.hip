@@ -58,11 +58,9 @@ __device__ inline u32x4 pack(const T* v) {
 // ---------------------------------------------------------------------------
 // k_index: one thread per record of push b (blockIdx.y): slot[row][b] = record.
 // A key outside the shard lowers ctrl->cutoff to the record's start position.
-// Rows listed twice by one push are flagged (rowflag[row] = 1): the reduce
-// skips them and the host replays just those rows through the exact layered
-// path. PLAIN: plain stores + k_verify (no scattered returning atomics);
-// otherwise atomicExch detects the repeat directly.
-template <bool PLAIN>
+// Rows listed twice by one push are flagged (rowflag[row] = 1): atomicExch sees
+// the earlier record; the reduce skips those rows and the host replays just
+// them through the exact layered path.
 __global__ __launch_bounds__(256) void k_index(const Batch bt, int64_t stride, int K, int64_t first, int64_t rows,
                                                int32_t* __restrict__ slot, uint32_t* __restrict__ rowflag,
                                                Ctrl* __restrict__ ctrl, uint64_t tail_cut) {
@@ -77,101 +75,18 @@ __global__ __launch_bounds__(256) void k_index(const Batch bt, int64_t stride, i
         atomicMin(&ctrl->cutoff, (unsigned long long)pos_of((uint64_t)bt.bidx[b], (uint64_t)off));
         return;
     }
-    if constexpr (PLAIN) {
-        *(DML_GLOBAL int32_t*)&slot[idx * slot_stride((int)gridDim.y) + b] = (int32_t)r;
-    } else {
-        const int32_t old = atomicExch(&slot[idx * slot_stride((int)gridDim.y) + b], (int32_t)r);
-        if (old != -1) {
-            rowflag[idx] = 1u;
-            ctrl->no_dup = 0u;  // benign race: every writer stores the same value
-        }
-    }
-}
-
-// k_index_multi: as k_index<false>, RPT records per thread (records
-// blockIdx.x*256*RPT + j*256 + tid): all RPT key loads, then all RPT
-// returning atomics, in flight together — fewer, shorter-lived waves beside
-// the previous chunk's reduce.
-template <int RPT>
-__global__ __launch_bounds__(256) void k_index_multi(const Batch bt, int64_t stride, int K, int64_t first,
-                                                     int64_t rows, int32_t* __restrict__ slot,
-                                                     uint32_t* __restrict__ rowflag, Ctrl* __restrict__ ctrl,
-                                                     uint64_t tail_cut) {
-    const int b = blockIdx.y;
-    const int64_t r0 = (int64_t)blockIdx.x * 256 * RPT + threadIdx.x;
-    if (r0 == 0 && b == 0 && tail_cut != kNoPos) atomicMin(&ctrl->cutoff, (unsigned long long)tail_cut);
-    const int64_t nrec = bt.nrec[b];
-    const uint8_t* base = bt.base[b];
-    int64_t idx[RPT];
-#pragma unroll
-    for (int j = 0; j < RPT; ++j) {
-        const int64_t r = r0 + j * 256;
-        idx[j] = r < nrec ? row_index(ld_key(base + r * stride, K), first, rows) : -2;
-    }
-    int32_t old[RPT];
-#pragma unroll
-    for (int j = 0; j < RPT; ++j) {
-        old[j] = -1;
-        if (idx[j] >= 0) old[j] = atomicExch(&slot[idx[j] * slot_stride((int)gridDim.y) + b], (int32_t)(r0 + j * 256));
-    }
-#pragma unroll
-    for (int j = 0; j < RPT; ++j) {
-        if (idx[j] == -1)
-            atomicMin(&ctrl->cutoff, (unsigned long long)pos_of((uint64_t)bt.bidx[b], (uint64_t)((r0 + j * 256) * stride)));
-        if (old[j] != -1) {
-            rowflag[idx[j]] = 1u;
-            ctrl->no_dup = 0u;  // benign race: every writer stores the same value
-        }
-    }
-}
-
-// k_verify (after k_index<true>): a record whose slot holds another record lost
-// a race with a record of the same row and push -> flag the row.
-__global__ __launch_bounds__(256) void k_verify(const Batch bt, int64_t stride, int K, int64_t first, int64_t rows,
-                                                const int32_t* __restrict__ slot, uint32_t* __restrict__ rowflag,
-                                                Ctrl* __restrict__ ctrl) {
-    const int b = blockIdx.y;
-    const int64_t r = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (r >= bt.nrec[b]) return;
-    const int64_t idx = row_index(ld_key(bt.base[b] + r * stride, K), first, rows);
-    if (idx < 0) return;
-    if (slot[idx * slot_stride((int)gridDim.y) + b] != (int32_t)r) {
+    const int32_t old = atomicExch(&slot[idx * slot_stride((int)gridDim.y) + b], (int32_t)r);
+    if (old != -1) {
         rowflag[idx] = 1u;
-        ctrl->no_dup = 0u;
+        ctrl->no_dup = 0u;  // benign race: every writer stores the same value
     }
-}
-
-int index_variant() {
-    const char* v = getenv("DML_INDEX_VARIANT");
-    return v ? atoi(v) : 0;
 }
 
 hipError_t launch_index(const Batch& bt, int nb, int64_t max_nrec, int64_t stride, int K, int64_t first,
                         int64_t rows, int32_t* slot, uint32_t* rowflag, Ctrl* ctrl, uint64_t tail_cut, hipStream_t st) {
     if (nb <= 0) return hipSuccess;
     dim3 grid((unsigned)std::max<int64_t>(1, (max_nrec + 255) / 256), (unsigned)nb);
-    const int iv = index_variant();
-    if (iv == 2 || iv == 3) {
-        const int rpt = iv == 2 ? 8 : 4;
-        dim3 g((unsigned)std::max<int64_t>(1, (max_nrec + 256 * rpt - 1) / (256 * rpt)), (unsigned)nb);
-        if (rpt == 8)
-            hipLaunchKernelGGL(k_index_multi<8>, g, dim3(256), 0, st, bt, stride, K, first, rows, slot, rowflag, ctrl,
-                               tail_cut);
-        else
-            hipLaunchKernelGGL(k_index_multi<4>, g, dim3(256), 0, st, bt, stride, K, first, rows, slot, rowflag, ctrl,
-                               tail_cut);
-        return hipGetLastError();
-    }
-    if (iv == 0) {
-        hipLaunchKernelGGL(k_index<false>, grid, dim3(256), 0, st, bt, stride, K, first, rows, slot, rowflag, ctrl,
-                           tail_cut);
-        return hipGetLastError();
-    }
-    hipLaunchKernelGGL(k_index<true>, grid, dim3(256), 0, st, bt, stride, K, first, rows, slot, rowflag, ctrl,
-                       tail_cut);
-    hipError_t e = hipGetLastError();
-    if (e != hipSuccess) return e;
-    hipLaunchKernelGGL(k_verify, grid, dim3(256), 0, st, bt, stride, K, first, rows, slot, rowflag, ctrl);
+    hipLaunchKernelGGL(k_index, grid, dim3(256), 0, st, bt, stride, K, first, rows, slot, rowflag, ctrl, tail_cut);
     return hipGetLastError();
 }
 
@@ -648,66 +563,7 @@ __global__ __launch_bounds__(64 * WPB) void k_reduce_rows(T* __restrict__ shard,
             if ((live >> r & 1u) && lane < nb) slot[row[r] * slot_stride(nb) + lane] = -1;
     }
     const uint64_t vbase = lane < nb ? (uint64_t)bt.base[lane] : 0ull;
-    if constexpr (DEPTH == 2) {
-        static_assert(FULL, "two-deep ring: whole-vector rows only");
-        // Two pushes' loads in flight (a ring of two register sets): push b+2's loads
-        // are issued as soon as push b is added, so the wave never drains its loads.
-        // Absent rows and pushes past the batch load a live row (an L2 hit) and add nothing.
-        auto issue = [&](int b, u32x4 (&raw)[RPW][CPW], unsigned& h, int32_t (&rrb)[RPW]) {
-            const int bb = b < nb ? b : (nb > 0 ? nb - 1 : 0);
-            const uint8_t* bp =
-                (const uint8_t*)(((uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)vbase, bb)) |
-                                 ((uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)(vbase >> 32), bb) << 32));
-            h = 0;
-#pragma unroll
-            for (int r = 0; r < RPW; ++r) {
-                rrb[r] = b < nb ? __builtin_amdgcn_readlane(vslot[r], bb) : -1;
-                h |= (rrb[r] >= 0 ? 1u : 0u) << r;
-                const uint8_t* rb = rrb[r] >= 0 ? bp + (int64_t)rrb[r] * stride + voff[0] : fbv;
-#pragma unroll
-                for (int c = 0; c < CPW; ++c) {
-                    const uint8_t* src = rb + c * 64 * VEC * (int)sizeof(T);
-                    raw[r][c] = NT ? ldg16_nt(src) : ldg16(src);
-                }
-            }
-        };
-        auto consume = [&](const u32x4 (&raw)[RPW][CPW], unsigned h, const int32_t (&rrb)[RPW], int b) {
-            touched |= h;
-#pragma unroll
-            for (int r = 0; r < RPW; ++r) {
-                const bool on = (h >> r) & 1u;
-#pragma unroll
-                for (int c = 0; c < CPW; ++c) {
-                    T t[VEC];
-                    unpack<T>(raw[r][c], t);
-#pragma unroll
-                    for (int e = 0; e < VEC; ++e) {
-                        const T sum = Elem<T>::add(acc[r][c][e], t[e]);
-                        if constexpr (MODE == kAddCheckI32) {
-                            if (on && sum < 0) {
-                                const uint64_t p = pos_of((uint64_t)bt.bidx[b < nb ? b : 0],
-                                                          (uint64_t)((int64_t)rrb[r] * stride + voff[c] + e * (int64_t)sizeof(T)));
-                                negpos = p < negpos ? p : negpos;
-                            }
-                        }
-                        acc[r][c][e] = on ? sum : acc[r][c][e];  // a select: an absent row keeps its bits (-0.0)
-                    }
-                }
-            }
-        };
-        u32x4 ra[RPW][CPW], rb2[RPW][CPW];
-        unsigned ha, hb;
-        int32_t rra[RPW], rrb2[RPW];
-        issue(0, ra, ha, rra);
-        issue(1, rb2, hb, rrb2);
-#pragma unroll 1
-        for (int b = 0; b < nb; b += 2) {
-            consume(ra, ha, rra, b);
-            issue(b + 2, ra, ha, rra);
-            consume(rb2, hb, rrb2, b + 1);
-            issue(b + 3, rb2, hb, rrb2);
-        }
-    } else if constexpr (DEPTH == 3) {
+    if constexpr (DEPTH == 3) {
         // Pair-packed: the wave's (push, row) records in push order, RPW of them per
         // load group whatever push they come from. A batch whose pushes list few of
         // these rows (LDA's and Word2Vec's touched-row pushes) keeps RPW x CPW loads in
@@ -869,16 +725,7 @@ __global__ __launch_bounds__(64 * WPB) void k_reduce_rows(T* __restrict__ shard,
         for (int c = 0; c < CPW; ++c) {
             T* prow = rowp[r] + c0[c];
             if (nv[c] == VEC) {
-                // SNT: 0 plain, 1 non-temporal, 2 write-through (sc1: no dirty L2 line left
-                // for the kernel-end writeback)
-                if constexpr (SNT == 2) {
-                    const uint64_t rb = (uint64_t)rowp[r];
-                    const void* base = (const void*)(((uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)rb)) |
-                                                     ((uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)(rb >> 32)) << 32));
-                    const auto rsrc = __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(base), 0,
-                                                                        cols * (int)sizeof(T), 0x00020000);
-                    __builtin_amdgcn_raw_buffer_store_b128(pack<T>(acc[r][c]), rsrc, c0[c] * (int)sizeof(T), 0, 16);
-                } else if constexpr (SNT == 1) {
+                if constexpr (SNT == 1) {
                     stg16_nt(prow, pack<T>(acc[r][c]));
                 } else {
                     stg16(prow, pack<T>(acc[r][c]));
@@ -912,17 +759,16 @@ static hipError_t launch_reduce_t(void* shard, int64_t rows, int32_t cols, const
     const int64_t nblocks = (ntask + WPB - 1) / WPB;
     if (nblocks_out) *nblocks_out = nblocks;
     if (nblocks <= 0) return hipSuccess;
-    // blocks per CU: the shape's cap, or DML_REDUCE_LDS bytes of dynamic LDS (occupancy study)
-    static const char* lds_env = getenv("DML_REDUCE_LDS");
-    const unsigned occ_lds = lds_env ? (unsigned)atoi(lds_env) : lds_for_blocks_per_cu(bpc);
+    // blocks per CU: the shape's cap (unused dynamic LDS), 0 = none
+    const unsigned occ_lds = lds_for_blocks_per_cu(bpc);
     if constexpr (RPW > 1) {
         static_assert(MODE != kAdaGrad && MODE != kRollbackI32, "k_reduce_rows shapes");
         if (ev.start || ev.stop)
-            hipExtLaunchKernelGGL((k_reduce_rows<T, MODE, CPW, RPW, NT, FULL, G == 3 ? 3 : (FULL && G == 2) ? 2 : 1, WPB, SNT>), dim3((unsigned)nblocks),
+            hipExtLaunchKernelGGL((k_reduce_rows<T, MODE, CPW, RPW, NT, FULL, G == 3 ? 3 : 1, WPB, SNT>), dim3((unsigned)nblocks),
                                   dim3(64 * WPB), occ_lds, st, ev.start, ev.stop, 0, (T*)shard, rows, cols, ngroups, bt, nb, stride,
                                   K, const_cast<int32_t*>(slot), rowflag, ctrl, tail_cut, rm);
         else
-            hipLaunchKernelGGL((k_reduce_rows<T, MODE, CPW, RPW, NT, FULL, G == 3 ? 3 : (FULL && G == 2) ? 2 : 1, WPB, SNT>), dim3((unsigned)nblocks),
+            hipLaunchKernelGGL((k_reduce_rows<T, MODE, CPW, RPW, NT, FULL, G == 3 ? 3 : 1, WPB, SNT>), dim3((unsigned)nblocks),
                                dim3(64 * WPB), occ_lds, st, (T*)shard, rows, cols, ngroups, bt, nb, stride, K, const_cast<int32_t*>(slot), rowflag,
                                ctrl, tail_cut, rm);
     } else {
@@ -936,18 +782,6 @@ static hipError_t launch_reduce_t(void* shard, int64_t rows, int32_t cols, const
                                tail_cut, ada, rm);
     }
     return hipGetLastError();
-}
-
-// Tuning variants of the f32 plain reduce (env DML_REDUCE_VARIANT, read per launch;
-// 0 = auto = the shape rule below). Kept for A/B runs (scripts/tune.py):
-// G = pushes per load group, CPW = chunks per wave, RPW = rows per wave.
-// 10: G4/CPW4/RPW1 (the previous rule, k_reduce), 13: same with plain loads, 14: G2/CPW4/RPW1,
-// 20: CPW4/RPW4 (k_reduce_rows), 21: CPW4/RPW2, 24: CPW4/RPW4 plain loads, 27: CPW2/RPW4,
-// 28: CPW4/RPW2 FULL uncapped, 29: CPW4/RPW4 FULL, 30: CPW4/RPW4 FULL two-deep ring, 31: CPW4/RPW2 FULL two-deep ring
-// (0 = auto: CPW4/RPW2 FULL, 2 blocks per CU, for config 2).
-int reduce_variant() {
-    const char* v = getenv("DML_REDUCE_VARIANT");
-    return v ? atoi(v) : 0;
 }
 
 // Shape rule (measured, scripts/ubench_reduce.hip, scripts/exp_variants.py): a
@@ -968,59 +802,41 @@ static hipError_t launch_auto(void* shard, int64_t rows, int32_t cols, const Bat
 #define DML_LF(G, CPW, RPW, BPC) launch_reduce_t<T, MODE, G, true, 4, false, CPW, RPW, true>(shard, rows, cols, bt, nb, \
                                                      stride, K, slot, rowflag, ctrl, tail_cut, ada, st, nblocks_out, ev, rm, BPC)
     if constexpr (MODE == kAdaGrad) {
-        // default G8 with nt shard / delta / alpha traffic (measured best).
-        // DML_ADA_VARIANT (A/B, read once): 1 G4 cached, 2 G16 cached, 3 G8 nt, 4 plain loads,
-        // 5 WPB 8 cached, 7 G8 cached (the previous default), 8 G4 nt, 9 G16 nt, 10 G8 nt WPB 8
-        // (the candidate buffer holds one entry per 4-wave block: no WPB below 4)
-        static const int av = getenv("DML_ADA_VARIANT") ? atoi(getenv("DML_ADA_VARIANT")) : 0;
-        switch (av) {
-            case 1: return DML_L(4, 1, 1);
-            case 2: return DML_L(16, 1, 1);
-            case 3: return launch_reduce_t<T, MODE, 8, true, 4, true, 1, 1>(shard, rows, cols, bt, nb, stride, K, slot, rowflag, ctrl, tail_cut, ada, st, nblocks_out, ev, rm);
-            case 4: return launch_reduce_t<T, MODE, 8, false, 4, false, 1, 1>(shard, rows, cols, bt, nb, stride, K, slot, rowflag, ctrl, tail_cut, ada, st, nblocks_out, ev, rm);
-            case 5: return launch_reduce_t<T, MODE, 8, true, 8, false, 1, 1>(shard, rows, cols, bt, nb, stride, K, slot, rowflag, ctrl, tail_cut, ada, st, nblocks_out, ev, rm);
-            case 7: return DML_L(8, 1, 1);
-            case 8: return launch_reduce_t<T, MODE, 4, true, 4, true, 1, 1>(shard, rows, cols, bt, nb, stride, K, slot, rowflag, ctrl, tail_cut, ada, st, nblocks_out, ev, rm);
-            case 9: return launch_reduce_t<T, MODE, 16, true, 4, true, 1, 1>(shard, rows, cols, bt, nb, stride, K, slot, rowflag, ctrl, tail_cut, ada, st, nblocks_out, ev, rm);
-            case 10: return launch_reduce_t<T, MODE, 8, true, 8, true, 1, 1>(shard, rows, cols, bt, nb, stride, K, slot, rowflag, ctrl, tail_cut, ada, st, nblocks_out, ev, rm);
-            default: return launch_reduce_t<T, MODE, 8, true, 4, true, 1, 1>(shard, rows, cols, bt, nb, stride, K, slot, rowflag, ctrl, tail_cut, ada, st, nblocks_out, ev, rm);
-        }
+        // G8 with nt shard / delta / alpha traffic (measured best: G4 +10 %, G16 +35 %,
+        // 8-wave blocks +15 %, cached stores slower). The candidate buffer
+        // holds one entry per 4-wave block.
+        return launch_reduce_t<T, MODE, 8, true, 4, true, 1, 1>(shard, rows, cols, bt, nb, stride, K, slot, rowflag,
+                                                                ctrl, tail_cut, ada, st, nblocks_out, ev, rm);
     } else if constexpr (MODE == kRollbackI32) {
         return DML_L(8, 1, 1);
     } else {
         if (cols < VEC) return DML_L(16, 1, 1);  // narrower than one vector: k_reduce's generic path
-        // pair-packed load groups (k_reduce_rows DEPTH 3) unless DML_PAIRS=0 (A/B)
-        static const bool pairs = !(getenv("DML_PAIRS") && atoi(getenv("DML_PAIRS")) == 0);
         // whole 4-KiB rows: two rows per wave and at most 8 waves per CU (64 KiB of
         // loads in flight per CU) measured 3.5-5 % faster than 4 rows per wave at the
-        // register-limited 12-24 waves (scripts/exp_variants.py)
+        // register-limited 12-24 waves
         if (cols % (64 * VEC * 4) == 0) return DML_LF(1, 4, 2, 2);
-        static const int nf_rpw = getenv("DML_NF_RPW") ? atoi(getenv("DML_NF_RPW")) : 4;  // A/B knob
-        // Non-temporal shard stores on the other shapes (the rows are written once per
-        // batch): config 5 460 -> 433 us; config 2's FULL shape measured no gain
-        // (variant 34). Pre-reduce partials are read back by RCCL right away: cached.
-        // DML_NF_SNT (A/B, read once): 0 plain stores for every mode.
-        static const bool nf_snt = !(getenv("DML_NF_SNT") && atoi(getenv("DML_NF_SNT")) == 0);
-        if (nf_snt && MODE != kPreReduce) {
+        // Other widths: pair-packed load groups (DEPTH 3) over 4 rows per wave.
+        // Non-temporal shard stores (the rows are written once per batch): config 5
+        // 460 -> 433 us; config 2's FULL shape measured no gain. Pre-reduce partials
+        // are read back by RCCL right away: cached.
 #define DML_LN(G, CPW, RPW) launch_reduce_t<T, MODE, G, true, 4, 1, CPW, RPW>(shard, rows, cols, bt, nb, stride, K, \
                                                      slot, rowflag, ctrl, tail_cut, ada, st, nblocks_out, ev, rm)
 #define DML_LFN(G, CPW, RPW) launch_reduce_t<T, MODE, G, true, 4, 1, CPW, RPW, true>(shard, rows, cols, bt, nb, \
                                                      stride, K, slot, rowflag, ctrl, tail_cut, ada, st, nblocks_out, ev, rm, 0)
-            if (nchunks >= 4 && nf_rpw == 2) return DML_LN(3, 4, 2);
-            if (nchunks >= 4) return pairs ? DML_LN(3, 4, 4) : DML_LN(1, 4, 4);
+        if (MODE != kPreReduce) {
+            if (nchunks >= 4) return DML_LN(3, 4, 4);
             if (cols % (64 * VEC * 2) == 0) return DML_LFN(1, 2, 4);
-            if (nchunks >= 2) return pairs ? DML_LN(3, 2, 4) : DML_LN(1, 2, 4);
+            if (nchunks >= 2) return DML_LN(3, 2, 4);
             if (cols % (64 * VEC) == 0) return DML_LFN(1, 1, 4);
-            return pairs ? DML_LN(3, 1, 4) : DML_LN(1, 1, 4);
+            return DML_LN(3, 1, 4);
+        }
 #undef DML_LN
 #undef DML_LFN
-        }
-        if (nchunks >= 4 && nf_rpw == 2) return DML_L(3, 4, 2);
-        if (nchunks >= 4) return pairs ? DML_L(3, 4, 4) : DML_L(1, 4, 4);
+        if (nchunks >= 4) return DML_L(3, 4, 4);
         if (cols % (64 * VEC * 2) == 0) return DML_LF(1, 2, 4, 0);
-        if (nchunks >= 2) return pairs ? DML_L(3, 2, 4) : DML_L(1, 2, 4);
+        if (nchunks >= 2) return DML_L(3, 2, 4);
         if (cols % (64 * VEC) == 0) return DML_LF(1, 1, 4, 0);
-        return pairs ? DML_L(3, 1, 4) : DML_L(1, 1, 4);
+        return DML_L(3, 1, 4);
     }
 #undef DML_L
 #undef DML_LF
@@ -1031,10 +847,6 @@ bool reduce_clears_slots(int vtype, int mode, int32_t cols) {
     if (mode != kAdd && mode != kPreReduce) return false;
     const int VEC = vtype == kF64 ? 2 : 4;
     if (cols < VEC) return false;  // k_reduce's generic path
-    if (vtype == kF32 && mode == kAdd) {
-        const int v = reduce_variant();
-        if (v == 10 || v == 13 || v == 14 || v == 40 || v == 41 || v == 44) return false;  // one-row k_reduce variants
-    }
     return true;
 }
 
@@ -1050,37 +862,8 @@ hipError_t launch_reduce(int vtype, int mode, void* shard, int64_t rows, int32_t
                          uint64_t tail_cut, const AdaArgs& ada, hipStream_t st, int64_t* nblocks_out, LaunchEv ev,
                          RowMap rm) {
 #define DML_A(T, M) launch_auto<T, M>(shard, rows, cols, bt, nb, stride, K, slot, rowflag, ctrl, tail_cut, ada, st, nblocks_out, ev, rm)
-#define DML_V(G, NT, WPB, SNT, CPW, RPW) launch_reduce_t<float, kAdd, G, NT, WPB, SNT, CPW, RPW, false>(shard, rows, cols, bt, nb, stride, K, slot, rowflag, ctrl, tail_cut, ada, st, nblocks_out, ev)
     if (vtype == kF32) {
-        if (mode == kAdd) {
-            switch (reduce_variant()) {
-                case 10: return DML_V(4, true, 4, false, 4, 1);
-                case 13: return DML_V(4, false, 4, false, 4, 1);
-                case 14: return DML_V(2, true, 4, false, 4, 1);
-                case 20: return DML_V(1, true, 4, false, 4, 4);
-                case 21: return DML_V(1, true, 4, false, 4, 2);
-                case 24: return DML_V(1, false, 4, false, 4, 4);
-                case 27: return DML_V(1, true, 4, false, 2, 4);
-                case 30: return launch_reduce_t<float, kAdd, 2, true, 4, false, 4, 4, true>(shard, rows, cols, bt, nb, stride, K, slot, rowflag, ctrl, tail_cut, ada, st, nblocks_out, ev);
-                case 31: return launch_reduce_t<float, kAdd, 2, true, 4, false, 4, 2, true>(shard, rows, cols, bt, nb, stride, K, slot, rowflag, ctrl, tail_cut, ada, st, nblocks_out, ev);
-                case 28: return launch_reduce_t<float, kAdd, 1, true, 4, false, 4, 2, true>(shard, rows, cols, bt, nb, stride, K, slot, rowflag, ctrl, tail_cut, ada, st, nblocks_out, ev);
-                case 32: return launch_reduce_t<float, kAdd, 1, true, 8, false, 4, 2, true>(shard, rows, cols, bt, nb, stride, K, slot, rowflag, ctrl, tail_cut, ada, st, nblocks_out, ev, {}, 1);
-                case 33: return launch_reduce_t<float, kAdd, 1, true, 2, false, 4, 2, true>(shard, rows, cols, bt, nb, stride, K, slot, rowflag, ctrl, tail_cut, ada, st, nblocks_out, ev, {}, 4);
-                case 34: return launch_reduce_t<float, kAdd, 1, true, 4, true, 4, 2, true>(shard, rows, cols, bt, nb, stride, K, slot, rowflag, ctrl, tail_cut, ada, st, nblocks_out, ev, {}, 2);
-                case 35: return launch_reduce_t<float, kAdd, 1, true, 1, false, 4, 2, true>(shard, rows, cols, bt, nb, stride, K, slot, rowflag, ctrl, tail_cut, ada, st, nblocks_out, ev, {}, 8);
-                case 37: return launch_reduce_t<float, kAdd, 1, true, 4, 2, 4, 2, true>(shard, rows, cols, bt, nb, stride, K, slot, rowflag, ctrl, tail_cut, ada, st, nblocks_out, ev, {}, 2);
-                case 38: return launch_reduce_t<float, kAdd, 3, true, 4, 0, 4, 2, true>(shard, rows, cols, bt, nb, stride, K, slot, rowflag, ctrl, tail_cut, ada, st, nblocks_out, ev, {}, 2);
-                case 36: return launch_reduce_t<float, kAdd, 1, true, 4, false, 4, 1 + 1, true>(shard, rows, cols, bt, nb, stride, K, slot, rowflag, ctrl, tail_cut, ada, st, nblocks_out, ev, {}, 2);
-                case 29: return launch_reduce_t<float, kAdd, 1, true, 4, false, 4, 4, true>(shard, rows, cols, bt, nb, stride, K, slot, rowflag, ctrl, tail_cut, ada, st, nblocks_out, ev);
-                // narrow rows (config 4, 200 cols): one-row k_reduce with G pushes per load group, nt
-                case 40: return launch_reduce_t<float, kAdd, 8, true, 4, 1, 1, 1>(shard, rows, cols, bt, nb, stride, K, slot, rowflag, ctrl, tail_cut, ada, st, nblocks_out, ev);
-                case 41: return launch_reduce_t<float, kAdd, 4, true, 4, 1, 1, 1>(shard, rows, cols, bt, nb, stride, K, slot, rowflag, ctrl, tail_cut, ada, st, nblocks_out, ev);
-                case 42: return launch_reduce_t<float, kAdd, 1, true, 4, 1, 1, 4>(shard, rows, cols, bt, nb, stride, K, slot, rowflag, ctrl, tail_cut, ada, st, nblocks_out, ev);
-                case 43: return launch_reduce_t<float, kAdd, 3, true, 4, 1, 1, 2>(shard, rows, cols, bt, nb, stride, K, slot, rowflag, ctrl, tail_cut, ada, st, nblocks_out, ev);
-                case 44: return launch_reduce_t<float, kAdd, 16, true, 4, 1, 1, 1>(shard, rows, cols, bt, nb, stride, K, slot, rowflag, ctrl, tail_cut, ada, st, nblocks_out, ev);
-                default: return DML_A(float, kAdd);
-            }
-        }
+        if (mode == kAdd) return DML_A(float, kAdd);
         if (mode == kAdaGrad) return DML_A(float, kAdaGrad);
         if (mode == kPreReduce) return DML_A(float, kPreReduce);
     } else if (vtype == kI32) {
@@ -1092,7 +875,6 @@ hipError_t launch_reduce(int vtype, int mode, void* shard, int64_t rows, int32_t
         if (mode == kPreReduce) return DML_A(double, kPreReduce);
     }
 #undef DML_A
-#undef DML_V
     return hipErrorInvalidValue;
 }
 

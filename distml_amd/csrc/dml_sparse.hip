@@ -309,18 +309,11 @@ __global__ __launch_bounds__(256) void k_sp_bounds(const SpPlan pl, const SpMeta
 // owners of repeated rows walk their bucket in ascending comp order. Buckets
 // over kSpBucketMax records (adversarial keys) send the whole leaf to the exact
 // replay before any of its rows is written.
-#ifndef DML_SP_LEAF_THREADS
-#define DML_SP_LEAF_THREADS 512  // 8 waves per leaf (A/B builds override)
-#endif
-constexpr int kSpLeafThreads = DML_SP_LEAF_THREADS;
-// DML_SP_LEAF_EARLY: issue every record's shard load right after its comp is
-// loaded (its row is known then), so the HBM round trip runs under the LDS
-// counting sort and ownership phases. 1: owners add and store in record
-// (unsorted) order from those registers; 2: owners' start values go through
-// LDS and the stores stay in address order.
-#ifndef DML_SP_LEAF_EARLY
-#define DML_SP_LEAF_EARLY 1  // measured: apply 1.53 -> 1.49 ms (config 3); 2: 1.50 ms
-#endif
+constexpr int kSpLeafThreads = 512;  // 8 waves per leaf
+// Every record's shard load is issued right after its comp is loaded (its row
+// is known then), so the HBM round trip runs under the LDS counting sort and
+// the ownership phase; owners then add and store in record order (measured:
+// apply 1.53 -> 1.49 ms on config 3 against loads after the sort).
 constexpr int kSpLines = 2 * kSpLeafThreads;
 constexpr int kSpBucketMax = 64;
 
@@ -366,9 +359,7 @@ __global__ __launch_bounds__(kSpLeafThreads) void k_sp_leaf(T* __restrict__ shar
     __shared__ uint32_t cur[kSpLines];
     __shared__ uint32_t wsum[kT / 64];
     __shared__ int s_over;
-#if DML_SP_LEAF_EARLY
     __shared__ uint8_t oflag[kSpLeafCap];  // record i: bit 0 owns its row, bit 1 row repeated
-#endif
     if (prev && ctrl_abnormal(prev)) return;  // predecessor needs the host first
     const int tid = threadIdx.x;
     const int64_t L = blockIdx.x;
@@ -396,11 +387,9 @@ __global__ __launch_bounds__(kSpLeafThreads) void k_sp_leaf(T* __restrict__ shar
         c[k] = comp[lo + i];
         u[k] = val[lo + i];
     }
-#if DML_SP_LEAF_EARLY
     T x0[kPer];
 #pragma unroll
     for (int k = 0; k < kPer; ++k) x0[k] = shard[c[k] >> 32];  // every comp row lies in this leaf
-#endif
 #pragma unroll
     for (int k = 0; k < kPer; ++k) {
         const int i = tid + k * kT;
@@ -472,11 +461,9 @@ __global__ __launch_bounds__(kSpLeafThreads) void k_sp_leaf(T* __restrict__ shar
         own[k] = first;
         multi[k] = dup;
     }
-#if DML_SP_LEAF_EARLY
 #pragma unroll
     for (int k = 0; k < kPer; ++k)
         if (tid + k * kT < n) oflag[ri[k]] = (uint8_t)((own[k] ? 1 : 0) | (multi[k] ? 2 : 0));
-#endif
     __syncthreads();
     if (s_over) {  // uniform
         if (tid == 0) {
@@ -485,26 +472,6 @@ __global__ __launch_bounds__(kSpLeafThreads) void k_sp_leaf(T* __restrict__ shar
         }
         return;
     }
-#if DML_SP_LEAF_EARLY == 2
-    // owners' start values (shard + their own value) go through sv; the owners
-    // then finish and store in address order
-#pragma unroll
-    for (int k = 0; k < kPer; ++k) {
-        const int i = tid + k * kT;
-        if (i < n && (oflag[i] & 1)) sv[i] = Elem<T>::add(x0[k], u[k]);
-    }
-    __syncthreads();
-#pragma unroll
-    for (int k = 0; k < kPer; ++k) {
-        if (!own[k]) continue;
-        const int i = ri[k];
-        const uint64_t ci = sc[i], row = ci >> 32;
-        T x = sv[i];
-        if (multi[k]) x = leaf_chain(x, row, row0, bshift, bstart, perm, sc, sv, true, ci);
-        shard[row] = x;
-    }
-    return;
-#elif DML_SP_LEAF_EARLY
 #pragma unroll
     for (int k = 0; k < kPer; ++k) {
         const int i = tid + k * kT;
@@ -515,27 +482,6 @@ __global__ __launch_bounds__(kSpLeafThreads) void k_sp_leaf(T* __restrict__ shar
         T x = x0[k];
         if (!(f & 2)) {
             x = Elem<T>::add(x, u[k]);
-        } else {
-            x = leaf_chain(x, row, row0, bshift, bstart, perm, sc, sv);
-        }
-        shard[row] = x;
-    }
-    return;
-#endif
-    T v[kPer];
-    uint64_t rw[kPer];
-#pragma unroll
-    for (int k = 0; k < kPer; ++k) rw[k] = own[k] ? sc[ri[k]] >> 32 : row0;  // row0: a valid row of this leaf
-#pragma unroll
-    for (int k = 0; k < kPer; ++k) v[k] = shard[rw[k]];  // every shard load in flight together
-#pragma unroll
-    for (int k = 0; k < kPer; ++k) {
-        if (!own[k]) continue;
-        const int i = ri[k];
-        const uint64_t row = rw[k];
-        T x = v[k];
-        if (!multi[k]) {
-            x = Elem<T>::add(x, sv[i]);
         } else {
             x = leaf_chain(x, row, row0, bshift, bstart, perm, sc, sv);
         }
@@ -586,11 +532,6 @@ SpPlan sparse_plan(const Batch& bt, int nb, int64_t rows) {
     const double span = (double)(kSpLeafCap / 2) * (double)rows / (double)std::max<int64_t>(nrec, 1);
     int SL = 0;
     while (SL < 31 && (double)((int64_t)1 << (SL + 1)) <= span) ++SL;
-    static const int sl_bias = [] {  // A/B knob: leaves 2^bias times larger
-        const char* v = getenv("DML_SP_SL_BIAS");
-        return v ? atoi(v) : 0;
-    }();
-    SL = std::max(0, std::min(31, SL + sl_bias));
     while (SL < 31 && ((rows + ((int64_t)1 << SL) - 1) >> SL) > 65536) ++SL;
     pl.SL = SL;
     pl.nleaves = (rows + ((int64_t)1 << SL) - 1) >> SL;

@@ -387,13 +387,7 @@ int launch_apply(dml_store* s, Chunk& c, Workspace& W, const Ctrl* prev) {
 
 // Index on the side stream (overlaps the previous chunk's apply), then apply.
 int launch_chunk(dml_store* s, Chunk& c, Workspace& W, const Ctrl* prev) {
-    // DML_SERIAL_INDEX=1: index on the apply stream (A/B of the overlap; no cross-queue wait)
-    static const bool serial = getenv("DML_SERIAL_INDEX") && atoi(getenv("DML_SERIAL_INDEX"));
-    hipStream_t is = serial ? s->stream : s->istream;
-    if (serial) {  // host pushes are DMA'd on the index stream: the apply stream waits for them
-        HIPCHK(hipEventRecord(W.idx_done, s->istream));
-        HIPCHK(hipStreamWaitEvent(s->stream, W.idx_done, 0));
-    }
+    hipStream_t is = s->istream;
     // A workspace whose last chunk retired normally through a slot-clearing reduce
     // (k_reduce_rows, plain-sum modes) already holds an all -1 slot table and zero
     // rowflags: only its Ctrl is reset (the 4 MiB-class memsets otherwise compete
@@ -408,11 +402,9 @@ int launch_chunk(dml_store* s, Chunk& c, Workspace& W, const Ctrl* prev) {
     } else {
         // float / double arrays: partition the chunk by leaf (row range) for the ordered
         // per-leaf apply (its first pass also finds the cutoff); int32 arrays keep the
-        // validated per-push atomic path (negativity check). DML_SPARSE_ATOMIC=1 forces
-        // the per-push path (A/B).
-        static const bool atomic_only = getenv("DML_SPARSE_ATOMIC") && atoi(getenv("DML_SPARSE_ATOMIC"));
+        // validated per-push atomic path (negativity check).
         const int vt = vtype_of(s->desc);
-        c.sorted = !atomic_only && (vt == kF32 || vt == kF64);
+        c.sorted = vt == kF32 || vt == kF64;
         if (!c.sorted)
             HIPCHK(launch_array_validate(c.bt, c.nb, c.max_nrec, s->stride, s->K, s->first, s->rows, W.ctrl,
                                          c.tail_cut, is));
@@ -431,16 +423,12 @@ int launch_chunk(dml_store* s, Chunk& c, Workspace& W, const Ctrl* prev) {
                                            c.tail_cut, is));
         }
     }
-    if (!serial) {
-        HIPCHK(hipEventRecord(W.idx_done, s->istream));
-        // The index (tens of µs) finishes while the previous chunk's reduce (hundreds
-        // of µs) still runs: wait for it on the host and enqueue this chunk's apply
-        // directly behind that reduce. A cross-queue barrier packet instead costs
-        // ~16 µs of idle GPU between the two reduces (measured).
-        static const bool device_wait = getenv("DML_DEVICE_WAIT") && atoi(getenv("DML_DEVICE_WAIT"));
-        if (device_wait) HIPCHK(hipStreamWaitEvent(s->stream, W.idx_done, 0));
-        else HIPCHK(hipEventSynchronize(W.idx_done));
-    }
+    HIPCHK(hipEventRecord(W.idx_done, s->istream));
+    // The index (tens of µs) finishes while the previous chunk's reduce (hundreds
+    // of µs) still runs: wait for it on the host and enqueue this chunk's apply
+    // directly behind that reduce. A cross-queue barrier packet instead costs
+    // ~16 µs of idle GPU between the two reduces (measured).
+    HIPCHK(hipEventSynchronize(W.idx_done));
     return launch_apply(s, c, W, prev);
 }
 
@@ -791,14 +779,7 @@ int dml_store_create_range(const dml_desc* desc, int64_t first_key, int64_t last
         return set_err(DML_E_HIP, std::string(what) + ": " + hipGetErrorString(e));
     };
     hipError_t e;
-    // DML_STREAM_PRIO=1: apply stream at high priority, index stream at low priority
-    // (the next chunk's index then fills the wave slots the reduce leaves free).
-    static const int prio_mode = getenv("DML_STREAM_PRIO") ? atoi(getenv("DML_STREAM_PRIO")) : 0;
-    int prio_least = 0, prio_greatest = 0;
-    if (prio_mode) (void)hipDeviceGetStreamPriorityRange(&prio_least, &prio_greatest);
-    if ((e = prio_mode ? hipStreamCreateWithPriority(&s->stream, hipStreamNonBlocking, prio_greatest)
-                       : hipStreamCreateWithFlags(&s->stream, hipStreamNonBlocking)) != hipSuccess)
-        return fail(e, "stream");
+    if ((e = hipStreamCreateWithFlags(&s->stream, hipStreamNonBlocking)) != hipSuccess) return fail(e, "stream");
     const size_t nbytes = (size_t)rows * (size_t)s->cols * (size_t)s->V;
     if ((e = hipMalloc(&s->data, nbytes)) != hipSuccess) return fail(e, "shard alloc");
     if ((e = hipMemsetAsync(s->data, 0, nbytes, s->stream)) != hipSuccess) return fail(e, "shard zero");
@@ -821,9 +802,7 @@ int dml_store_create_range(const dml_desc* desc, int64_t first_key, int64_t last
     }
     s->slot_bytes = s->is_matrix ? (size_t)rows * kMaxW * sizeof(int32_t) : 0;
     s->ws_bytes = sizeof(Ctrl) + s->slot_bytes + (s->is_matrix ? (size_t)rows * sizeof(uint32_t) : 0);
-    if ((e = prio_mode ? hipStreamCreateWithPriority(&s->istream, hipStreamNonBlocking, prio_least)
-                       : hipStreamCreateWithFlags(&s->istream, hipStreamNonBlocking)) != hipSuccess)
-        return fail(e, "index stream");
+    if ((e = hipStreamCreateWithFlags(&s->istream, hipStreamNonBlocking)) != hipSuccess) return fail(e, "index stream");
     if ((e = hipStreamCreateWithFlags(&s->cstream, hipStreamNonBlocking)) != hipSuccess) return fail(e, "copy stream");
     for (Workspace& W : s->ws) {
         if ((e = hipMalloc((void**)&W.base, s->ws_bytes)) != hipSuccess) return fail(e, "workspace alloc");
