@@ -32,7 +32,7 @@ Without a launcher (`python bench.py --gpus N`, WORLD_SIZE unset) the script
 starts its N rank processes itself before any GPU call and prints rank 0's
 line; under torchrun it reads RANK / LOCAL_RANK / WORLD_SIZE.
 
-`--config 4|4-32|4-asc|4-256|4-ada|5` measures one GPU's shard of configs 4
+`--config 4|4-perm|4-32|4-256|4-ada|5` measures one GPU's shard of configs 4
 and 5 (the per-shard kernel numbers DESIGN.md §7 quotes), N=1 only.
 """
 from __future__ import annotations
@@ -451,12 +451,13 @@ def leg_config4(ctx: Ctx, L, args) -> dict:
     fmt = DataDesc(DataDesc.DATA_TYPE_MATRIX, DataDesc.KEY_TYPE_INT, DataDesc.ELEMENT_TYPE_FLOAT)
     st = torch.cuda.current_stream().cuda_stream
     bufs = []
+    asc = args.c4_order == "asc"
     for b in range(w):
         t = torch.empty(rows * rec, dtype=torch.uint8, device="cuda")
         seed = 3000 + 64 * rank + b
-        pa = _coprime(seed * 2654435761 % rows | 1, rows)
-        assert L.dml_synth_dense_bucket(t.data_ptr(), C.byref(fmt.to_c()), 0, rows, rows, cols, seed, pa,
-                                        b * 7919 % rows, C.c_void_p(st)) == 0
+        pa, pc = (1, 0) if asc else (_coprime(seed * 2654435761 % rows | 1, rows), b * 7919 % rows)
+        assert L.dml_synth_dense_bucket(t.data_ptr(), C.byref(fmt.to_c()), 0, rows, rows, cols, seed, pa, pc,
+                                        C.c_void_p(st)) == 0
         bufs.append(t)
     torch.cuda.synchronize()
     ptrs, lens = [b.data_ptr() for b in bufs], [b.numel() for b in bufs]
@@ -498,7 +499,7 @@ def leg_config4(ctx: Ctx, L, args) -> dict:
     pre_ms, pre_n = _pre_time(L, every=0, reset=True) if sharded else (0.0, 0)
     algo = w * rows * rec + 2 * shard_rows * cols * 4
     out = {"workload": f"config4: Word2Vec rows {rows}x{cols} fp32 model, {w} full-range pushes per GPU "
-                       f"([int32][{cols} x f32], rows permuted per push)",
+                       f"([int32][{cols} x f32], rows {'ascending (keys implicit = row)' if asc else 'permuted per push'})",
            "value": round(algo * world * args.c4_steps / el / 2**30, 2), "unit": "GiB/s", "n_gpus": world,
            "pushes_per_gpu": w, "steps": args.c4_steps, "ms_per_step": round(el / args.c4_steps * 1e3, 3),
            "scaling": "weak", "dtype": "f32",
@@ -608,18 +609,22 @@ SHARD_CONFIGS = {
     "5": dict(name="config5: LDA IntMatrixStore shard 125000x1000 int32 (negativity check), "
                    "32 pushes x 8192 distinct rows ([int32][1000 x int32])",
               rows=125_000, cols=1000, W=32, nrec=8192, vt=0, ada=None, seed0=4000, mult=331, init=11, steps=20),
-    # config 4's metric is the plain sum (FloatMatrixStore), W = 8 and 32; AdaGrad is its variant
+    # config 4's metric is the plain sum (FloatMatrixStore), W = 8 and 32; AdaGrad is its variant.
+    # full-range gradients, keys implicit = row, i.e. every push lists the
+    # rows in ascending order (also Java HashMap<Integer>'s iteration order of a full key
+    # set); "4-perm" permutes the rows of every push (seeded), the harder layout.
     "4": dict(name="config4: Word2Vec rows, FloatMatrixStore shard 1250000x200 fp32, 8 full-range pushes "
-                   "([int32][200 x f32])",
+                   "([int32][200 x f32], rows ascending)",
               rows=1_250_000, cols=200, W=8, nrec=1_250_000, vt=1, ada=None, seed0=3000, mult=7919, init=13,
-              steps=10),
-    "4-32": dict(name="config4 (W=32): Word2Vec rows, FloatMatrixStore shard 1250000x200 fp32, 32 full-range pushes",
+              steps=10, asc=True),
+    "4-perm": dict(name="config4 with the rows of every push permuted (seeded): FloatMatrixStore shard "
+                        "1250000x200 fp32, 8 full-range pushes",
+                   rows=1_250_000, cols=200, W=8, nrec=1_250_000, vt=1, ada=None, seed0=3000, mult=7919, init=13,
+                   steps=10),
+    "4-32": dict(name="config4 (W=32): Word2Vec rows, FloatMatrixStore shard 1250000x200 fp32, 32 full-range pushes "
+                      "(rows ascending)",
                  rows=1_250_000, cols=200, W=32, nrec=1_250_000, vt=1, ada=None, seed0=3000, mult=7919, init=13,
-                 steps=5),
-    "4-asc": dict(name="config4 with every push in ascending row order (Java HashMap<Integer> iteration): "
-                       "FloatMatrixStore shard 1250000x200 fp32, 8 full-range pushes",
-                  rows=1_250_000, cols=200, W=8, nrec=1_250_000, vt=1, ada=None, seed0=3000, mult=7919, init=13,
-                  steps=10, asc=True),
+                 steps=5, asc=True),
     "4-256": dict(name="config4 shape probe: FloatMatrixStore shard 1250000x256 fp32 (whole 1-KiB rows), 8 full-range "
                        "pushes", rows=1_250_000, cols=256, W=8, nrec=1_250_000, vt=1, ada=None, seed0=3000, mult=7919,
                   init=13, steps=10),
@@ -767,11 +772,13 @@ def main():
                     help="use the sharded pre-reduce/reduce-scatter path even at N=1 (path check)")
     ap.add_argument("--legs", default="4,5", help="model-level config legs in the line ('' = none)")
     ap.add_argument("--c4-pushes", type=int, default=16, help="config-4 full-range pushes per GPU (8.04 GB each)")
+    ap.add_argument("--c4-order", choices=["asc", "perm"], default="asc",
+                    help="config-4 row order per push: ascending (SURVEY §8d, keys implicit = row) or permuted")
     ap.add_argument("--c4-steps", type=int, default=5)
     ap.add_argument("--c4-warmup", type=int, default=2)
     ap.add_argument("--c5-steps", type=int, default=20)
     ap.add_argument("--c5-warmup", type=int, default=4)
-    ap.add_argument("--config", choices=["2", "4", "4-32", "4-asc", "4-256", "4-ada", "5"], default="2",
+    ap.add_argument("--config", choices=["2", "4", "4-perm", "4-32", "4-256", "4-ada", "5"], default="2",
                     help="2 = the headline line (default); 4, 4-32, 4-ada, 5 = one GPU's shard of those configs")
     ap.add_argument("--cpu-seconds", type=float, default=8.0, help="CPU baseline budget for --config 4/5")
     ap.add_argument("--launcher-check", action="store_true", help=argparse.SUPPRESS)

@@ -64,12 +64,21 @@ struct dml_group {
     std::deque<dml_prereduce*> pending;
     int k = 0;
     bool plain = true;  // plain-sum dense matrix: the full-range pre-reduce path applies
-    // exchange path (dml_group_push_exchange): split output, receive buffer, count buffers
-    void* xsend = nullptr;
-    void* xrecv = nullptr;
-    int64_t xsend_cap = 0, xrecv_cap = 0;
+    // exchange path (dml_group_push_exchange), two buffer sets alternating by call:
+    // split output (read by that call's all-to-all), receive buffer (read by the
+    // store when the NEXT call hands it over), count buffers
+    void* xsend[2] = {nullptr, nullptr};
+    void* xrecv[2] = {nullptr, nullptr};
+    int64_t xsend_cap[2] = {0, 0}, xrecv_cap[2] = {0, 0};
+    hipEvent_t xsent[2] = {nullptr, nullptr};      // rstream: the set's all-to-all finished
+    hipEvent_t xconsumed[2] = {nullptr, nullptr};  // store stream: the store read the set's slices
     int64_t* xcnt = nullptr;  // device [2][world * kMaxW]: counts sent / received
-    bool xpending = false;    // the store may still read xrecv (its pushes are asynchronous)
+    int xk = 0;
+    // received slices of the last call, handed to the store by the next call or the flush
+    bool xheld = false;
+    int xheld_set = 0;
+    std::vector<const void*> xptrs;
+    std::vector<int64_t> xlens;
 };
 
 namespace {
@@ -89,10 +98,12 @@ void group_free(dml_group* g) {
     if (!g) return;
     (void)hipSetDevice(g->device);
     (void)end_pending(g, 0);
-    if (g->xsend) (void)hipFree(g->xsend);
-    if (g->xrecv) (void)hipFree(g->xrecv);
     if (g->xcnt) (void)hipFree(g->xcnt);
     for (int i = 0; i < 2; ++i) {
+        if (g->xsend[i]) (void)hipFree(g->xsend[i]);
+        if (g->xrecv[i]) (void)hipFree(g->xrecv[i]);
+        if (g->xsent[i]) (void)hipEventDestroy(g->xsent[i]);
+        if (g->xconsumed[i]) (void)hipEventDestroy(g->xconsumed[i]);
         if (g->partial[i]) (void)hipFree(g->partial[i]);
         if (g->recv[i]) (void)hipFree(g->recv[i]);
         if (g->rs_done[i]) (void)hipEventDestroy(g->rs_done[i]);
@@ -126,8 +137,10 @@ int group_init(dml_group* g, const uint8_t* unique_id) {
     for (int i = 0; i < 2; ++i) {
         GHIP(hipEventCreateWithFlags(&g->rs_done[i], hipEventDisableTiming));
         GHIP(hipEventCreateWithFlags(&g->applied[i], hipEventDisableTiming));
+        GHIP(hipEventCreateWithFlags(&g->xsent[i], hipEventDisableTiming));
+        GHIP(hipEventCreateWithFlags(&g->xconsumed[i], hipEventDisableTiming));
     }
-    GHIP(hipMalloc((void**)&g->xcnt, sizeof(int64_t) * 2 * (size_t)g->world * kMaxW));
+    GHIP(hipMalloc((void**)&g->xcnt, sizeof(int64_t) * 4 * (size_t)g->world * kMaxW));
     ncclUniqueId id;
     memcpy(&id, unique_id, sizeof id);
     GNCCL(ncclCommInitRank(&g->comm, g->world, id, g->rank));
@@ -144,6 +157,18 @@ int ensure_partials(dml_group* g) {
         GHIP(hipMalloc(&g->recv[i], rcv));
     }
     return DML_OK;
+}
+
+// Hand the last exchange call's received slices to the store, in rank-major push
+// order. Its all-to-all must be complete (the caller synchronized rstream).
+int hand_over(dml_group* g) {
+    if (!g->xheld) return DML_OK;
+    g->xheld = false;
+    if (g->xptrs.empty()) return DML_OK;
+    const int rc = dml_store_push_batch_device(g->store, g->xptrs.data(), g->xlens.data(), (int32_t)g->xptrs.size());
+    // the store's reads of the set are queued on its stream by now (index host-waited, reduce enqueued)
+    GHIP(hipEventRecord(g->xconsumed[g->xheld_set], g->sstream));
+    return rc;
 }
 
 int grow(void** p, int64_t* cap, int64_t need) {
@@ -213,6 +238,10 @@ int dml_group_push_full_range(dml_group* g, const void* const* dev_bufs, const i
     if (!g->plain)
         return set_error(DML_E_UNSUPPORTED, "the full-range pre-reduce path needs a plain-sum matrix (use dml_group_push_exchange)");
     GHIP(hipSetDevice(g->device));
+    if (g->xheld) {  // an exchange call's slices come first: the store applies calls in order
+        GHIP(hipStreamSynchronize(g->rstream));
+        GRC(hand_over(g));
+    }
     GRC(ensure_partials(g));
     const int64_t S = g->step_rows, P = g->pieces;
     if (S % P) return set_error(DML_E_INVALID_ARG, "pieces must divide the linearSplit step");
@@ -255,24 +284,26 @@ int dml_group_push_exchange(dml_group* g, const void* const* dev_bufs, const int
     const int64_t K = g->desc.key_type == 0 ? 4 : 8;
     const int64_t stride = g->desc.data_type == DML_DATA_TYPE_MATRIX ? K + (int64_t)g->vbytes * g->cols
                                                                       : K + (int64_t)g->vbytes;
-    // the previous exchange's slices may still be read by the store: finish them
-    // (their deferred errors surface here, like the store's own next call)
-    if (g->xpending) {
-        g->xpending = false;
-        GRC(dml_store_flush(g->store));
-    }
+    // Pipelined over calls (two buffer sets): this call's split runs while the
+    // previous call's all-to-all moves its slices; the previous slices reach the
+    // store once this call's count exchange (queued behind that all-to-all on the
+    // same stream) has completed, and the store applies them while this call's
+    // all-to-all runs. The only host waits: the split's counts and the count exchange.
+    const int i = g->xk;
+    g->xk ^= 1;
     int64_t total = 0;
     for (int b = 0; b < n; ++b) total += lens[b];
-    GRC(grow(&g->xsend, &g->xsend_cap, total));
+    GHIP(hipEventSynchronize(g->xsent[i]));  // the set's last all-to-all (two calls ago) read xsend[i]
+    GRC(grow(&g->xsend[i], &g->xsend_cap[i], total));
     std::vector<int64_t> cnt((size_t)n * W);  // [push][dest]
-    GRC(dml_shard_split(&g->desc, g->cols, g->total_rows, W, dev_bufs, lens, n, g->xsend, g->xsend_cap, cnt.data(),
-                        g->cstream));
+    GRC(dml_shard_split(&g->desc, g->cols, g->total_rows, W, dev_bufs, lens, n, g->xsend[i], g->xsend_cap[i],
+                        cnt.data(), g->cstream));
     // counts per destination, then per source: mine[d][b] out, theirs[q][b] in (n per peer)
     std::vector<int64_t> mine((size_t)W * n), theirs((size_t)W * n);
     for (int d = 0; d < W; ++d)
         for (int b = 0; b < n; ++b) mine[(size_t)d * n + b] = cnt[(size_t)b * W + d];
-    int64_t* dmine = g->xcnt;
-    int64_t* dtheirs = g->xcnt + (size_t)W * kMaxW;
+    int64_t* dmine = g->xcnt + (size_t)i * 2 * W * kMaxW;
+    int64_t* dtheirs = dmine + (size_t)W * kMaxW;
     GHIP(hipMemcpyAsync(dmine, mine.data(), sizeof(int64_t) * mine.size(), hipMemcpyHostToDevice, g->rstream));
     GNCCL(ncclGroupStart());
     for (int q = 0; q < W; ++q) {
@@ -281,7 +312,8 @@ int dml_group_push_exchange(dml_group* g, const void* const* dev_bufs, const int
     }
     GNCCL(ncclGroupEnd());
     GHIP(hipMemcpyAsync(theirs.data(), dtheirs, sizeof(int64_t) * theirs.size(), hipMemcpyDeviceToHost, g->rstream));
-    GHIP(hipStreamSynchronize(g->rstream));
+    GHIP(hipStreamSynchronize(g->rstream));  // also completes the previous call's all-to-all
+    GRC(hand_over(g));
     std::vector<int64_t> soff((size_t)W + 1, 0), roff((size_t)W + 1, 0);
     for (int q = 0; q < W; ++q) {
         int64_t sb = 0, rb = 0;
@@ -292,9 +324,12 @@ int dml_group_push_exchange(dml_group* g, const void* const* dev_bufs, const int
         soff[(size_t)q + 1] = soff[(size_t)q] + sb;
         roff[(size_t)q + 1] = roff[(size_t)q] + rb;
     }
-    GRC(grow(&g->xrecv, &g->xrecv_cap, roff[(size_t)W]));
-    uint8_t* sp = (uint8_t*)g->xsend;
-    uint8_t* rp = (uint8_t*)g->xrecv;
+    // xrecv[i] was last read by the store for the call two back
+    if (g->xrecv_cap[i] < roff[(size_t)W]) GHIP(hipEventSynchronize(g->xconsumed[i]));
+    GRC(grow(&g->xrecv[i], &g->xrecv_cap[i], roff[(size_t)W]));
+    GHIP(hipStreamWaitEvent(g->rstream, g->xconsumed[i], 0));
+    uint8_t* sp = (uint8_t*)g->xsend[i];
+    uint8_t* rp = (uint8_t*)g->xrecv[i];
     GNCCL(ncclGroupStart());
     for (int q = 0; q < W; ++q) {
         GNCCL(ncclSend(sp + soff[(size_t)q], (size_t)(soff[(size_t)q + 1] - soff[(size_t)q]), ncclUint8, q, g->comm,
@@ -303,30 +338,35 @@ int dml_group_push_exchange(dml_group* g, const void* const* dev_bufs, const int
                        g->rstream));
     }
     GNCCL(ncclGroupEnd());
-    GHIP(hipStreamSynchronize(g->rstream));
+    GHIP(hipEventRecord(g->xsent[i], g->rstream));
     // the owner's pushes, rank-major: rank 0's pushes in order, then rank 1's, ...
-    std::vector<const void*> ptrs;
-    std::vector<int64_t> ls;
+    g->xptrs.clear();
+    g->xlens.clear();
     int64_t off = 0;
     for (int q = 0; q < W; ++q)
         for (int b = 0; b < n; ++b) {
             const int64_t ln = theirs[(size_t)q * n + b] * stride;
             if (ln > 0) {
-                ptrs.push_back(rp + off);
-                ls.push_back(ln);
+                g->xptrs.push_back(rp + off);
+                g->xlens.push_back(ln);
             }
             off += ln;
         }
-    if (ptrs.empty()) return DML_OK;
-    g->xpending = true;
-    return dml_store_push_batch_device(g->store, ptrs.data(), ls.data(), (int32_t)ptrs.size());
+    g->xheld = true;
+    g->xheld_set = i;
+    return DML_OK;
 }
 
 int dml_group_flush(dml_group* g) {
     if (!g) return set_error(DML_E_INVALID_ARG, "null group");
     GHIP(hipSetDevice(g->device));
-    g->xpending = false;  // dml_store_flush below finishes the exchange's pushes too
-    int rc = end_pending(g, 0);
+    int rc = DML_OK;
+    if (g->xheld) {  // the last exchange call's slices
+        rc = hipStreamSynchronize(g->rstream) == hipSuccess ? DML_OK : set_error(DML_E_HIP, "exchange sync");
+        if (rc == DML_OK) rc = hand_over(g);
+    }
+    const int r1 = end_pending(g, 0);
+    if (rc == DML_OK) rc = r1;
     for (hipStream_t s : {g->cstream, g->rstream})
         if (hipStreamSynchronize(s) != hipSuccess && rc == DML_OK) rc = set_error(DML_E_HIP, "group stream sync");
     for (hipEvent_t e : g->applied)

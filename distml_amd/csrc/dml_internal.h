@@ -30,8 +30,9 @@ constexpr uint64_t kOffMask = (1ull << 40) - 1;
 struct Ctrl {
     unsigned long long cutoff;   // first key-out-of-shard position (exclusive apply limit)
     unsigned long long neg_pos;  // first add that left an int32 counter negative
+    unsigned long long ident;    // speculative chunk: bit b = push b taken as identity (record r is row r)
     unsigned int no_dup;         // 0xFFFFFFFF = no row repeated inside one push; 0 = repeat seen
-    unsigned int pad[3];
+    unsigned int spec_ok;        // speculative chunk: 0xFFFFFFFF = every identity record verified; 0 = not
 };
 static_assert(sizeof(Ctrl) == 32, "Ctrl layout");
 
@@ -42,13 +43,21 @@ struct Batch {
     int64_t nrec[kMaxW];  // records whose key is complete (a truncated tail record included)
     int32_t bidx[kMaxW];  // global push index of each column (positions use it; columns ascend)
     const Ctrl* prev;     // control block of the chunk enqueued just before (pipelining), or null
+    // Identity speculation (full-range chunks of plain sums): pushes
+    // whose sampled keys say "record r holds row r" skip the key index; the reduce
+    // takes slot = row for them and verifies every such record's key, reading the
+    // input shard at `src` and writing the output buffer (the host keeps the input
+    // until the chunk retires, so a failed verification re-runs it exactly).
+    const void* src;      // input shard (null: in place)
+    int64_t first;        // key of row 0 (KeyRange first), for the verification
+    int32_t spec;         // 1: speculative chunk
 };
 
-// A chunk whose predecessor ended abnormally (error, or rows to replay) must
-// not run ahead of the host's fix-up: its kernels turn into no-ops and the
-// host relaunches (replay) or drops (error) it.
+// A chunk whose predecessor ended abnormally (error, rows to replay, or a failed
+// identity speculation) must not run ahead of the host's fix-up: its kernels
+// turn into no-ops and the host relaunches (replay) or drops (error) it.
 __host__ __device__ inline bool ctrl_abnormal(const Ctrl* c) {
-    return c->cutoff != kNoPos || c->neg_pos != kNoPos || c->no_dup == 0u;
+    return c->cutoff != kNoPos || c->neg_pos != kNoPos || c->no_dup == 0u || c->spec_ok == 0u;
 }
 
 // Running AdaGrad maxDelta state (FloatMatrixStoreAdaGrad.java:27-29), device resident.
@@ -104,6 +113,10 @@ struct LaunchEv {
 hipError_t launch_index(const Batch& bt, int nb, int64_t max_nrec, int64_t stride, int K,
                         int64_t first, int64_t rows, int32_t* slot, uint32_t* rowflag, Ctrl* ctrl,
                         uint64_t tail_cut, hipStream_t st);
+// Identity speculation: clears ctrl->ident bit b unless push b is full-range and
+// every sampled record r of it has row_index(key) == r (Ctrl reset to all ones).
+hipError_t launch_ident_check(const Batch& bt, int nb, int64_t stride, int K, int64_t first, int64_t rows, Ctrl* ctrl,
+                              hipStream_t st);
 hipError_t launch_reduce(int vtype, int mode, void* shard, int64_t rows, int32_t cols, const Batch& bt,
                          int nb, int64_t stride, int K, const int32_t* slot, const uint32_t* rowflag, Ctrl* ctrl,
                          uint64_t tail_cut, const AdaArgs& ada, hipStream_t st, int64_t* nblocks_out,

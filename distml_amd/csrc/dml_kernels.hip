@@ -68,6 +68,7 @@ __global__ __launch_bounds__(256) void k_index(const Batch bt, int64_t stride, i
     const int64_t r = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (r == 0 && b == 0 && tail_cut != kNoPos) atomicMin(&ctrl->cutoff, (unsigned long long)tail_cut);
     if (r >= bt.nrec[b]) return;
+    if (bt.spec && ((ctrl->ident >> b) & 1ull)) return;  // identity push: the reduce verifies its keys
     const int64_t off = r * stride;
     const int64_t key = ld_key(bt.base[b] + off, K);
     const int64_t idx = row_index(key, first, rows);
@@ -80,6 +81,33 @@ __global__ __launch_bounds__(256) void k_index(const Batch bt, int64_t stride, i
         rowflag[idx] = 1u;
         ctrl->no_dup = 0u;  // benign race: every writer stores the same value
     }
+}
+
+// k_ident_check: one 64-lane block per push of a speculative chunk. Push b stays
+// an identity candidate if it is full-range (nrec == rows) and the records at 32
+// evenly spaced positions (first and last included) plus 32 hashed ones hold row
+// r at record r. Cheap (64 key lines per push); the reduce verifies every record.
+__global__ __launch_bounds__(64) void k_ident_check(const Batch bt, int64_t stride, int K, int64_t first, int64_t rows,
+                                                    Ctrl* __restrict__ ctrl) {
+    const int b = blockIdx.x, t = threadIdx.x;
+    bool ok = bt.nrec[b] == rows && rows > 0;
+    if (ok) {
+        const int64_t r = t < 32 ? (rows > 1 ? (int64_t)t * (rows - 1) / 31 : 0)
+                                 : (int64_t)(splitmix64_dev(((uint64_t)b << 32) + (uint64_t)t) % (uint64_t)rows);
+        ok = row_index(ld_key(bt.base[b] + r * stride, K), first, rows) == r;
+    }
+    const bool all = __ballot(!ok) == 0ull;
+    if (t == 0) {
+        unsigned long long clear = all ? 0ull : (1ull << b);
+        if (b == 0 && gridDim.x < 64) clear |= ~((1ull << gridDim.x) - 1ull);  // no such push
+        if (clear) atomicAnd(&ctrl->ident, ~clear);
+    }
+}
+hipError_t launch_ident_check(const Batch& bt, int nb, int64_t stride, int K, int64_t first, int64_t rows, Ctrl* ctrl,
+                              hipStream_t st) {
+    if (nb <= 0) return hipSuccess;
+    hipLaunchKernelGGL(k_ident_check, dim3((unsigned)nb), dim3(64), 0, st, bt, stride, K, first, rows, ctrl);
+    return hipGetLastError();
 }
 
 hipError_t launch_index(const Batch& bt, int nb, int64_t max_nrec, int64_t stride, int K, int64_t first,
@@ -494,6 +522,20 @@ __global__ __launch_bounds__(64 * WPB) void k_reduce_rows(T* __restrict__ shard,
     uint64_t cut = ctrl->cutoff;
     if (tail_cut < cut) cut = tail_cut;
     uint64_t negpos = kNoPos;  // kAddCheckI32: earliest add that left a counter negative
+    // Identity speculation (Batch::spec): pushes in ctrl->ident take slot = row and
+    // every such record's key is verified below; a chunk that met a cutoff or a
+    // repeated row turns into a no-op the host re-runs without speculation.
+    uint64_t ident = 0;
+    bool bad = false;
+    if constexpr (MODE == kAdd) {
+        if (bt.spec) {
+            if (cut != kNoPos || ctrl->no_dup == 0u) {
+                if (lane == 0) ctrl->spec_ok = 0u;
+                return;
+            }
+            ident = ctrl->ident;
+        }
+    }
 
     if (cut != kNoPos) {
         // Error batch: element-wise RMW of the wave's rows in place, pushes in order,
@@ -536,11 +578,13 @@ __global__ __launch_bounds__(64 * WPB) void k_reduce_rows(T* __restrict__ shard,
 #pragma unroll
         for (int c = 0; c < CPW; ++c) {
             const bool ld = MODE != kPreReduce && (live >> r & 1u);
+            // the input row: in place, or the speculative chunk's input buffer
+            const T* const lrow = (MODE == kAdd && bt.src) ? (const T*)bt.src + row[r] * (int64_t)cols : rowp[r];
             if (ld && nv[c] == VEC) {
-                unpack<T>(ldg16((const uint8_t*)(rowp[r] + c0[c])), acc[r][c]);
+                unpack<T>(ldg16((const uint8_t*)(lrow + c0[c])), acc[r][c]);
             } else {
 #pragma unroll
-                for (int e = 0; e < VEC; ++e) acc[r][c][e] = ld && e < nv[c] ? rowp[r][c0[c] + e] : T(0);
+                for (int e = 0; e < VEC; ++e) acc[r][c][e] = ld && e < nv[c] ? lrow[c0[c] + e] : T(0);
             }
         }
     unsigned touched = 0;
@@ -551,16 +595,22 @@ __global__ __launch_bounds__(64 * WPB) void k_reduce_rows(T* __restrict__ shard,
     // has returned), so every lane v_readlane reads holds its value.
     static_assert(kMaxW == 64, "one push per lane");
     int32_t vslot[RPW];
+    // lanes >= nb read past the row's entries (another row's): masked to -1;
+    // an identity push (speculation) holds row r at record r when r < nrec
+    const bool lane_ident = lane < nb && ((ident >> lane) & 1ull);
 #pragma unroll
-    // lanes >= nb read past the row's entries (another row's): masked to -1
-    for (int r = 0; r < RPW; ++r) vslot[r] = ((live >> r & 1u) && lane < nb) ? slot[row[r] * slot_stride(nb) + lane] : -1;
+    for (int r = 0; r < RPW; ++r)
+        vslot[r] = ((live >> r & 1u) && lane < nb)
+                       ? (lane_ident ? (row[r] < bt.nrec[lane] ? (int32_t)row[r] : -1) : slot[row[r] * slot_stride(nb) + lane])
+                       : -1;
     if constexpr (MODE != kAddCheckI32) {
         // Hand the slot rows back as the next batch's index expects them (-1 = no
         // record), so the host skips the slot-table memset (reduce_clears_slots). The
-        // int32-check mode keeps them: its rollback re-reads the table.
+        // int32-check mode keeps them: its rollback re-reads the table. Identity
+        // pushes never wrote theirs.
 #pragma unroll
         for (int r = 0; r < RPW; ++r)
-            if ((live >> r & 1u) && lane < nb) slot[row[r] * slot_stride(nb) + lane] = -1;
+            if ((live >> r & 1u) && lane < nb && !lane_ident) slot[row[r] * slot_stride(nb) + lane] = -1;
     }
     const uint64_t vbase = lane < nb ? (uint64_t)bt.base[lane] : 0ull;
     if constexpr (DEPTH == 3) {
@@ -621,6 +671,14 @@ __global__ __launch_bounds__(64 * WPB) void k_reduce_rows(T* __restrict__ shard,
                         raw[g][c] = NT ? ldg16_nt(src) : ldg16(src);
                     }
                 }
+                if constexpr (MODE == kAdd) {
+                    if (rr >= 0 && ((ident >> b) & 1ull)) {  // wave-uniform: verify the identity record's key
+                        int64_t rw = row[0];
+#pragma unroll
+                        for (int r = 1; r < RPW; ++r) rw = pr[g] == r ? row[r] : rw;
+                        bad |= row_index(ld_key(bp + (int64_t)rr * stride, K), bt.first, rows) != rw;
+                    }
+                }
             }
 #pragma unroll
             for (int g = 0; g < RPW; ++g) {
@@ -670,8 +728,13 @@ __global__ __launch_bounds__(64 * WPB) void k_reduce_rows(T* __restrict__ shard,
         const uint8_t* bp = (const uint8_t*)(((uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)vbase, b)) |
                                              ((uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)(vbase >> 32), b) << 32));
         u32x4 raw[RPW][CPW];
+        int64_t kv[RPW];
 #pragma unroll
         for (int r = 0; r < RPW; ++r) {
+            if constexpr (MODE == kAdd) {
+                // identity push: verify the key of every record taken as row r
+                kv[r] = ((ident >> b) & 1ull) && rr[r] >= 0 ? ld_key(bp + (int64_t)rr[r] * stride, K) : bt.first + row[r];
+            }
             if constexpr (FULL) {
                 // one address per row; the chunks are immediate offsets of the loads
                 const uint8_t* rb = rr[r] >= 0 ? bp + (int64_t)rr[r] * stride + voff[0] : fbv;
@@ -688,6 +751,10 @@ __global__ __launch_bounds__(64 * WPB) void k_reduce_rows(T* __restrict__ shard,
                     raw[r][c] = NT ? ldg16_nt(src) : ldg16(src);
                 }
             }
+        }
+        if constexpr (MODE == kAdd) {
+#pragma unroll
+            for (int r = 0; r < RPW; ++r) bad |= row_index(kv[r], bt.first, rows) != row[r];
         }
 #pragma unroll
         for (int r = 0; r < RPW; ++r) {
@@ -738,6 +805,7 @@ __global__ __launch_bounds__(64 * WPB) void k_reduce_rows(T* __restrict__ shard,
         }
     }
     if (MODE == kAddCheckI32 && negpos != kNoPos) atomicMin(&ctrl->neg_pos, (unsigned long long)negpos);
+    if (MODE == kAdd && bad) ctrl->spec_ok = 0u;  // an identity push is not: the host re-runs the chunk
 }
 
 // Occupancy cap: dynamic LDS (unused by the kernels) so that at most `bpc`

@@ -66,6 +66,9 @@ struct Chunk {
     bool sorted = false;  // array store: partitioned + per-leaf ordered apply (dml_sparse.hip)
     SpPlan sp{};
     SpLayout spl{};
+    bool spec = false;     // identity speculation (full-range plain-sum chunk, Batch::spec)
+    void* in = nullptr;    // matrix shard the chunk reads (the previous chunk's output)
+    void* out = nullptr;   // and writes: == in, or the other buffer of a speculative chunk
 };
 
 int vtype_of(const dml_desc& d) { return d.value_type; }
@@ -112,7 +115,8 @@ struct dml_store {
     int64_t first = 0, last = 0, rows = 0;
     int32_t cols = 1;
     int64_t stride = 0;         // record stride
-    void* data = nullptr;       // rows*cols values
+    void* data = nullptr;       // rows*cols values, as of the last retired chunk
+    void* data_alt = nullptr;   // second buffer of speculative chunks (allocated on first use)
     float* alpha = nullptr;     // AdaGrad (FloatMatrixStoreAdaGrad.java:23-24)
     float* delta = nullptr;
     DeltaCand* cand = nullptr;
@@ -341,7 +345,8 @@ int launch_apply(dml_store* s, Chunk& c, Workspace& W, const Ctrl* prev) {
         if (s->timing && !inpacket) HIPCHK(hipEventRecord(W.kstart, s->stream));
         int64_t nblk = 0;
         W.clears = reduce_clears_slots(vtype_of(s->desc), reduce_mode(s), s->cols);
-        HIPCHK(launch_reduce(vtype_of(s->desc), reduce_mode(s), s->data, s->rows, s->cols, c.bt, c.nb, s->stride,
+        c.bt.src = c.in != c.out ? c.in : nullptr;
+        HIPCHK(launch_reduce(vtype_of(s->desc), reduce_mode(s), c.out, s->rows, s->cols, c.bt, c.nb, s->stride,
                              s->K, W.slot, W.rowflag, W.ctrl, c.tail_cut, ada_args(s), s->stream, &nblk, ev));
         if (s->adagrad)
             HIPCHK(launch_maxdelta_finalize(s->cand, nblk, s->md, c.bt, c.nb, s->stride, s->K, s->V, s->stream));
@@ -397,6 +402,7 @@ int launch_chunk(dml_store* s, Chunk& c, Workspace& W, const Ctrl* prev) {
     HIPCHK(hipMemsetAsync(W.base, 0xFF, sizeof(Ctrl) + (clean ? 0 : s->slot_bytes), is));
     if (s->is_matrix) {
         if (!clean) HIPCHK(hipMemsetAsync(W.rowflag, 0, (size_t)s->rows * sizeof(uint32_t), is));
+        if (c.spec) HIPCHK(launch_ident_check(c.bt, c.nb, s->stride, s->K, s->first, s->rows, W.ctrl, is));
         HIPCHK(launch_index(c.bt, c.nb, c.max_nrec, s->stride, s->K, s->first, s->rows, W.slot, W.rowflag, W.ctrl,
                             c.tail_cut, is));
     } else {
@@ -555,6 +561,34 @@ int record_error(dml_store* s, int code, int64_t key, int32_t col) {
     return set_err(code, buf);
 }
 
+// A chunk's input and output shard buffers: it reads `in` (the output of the
+// chunk before it); a speculative chunk writes the other buffer, so the input
+// survives until its identity records are verified.
+void set_buffers(dml_store* s, Chunk& c, void* in) {
+    c.in = in;
+    c.out = c.spec ? (in == s->data ? s->data_alt : s->data) : in;
+}
+
+// Failed identity speculation: redo the chunk without it, in place on its input
+// (== s->data: every chunk before it has retired), on the apply stream, and
+// return the new Ctrl. The workspace's slot table / rowflags are rebuilt.
+int rerun_unspeculated(dml_store* s, Chunk& c, Workspace& W, Ctrl* ctl) {
+    c.spec = false;
+    c.bt.spec = 0;
+    c.bt.prev = nullptr;
+    set_buffers(s, c, s->data);
+    HIPCHK(hipMemsetAsync(W.base, 0xFF, sizeof(Ctrl) + s->slot_bytes, s->stream));
+    HIPCHK(hipMemsetAsync(W.rowflag, 0, (size_t)s->rows * sizeof(uint32_t), s->stream));
+    HIPCHK(launch_index(c.bt, c.nb, c.max_nrec, s->stride, s->K, s->first, s->rows, W.slot, W.rowflag, W.ctrl,
+                        c.tail_cut, s->stream));
+    c.bt.src = nullptr;
+    int64_t nblk = 0;
+    HIPCHK(launch_reduce(vtype_of(s->desc), reduce_mode(s), c.out, s->rows, s->cols, c.bt, c.nb, s->stride, s->K,
+                         W.slot, W.rowflag, W.ctrl, c.tail_cut, ada_args(s), s->stream, &nblk));
+    W.clears = reduce_clears_slots(vtype_of(s->desc), reduce_mode(s), s->cols);
+    return read_ctrl(s, W, ctl);
+}
+
 // Turn the oldest pending chunk's Ctrl into final state + status: replay rows a
 // push repeats, undo int32 adds past the first negative counter, map the first
 // failing position to (code, key, col). If it ended abnormally, the chunk queued
@@ -565,12 +599,21 @@ int retire_front(dml_store* s) {
     Pending p = s->pend.front();
     s->pend.pop_front();
     Workspace& W = s->ws[p.w];
-    const Chunk& c = p.c;
+    Chunk& c = p.c;
     HIPCHK(hipEventSynchronize(W.done));
     Ctrl ctl = *W.hctrl;
     if (s->timing) ev_collect(s);
-    const bool abnormal = ctrl_abnormal(&ctl);
+    const bool abnormal = ctrl_abnormal(&ctl);  // the chunk queued behind it ran as a no-op
     W.clean = s->is_matrix && !abnormal && W.clears;
+    if (c.spec && ctl.spec_ok != 0u) {
+        std::swap(s->data, s->data_alt);  // every identity record verified: the output is the shard
+    } else if (c.spec) {
+        // An identity push was not (or the chunk met a cutoff / repeated row): the
+        // output is discarded and the chunk re-runs exactly, in place on its input
+        // (the shard as of the chunks before it), with the full key index.
+        if (int r2 = rerun_unspeculated(s, c, W, &ctl)) return r2;
+        W.clean = !ctrl_abnormal(&ctl) && W.clears;
+    }
     int rc = DML_OK;
     if (s->is_matrix && ctl.no_dup == 0u) {
         rc = replay_rows(s, c, W, &ctl);
@@ -630,6 +673,7 @@ int retire_front(dml_store* s) {
         } else {
             Pending& q = s->pend.front();  // relaunch its apply; its index is still valid
             HIPCHK(hipEventSynchronize(s->ws[q.w].done));
+            set_buffers(s, q.c, s->data);
             if (int r2 = launch_apply(s, q.c, s->ws[q.w], nullptr)) return r2;
         }
     }
@@ -674,7 +718,23 @@ int run_batch(dml_store* s, const uint8_t* const* dptr, const int64_t* lens, int
             if (rc) { s->pend.clear(); return rc; }
         }
         if (s->err) return set_err(s->err, "store is in a failed state (see dml_store_error_state)");
+        // Identity speculation: plain-sum matrices whose every push of
+        // the chunk is full-range (one record per row, no ragged tail).
+        if (s->is_matrix && reduce_mode(s) == kAdd && s->cols >= (vtype_of(s->desc) == kF64 ? 2 : 4) &&
+            c.tail_cut == kNoPos) {
+            bool full = true;
+            for (int j = 0; j < c.nb && full; ++j) full = c.bt.nrec[j] == s->rows && c.bt.len[j] == s->rows * s->stride;
+            if (full && !s->data_alt &&
+                hipMalloc(&s->data_alt, (size_t)s->rows * (size_t)s->cols * (size_t)s->V) != hipSuccess) {
+                (void)hipGetLastError();
+                s->data_alt = nullptr;  // no room for a second buffer: no speculation
+            }
+            c.spec = full && s->data_alt;
+        }
+        c.bt.spec = c.spec ? 1 : 0;
+        c.bt.first = s->first;
         const Ctrl* prev = s->pend.empty() ? nullptr : s->ws[s->pend.back().w].ctrl;
+        set_buffers(s, c, s->pend.empty() ? s->data : s->pend.back().c.out);
         Pending p;
         p.c = c;
         p.w = s->next_ws;
@@ -844,6 +904,7 @@ void dml_store_destroy(dml_store* s) {
             if (W.kstart) (void)hipEventDestroy(W.kstart);
         }
         (void)hipFree(s->data);
+        (void)hipFree(s->data_alt);
         (void)hipFree(s->alpha);
         (void)hipFree(s->delta);
         (void)hipFree(s->cand);

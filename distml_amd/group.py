@@ -115,7 +115,8 @@ class ShardGroup:
         # (side stream) and pre-reduce overlap call k's reduce-scatter and apply
         self.pieces = pieces
         self._pending: list = []  # pre-reduce handles whose errors are not yet collected
-        self._xbufs: list = []    # exchange receive buffers the store may still read
+        self._xbufs: list = []    # exchange receive buffers the store may still read: (event, recv, send)
+        self._held = None         # the last exchange call's slices, handed to the store next call / flush
         self._k = 0
         if self.partial.is_cuda:
             self.comm = torch.cuda.Stream(device=dev)
@@ -146,6 +147,10 @@ class ShardGroup:
     def push_full_range(self, dev_ptrs: Sequence[int], lens: Sequence[int], stream: int = 0) -> None:
         """Ordered local pre-reduce -> reduce-scatter -> owner apply (see module doc)."""
         torch = self.torch
+        if getattr(self, "_held", None) is not None:  # an exchange call's slices come first (call order)
+            if self.partial.is_cuda:
+                torch.cuda.current_stream(self.partial.device).synchronize()
+            self._hand_over()
         if (self.partial.is_cuda and hasattr(self.ops, "begin") and len(dev_ptrs) <= 64
                 and self.step_rows % self.pieces == 0):
             return self._push_pipelined(dev_ptrs, lens)
@@ -225,7 +230,13 @@ class ShardGroup:
         send/recv over xGMI), and every owner applies its W slices in global push
         order — rank-major: rank 0's pushes, then rank 1's — through the store's
         ordered reduce (exact, errors included). Every rank passes the same number
-        of pushes per call; keys outside the matrix are dropped like the client does."""
+        of pushes per call; keys outside the matrix are dropped like the client does.
+
+        Pipelined over calls: a call's received slices reach the store at the next
+        exchange call (once its count exchange, queued behind the previous data
+        exchange, has completed) or at flush(), so this call's split overlaps the
+        previous all-to-all and the store's apply overlaps this call's all-to-all.
+        The caller's push buffers are free when the call returns (the split copied them)."""
         torch, dist = self.torch, self.dist
         n, world = len(dev_ptrs), self.world
         stride = self.record_stride()
@@ -246,7 +257,10 @@ class ShardGroup:
         else:
             t = theirs.to(dev)
             dist.all_to_all_single(t.view(-1), mine.to(dev).view(-1))
-            theirs = t.cpu()
+            theirs = t.cpu()  # waits for the previous call's data exchange too (same stream)
+        if send.is_cuda:
+            torch.cuda.current_stream(dev).synchronize()
+        self._hand_over()  # the previous call's slices have arrived
         send_sizes = [int(mine[d].sum()) * stride for d in range(world)]
         recv_sizes = [int(theirs[q].sum()) * stride for q in range(world)]
         nsend, nrecv = sum(send_sizes), sum(recv_sizes)
@@ -259,8 +273,6 @@ class ShardGroup:
             recv[:nrecv].copy_(hr)
         else:
             dist.all_to_all_single(recv[:nrecv], send[:nsend], recv_sizes, send_sizes)
-        if recv.is_cuda:
-            torch.cuda.current_stream(dev).synchronize()  # the store's streams read recv next
         ptrs, ls, off = [], [], 0
         for q in range(world):
             for b in range(n):
@@ -269,12 +281,30 @@ class ShardGroup:
                     ptrs.append(recv.data_ptr() + off)
                     ls.append(ln)
                 off += ln
+        # held until the next call / flush; `send` stays alive until the exchange ran
+        self._held = (ptrs, ls, recv, send)
+
+    def _hand_over(self) -> None:
+        """Push the last exchange call's received slices into the store (asynchronous
+        apply); their buffers stay alive until the store has read them."""
+        held, self._held = getattr(self, "_held", None), None
+        if held is None:
+            return
+        ptrs, ls, recv, send = held
         if ptrs:
-            if len(self._xbufs) >= 2:  # bound the receive buffers held for the asynchronous store
-                self.store.flush()     # (a deferred error of an earlier call surfaces here)
-                self._xbufs.clear()
             self.store.pushDevice(ptrs, ls)
-            self._xbufs.append(recv)  # alive until the store has consumed it (flush)
+        if not recv.is_cuda:
+            return  # host stand-in stores apply synchronously
+        if getattr(self, "_store_stream", None) is None:
+            self.torch.cuda.synchronize(recv.device)
+            return
+        ev = self.torch.cuda.Event()
+        ev.record(self._store_stream)
+        # keep the buffers until the store's stream has passed them
+        keep = [x for x in self._xbufs if not x[0].query()] + [(ev, recv, send)]
+        while len(keep) > 3:  # bound the memory held for the asynchronous store
+            keep.pop(0)[0].synchronize()
+        self._xbufs = keep
 
     def push_local(self, dev_ptrs: Sequence[int], lens: Sequence[int]) -> None:
         """Pushes already split to this shard: exact ordered apply, no exchange."""
@@ -283,6 +313,10 @@ class ShardGroup:
     def _drain(self) -> None:
         """Every pipelined call's pieces, reduce-scatters and applies have finished."""
         try:
+            if getattr(self, "_held", None) is not None:
+                if self.partial.is_cuda:
+                    self.torch.cuda.current_stream(self.partial.device).synchronize()
+                self._hand_over()
             self._end_pending(0)
         finally:
             if self.partial.is_cuda:

@@ -121,11 +121,14 @@ XR, XC, XW = 2000, 200, 4
 XADA = (0.025, 0.0001, 1.5)
 
 
-def _xbuckets(vt, rank):
+XCALLS = 2  # back-to-back exchange calls, no flush between them (the pipelined path)
+
+
+def _xbuckets(vt, rank, call=0):
     from distml_amd import encode_matrix_push
     out = []
     for b in range(XW):
-        rng = np.random.default_rng(500 * rank + b)
+        rng = np.random.default_rng(500 * rank + 50 * call + b)
         keys = rng.permutation(XR)[: rng.integers(XR // 4, XR)]
         vals = ((rng.standard_normal((len(keys), XC)) * 0.6).astype(np.float32) if vt == 1
                 else rng.integers(-2, 3, size=(len(keys), XC)).astype(np.int32))
@@ -150,9 +153,11 @@ def _xworker(rank, world, port, vt, out_dir):
     g.store.load_values(_init(vt, XR, XC)[sh.firstKey:sh.lastKey + 1])
     if vt == 1:
         g.store.setAlpha(*XADA)
-    bufs = [torch.from_numpy(b).cuda() for b in _xbuckets(vt, rank)]
-    torch.cuda.synchronize()
-    g.push_exchange([b.data_ptr() for b in bufs], [b.numel() for b in bufs])
+    for call in range(XCALLS):
+        bufs = [torch.from_numpy(b).cuda() for b in _xbuckets(vt, rank, call)]
+        torch.cuda.synchronize()
+        g.push_exchange([b.data_ptr() for b in bufs], [b.numel() for b in bufs])
+        del bufs  # the split copied them
     g.flush()
     np.save(os.path.join(out_dir, f"data{rank}.npy"), g.store.values())
     if vt == 1:
@@ -167,14 +172,14 @@ def _xworker(rank, world, port, vt, out_dir):
 @pytest.mark.parametrize("world,vt", [(2, 1), (3, 1), (2, 0)])
 def test_exchange_hip_multiprocess(tmp_path, oracle, world, vt):
     """push_exchange with the real dml_shard_split and HIP stores (ranks share cuda:0,
-    all-to-all over gloo through the host): bit-exact against one oracle store fed
-    every rank's pushes in rank-major order; each shard's maxDelta against an oracle
+    all-to-all over gloo through the host), two calls back to back without a flush:
+    bit-exact against one oracle store fed every call's pushes, rank-major per call; each shard's maxDelta against an oracle
     shard fed the same pushes restricted to its keys."""
     import torch.multiprocessing as mp
     from distml_amd.datadesc import KeyRange
     mp.spawn(_xworker, args=(world, _free_port(), vt, str(tmp_path)), nprocs=world, join=True)
     init = _init(vt, XR, XC)
-    allb = [b for r in range(world) for b in _xbuckets(vt, r)]
+    allb = [b for call in range(XCALLS) for r in range(world) for b in _xbuckets(vt, r, call)]
     o = oracle.OracleStore(1, 0, vt, 0, XR - 1, XC, 1, int(vt == 1))
     if vt == 1:
         o.set_alpha(*XADA)

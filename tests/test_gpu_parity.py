@@ -1135,14 +1135,15 @@ def test_rand_reference_distributions():
         st.close()
 
 
-@pytest.mark.parametrize("ada", [False, True])
-def test_config4_full_shard_bit_exact(oracle, ada):
+@pytest.mark.parametrize("ada,asc", [(False, False), (False, True), (True, False)])
+def test_config4_full_shard_bit_exact(oracle, ada, asc):
     """BASELINE config 4 at the full per-GPU shard bench.py --config 4 times:
     1 250 000 x 200 fp32 (linearSplit(8) of 10M rows), full-range pushes with every
     row permuted per push, device-resident, one batch — bit-exact against the oracle
     (VERDICT r1 #10). Plain sum: W = 8, oracle row-partitioned over 16 threads (each
     thread still applies its rows' adds in push order). AdaGrad (data, alpha, delta,
-    maxDelta): W = 4, oracle single thread."""
+    maxDelta): W = 4, oracle single thread. Ascending rows take the identity-speculation
+    path (no key index, every key verified by the reduce)."""
     import ctypes as C
     import math
     from distml_amd import DataDesc, DataStore, KeyRange, _lib
@@ -1159,6 +1160,8 @@ def test_config4_full_shard_bit_exact(oracle, ada):
     o.synth_fill(13)
 
     def perm(b):
+        if asc:  # keys implicit = row: the identity-speculation path
+            return 1, 0
         a = (3000 + b) * 2654435761 % rows | 1
         while math.gcd(a, rows) != 1:
             a += 1
@@ -1182,4 +1185,79 @@ def test_config4_full_shard_bit_exact(oracle, ada):
         a, d = st.adagrad_state()
         assert a.tobytes() == o.alpha.tobytes() and d.tobytes() == o.delta.tobytes()
         assert st.maxDelta() == o.max_delta()
+    st.close()
+
+
+def _sampled_rows(oracle, b, rows):
+    """The record positions k_ident_check samples in push b of a chunk (32 evenly
+    spaced + 32 hashed), so a test can corrupt records the sample does not see."""
+    ev = {t * (rows - 1) // 31 for t in range(32)}
+    hs = {oracle.splitmix64((b << 32) + t) % rows for t in range(32, 64)}
+    return ev | hs
+
+
+@pytest.mark.parametrize("case", ["ascending", "swapped", "duplicate", "out_of_shard", "mixed_pipelined"])
+def test_identity_speculation_exact(oracle, case):
+    """Identity speculation: full-range pushes whose sampled keys are
+    ascending skip the key index; the reduce verifies every record's key and a
+    chunk with a non-identity push re-runs exactly from its input buffer. Each case
+    is bit-exact against the oracle, error state included: ascending pushes; an
+    ascending push with two records swapped where the sample cannot see them; one
+    with a row listed twice (and one missing: the repeated-row replay); one with an
+    out-of-shard key (the cutoff: ArrayIndexOutOfBoundsException state); and
+    several pipelined batches mixing all of them with permuted pushes."""
+    from distml_amd import DataDesc, DataStore, KeyRange, encode_matrix_push, ArrayIndexOutOfBoundsException
+    rows, cols, W = 4000, 256, 6
+    fmt = DataDesc(1, 0, 1)
+    rng = np.random.default_rng(hash(case) % 2**32)
+    st = DataStore(fmt, KeyRange(100, 100 + rows - 1), cols, async_push=True)
+    o = oracle_store(oracle, fmt, 100, 100 + rows - 1, cols)
+    init = rng.standard_normal((rows, cols)).astype(np.float32)
+    st.load_values(init)
+    o.data[:] = init
+
+    def push(b, kind):
+        keys = np.arange(rows)
+        free = sorted(set(range(rows)) - _sampled_rows(oracle, b % 64, rows))
+        if kind == "permuted":
+            keys = rng.permutation(rows)
+        elif kind == "swapped":
+            i = free[len(free) // 2]
+            j = free[len(free) // 2 + 1]
+            keys[i], keys[j] = keys[j], keys[i]
+        elif kind == "duplicate":
+            i = free[len(free) // 3]
+            keys[i] = keys[free[len(free) // 3 + 5]]
+        elif kind == "out_of_shard":
+            keys = keys.copy()
+            keys[free[len(free) // 2]] = rows + 7  # key - first outside the shard
+        v = (rng.standard_normal((rows, cols)) * 1e-3).astype(np.float32)
+        return encode_matrix_push(keys + 100, v, 0, 1)
+
+    if case == "mixed_pipelined":
+        kinds = [["ascending"] * W, ["ascending", "permuted"] * 3, ["ascending", "swapped"] + ["ascending"] * 4,
+                 ["ascending"] * W, ["duplicate"] + ["ascending"] * 5, ["permuted"] * W, ["ascending"] * W]
+    else:
+        kinds = [["ascending"] * 2 + [case] + ["ascending"] * (W - 3)]
+    err = None
+    dev_all = []
+    for bi, ks in enumerate(kinds):
+        host = [np.frombuffer(push(b, k), np.uint8).copy() for b, k in enumerate(ks)]
+        dev = [torch.from_numpy(h).cuda() for h in host]
+        dev_all.append(dev)
+        torch.cuda.synchronize()
+        st.pushDevice([d.data_ptr() for d in dev], [d.numel() for d in dev])
+        if err is None:
+            for h in host:
+                rc = o.push(h.tobytes())
+                if rc:
+                    err = o.error()
+                    break
+    if err is None:
+        st.flush()
+    else:
+        with pytest.raises(ArrayIndexOutOfBoundsException) as ei:
+            st.flush()
+        assert (ei.value.key, ei.value.col) == (err[1], err[2])
+    assert st.values().tobytes() == o.data.tobytes()
     st.close()

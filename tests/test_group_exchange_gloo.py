@@ -8,8 +8,9 @@ split kernel and the store are CPU stand-ins here (numpy split; the oracle as
 the store), injected by this test — the product ops are dml_shard_split and the
 HIP DataStore (tests/test_gpu_parity.py covers both on the GPU).
 
-Expected: bit-exact against ONE oracle store applying every rank's buckets in
-rank-major order — AdaGrad data, alpha and delta, and int32 counts — because the
+Two exchange calls run back to back without a flush (the pipelined path hands a
+call's slices to the store at the next call). Expected: bit-exact against ONE
+oracle store applying every call's buckets, each call in rank-major order — AdaGrad data, alpha and delta, and int32 counts — because the
 split keeps each push's record order and rows are independent.
 """
 import ctypes as C
@@ -30,11 +31,14 @@ def _fmt(vt):
     return DataDesc(1, 0, vt, False, True, vt == 1)
 
 
-def _buckets(vt, rank):
+CALLS = 2  # back-to-back exchange calls without a flush between them (pipelined path)
+
+
+def _buckets(vt, rank, call=0):
     from distml_amd import encode_matrix_push
     out = []
     for b in range(W):
-        rng = np.random.default_rng(1000 * rank + b)
+        rng = np.random.default_rng(1000 * rank + 100 * call + b)
         keys = rng.permutation(ROWS)[: rng.integers(ROWS // 3, ROWS)]
         if vt == 1:
             vals = (rng.standard_normal((len(keys), COLS)) * 0.6).astype(np.float32)
@@ -111,8 +115,10 @@ def _worker(rank, world, port, vt, out_dir):
             super().__init__(*a, **k)
 
     g = G(fmt, ROWS, COLS, rank, world, device=None, ops=SplitOps(), store_factory=factory)
-    bufs = [torch.from_numpy(b) for b in _buckets(vt, rank)]
-    g.push_exchange([b.data_ptr() for b in bufs], [b.numel() for b in bufs])
+    for call in range(CALLS):
+        bufs = [torch.from_numpy(b) for b in _buckets(vt, rank, call)]
+        g.push_exchange([b.data_ptr() for b in bufs], [b.numel() for b in bufs])
+        del bufs  # the split copied them: the caller may reuse its buffers at once
     g.flush()
     o = g.store.o
     np.save(os.path.join(out_dir, f"data{rank}.npy"), o.data)
@@ -138,9 +144,10 @@ def test_exchange_push_gloo_bit_exact(tmp_path, oracle, world, vt):
     if vt == 1:
         o.set_alpha(*ADA)
     o.data[:] = _init(vt)
-    for r in range(world):
-        for b in _buckets(vt, r):
-            assert o.push(b.tobytes()) == 0
+    for call in range(CALLS):
+        for r in range(world):
+            for b in _buckets(vt, r, call):
+                assert o.push(b.tobytes()) == 0
     got = np.concatenate([np.load(tmp_path / f"data{r}.npy") for r in range(world)])
     assert got.tobytes() == o.data.tobytes()
     if vt == 1:
