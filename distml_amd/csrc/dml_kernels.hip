@@ -613,6 +613,11 @@ __global__ __launch_bounds__(64 * WPB) void k_reduce_rows(T* __restrict__ shard,
             if ((live >> r & 1u) && lane < nb && !lane_ident) slot[row[r] * slot_stride(nb) + lane] = -1;
     }
     const uint64_t vbase = lane < nb ? (uint64_t)bt.base[lane] : 0ull;
+    // Speculative chunks verify identity records through lane 63 of the wave's last
+    // chunk when that lane owns no column (spec_idle, wave-uniform): its load of the
+    // record start carries the key at no extra instruction; otherwise one key load.
+    const bool spec_idle = !FULL && ident != 0ull && ((cg * CPW + CPW - 1) * 64 + 63) * VEC >= cols;
+    const bool spec_lane = spec_idle && lane == 63;
     if constexpr (DEPTH == 3) {
         // Pair-packed: the wave's (push, row) records in push order, RPW of them per
         // load group whatever push they come from. A batch whose pushes list few of
@@ -645,6 +650,7 @@ __global__ __launch_bounds__(64 * WPB) void k_reduce_rows(T* __restrict__ shard,
             if (np == 0) break;
             u32x4 raw[RPW][CPW];
             int32_t prr[RPW];
+            int64_t kv[RPW];  // identity verification: the key each group element read
 #pragma unroll
             for (int g = 0; g < RPW; ++g) {
                 const int b = pb[g] < 64 ? pb[g] : 0;
@@ -666,18 +672,19 @@ __global__ __launch_bounds__(64 * WPB) void k_reduce_rows(T* __restrict__ shard,
                 } else {
 #pragma unroll
                     for (int c = 0; c < CPW; ++c) {
-                        const uint8_t* src =
-                            (rr >= 0 && nv[c] > 0) ? bp + (int64_t)rr * stride + voff[c] - shb[c] : fb;
+                        // an idle lane of the last chunk (spec_lane) loads the record's key
+                        // for the identity verification instead of a dummy address
+                        const uint8_t* src = (rr >= 0 && nv[c] > 0) ? bp + (int64_t)rr * stride + voff[c] - shb[c]
+                                             : (c == CPW - 1 && spec_lane && rr >= 0) ? bp + (int64_t)rr * stride
+                                                                                     : fb;
                         raw[g][c] = NT ? ldg16_nt(src) : ldg16(src);
                     }
                 }
                 if constexpr (MODE == kAdd) {
-                    if (rr >= 0 && ((ident >> b) & 1ull)) {  // wave-uniform: verify the identity record's key
-                        int64_t rw = row[0];
-#pragma unroll
-                        for (int r = 1; r < RPW; ++r) rw = pr[g] == r ? row[r] : rw;
-                        bad |= row_index(ld_key(bp + (int64_t)rr * stride, K), bt.first, rows) != rw;
-                    }
+                    // wave-uniform: the identity record's key, compared after the adds (an
+                    // early compare would wait for this group's loads before the next is issued)
+                    kv[g] = bt.first;
+                    if (rr >= 0 && ((ident >> b) & 1ull) && !spec_idle) kv[g] = ld_key(bp + (int64_t)rr * stride, K);
                 }
             }
 #pragma unroll
@@ -709,6 +716,24 @@ __global__ __launch_bounds__(64 * WPB) void k_reduce_rows(T* __restrict__ shard,
                                         if (p < negpos) negpos = p;
                                     }
                             }
+                    }
+                }
+            }
+            if constexpr (MODE == kAdd) {
+                if (ident) {
+#pragma unroll
+                    for (int g = 0; g < RPW; ++g) {
+                        if (pb[g] >= 64 || prr[g] < 0 || !((ident >> pb[g]) & 1ull)) continue;  // wave-uniform
+                        int64_t rw = row[0];
+#pragma unroll
+                        for (int r = 1; r < RPW; ++r) rw = pr[g] == r ? row[r] : rw;
+                        int64_t k = kv[g];
+                        if (spec_idle) {
+                            const uint32_t lo = (uint32_t)__builtin_amdgcn_readlane((int)raw[g][CPW - 1].x, 63);
+                            const uint32_t hi = (uint32_t)__builtin_amdgcn_readlane((int)raw[g][CPW - 1].y, 63);
+                            k = K == 4 ? (int64_t)(int32_t)lo : (int64_t)((uint64_t)lo | ((uint64_t)hi << 32));
+                        }
+                        bad |= row_index(k, bt.first, rows) != rw;
                     }
                 }
             }
@@ -806,6 +831,142 @@ __global__ __launch_bounds__(64 * WPB) void k_reduce_rows(T* __restrict__ shard,
     }
     if (MODE == kAddCheckI32 && negpos != kNoPos) atomicMin(&ctrl->neg_pos, (unsigned long long)negpos);
     if (MODE == kAdd && bad) ctrl->spec_ok = 0u;  // an identity push is not: the host re-runs the chunk
+}
+
+// ---------------------------------------------------------------------------
+// k_reduce_flat: plain sums (kAdd / kPreReduce) of rows narrower than 4 KiB
+// whose pushes list most rows (config 4's 800-B Word2Vec rows). A wave owns R
+// neighbouring rows, R = min(16, 512 / (cols / VEC)), and maps their R x cols
+// elements onto its 64 lanes as one flat run of 16-B vectors: lane l, step j
+// owns vector j*64 + l, so every lane works (k_reduce_rows leaves 14 of 64 lanes
+// idle at 200 columns) and the shard block is read and written as one
+// contiguous span. The wave's slot rows sit in LDS; per push a lane reads its
+// vector's record from there and issues up to JMAX 16-B loads, then adds them in
+// push order (one IEEE rounding per add, the reference's order per element).
+// Same results as k_reduce_rows bit for bit: same cutoff, repeated-row and
+// pre-reduce row-map rules.
+template <typename T, int MODE, int JMAX, int PB>
+__global__ __launch_bounds__(256) void k_reduce_flat(T* __restrict__ shard, int64_t rows, int32_t cols, int32_t R,
+                                                     const Batch bt, int nb, int64_t stride, int K,
+                                                     int32_t* __restrict__ slot, const uint32_t* __restrict__ rowflag,
+                                                     Ctrl* __restrict__ ctrl, uint64_t tail_cut, RowMap rm) {
+    constexpr int VEC = Elem<T>::VEC;
+    constexpr int RMAX = 16;
+    static_assert(MODE == kAdd || MODE == kPreReduce, "plain sums only");
+    __shared__ int32_t s_slot[4][RMAX * kMaxW];  // per wave: [row][push], -1 = no record / skipped row
+    const int lane = threadIdx.x & 63;
+    const int wid = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    const int64_t t0 = ((int64_t)blockIdx.x * 4 + wid) * R;  // first task row of the wave
+    if (t0 >= rows) return;
+    if (bt.prev && ctrl_abnormal(bt.prev)) return;  // predecessor needs the host first
+    const int NV = cols / VEC;
+    const int nrow = (int)(rows - t0 < (int64_t)R ? rows - t0 : (int64_t)R);
+    const int ss = slot_stride(nb);
+    int32_t* const ls = s_slot[wid];
+    auto model_row = [&](int64_t t) { return rm.block ? (t / rm.block) * rm.stride + rm.off + t % rm.block : t; };
+    auto out_ptr = [&](int rlj, int cvj) {
+        const int64_t t = t0 + rlj;
+        return (rm.out ? (T*)rm.out + t * (int64_t)cols : shard + model_row(t) * (int64_t)cols) + cvj * VEC;
+    };
+    // the wave's slot rows into LDS (rows a push repeats, and padding rows, stay -1;
+    // the table is handed back clean for the next batch's index)
+    for (int e = lane; e < nrow * nb; e += 64) {
+        const int rl = e / nb, b = e - rl * nb;
+        const int64_t mr = model_row(t0 + rl);
+        int32_t v = -1;
+        if (!(rm.block && mr >= rm.rows_total) && !(rowflag && rowflag[mr])) {
+            v = slot[mr * ss + b];
+            slot[mr * ss + b] = -1;
+        }
+        ls[rl * kMaxW + b] = v;
+    }
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+
+    // this lane's vectors: (row << 16 | vector within the row); bit j of `on` / `wr`:
+    // the vector belongs to a row this batch updates / is written back
+    int rc[JMAX];
+    uint32_t on = 0, wr = 0;
+    T acc[JMAX][VEC];
+    const int nvec = nrow * NV;
+#pragma unroll
+    for (int j = 0; j < JMAX; ++j) {
+        const int v = j * 64 + lane;
+        const int rlj = v < nvec ? v / NV : 0;
+        const int cvj = v < nvec ? v - rlj * NV : 0;
+        rc[j] = (rlj << 16) | cvj;
+        const int64_t mr = model_row(t0 + rlj);
+        const bool pad = rm.block && mr >= rm.rows_total;
+        const bool flagged = !pad && rowflag && rowflag[mr];
+        const bool o = v < nvec && !pad && !flagged;
+        on |= (o ? 1u : 0u) << j;
+        wr |= ((v < nvec && (MODE == kPreReduce ? !flagged : o)) ? 1u : 0u) << j;
+        if (MODE != kPreReduce && o) {
+            unpack<T>(ldg16((const uint8_t*)out_ptr(rlj, cvj)), acc[j]);
+        } else {
+#pragma unroll
+            for (int e = 0; e < VEC; ++e) acc[j][e] = T(0);
+        }
+    }
+    uint64_t cut = ctrl->cutoff;
+    if (tail_cut < cut) cut = tail_cut;
+    if (cut != kNoPos) {
+        // error batch: element by element, pushes in order, up to the cutoff byte
+        const int cut_b = (int)(cut >> 40);
+        const uint64_t cut_off = cut & kOffMask;
+        for (int j = 0; j < JMAX; ++j) {
+            if (!(on >> j & 1u)) continue;
+            for (int b = 0; b < nb; ++b) {
+                const int gb = bt.bidx[b];
+                if (gb > cut_b) break;
+                const int32_t rr = ls[(rc[j] >> 16) * kMaxW + b];
+                if (rr < 0) continue;
+                for (int e = 0; e < VEC; ++e) {
+                    const uint64_t off = (uint64_t)((int64_t)rr * stride + K +
+                                                    (int64_t)((rc[j] & 0xFFFF) * VEC + e) * (int64_t)sizeof(T));
+                    if (gb == cut_b && off >= cut_off) break;
+                    acc[j][e] = Elem<T>::add(acc[j][e], Elem<T>::load(bt.base[b] + off));
+                }
+            }
+        }
+    } else {
+        // PB pushes per round: all their loads in flight, then added push by push
+#pragma unroll 1
+        for (int b0 = 0; b0 < nb; b0 += PB) {
+            int32_t rr[PB][JMAX];
+            u32x4 raw[PB][JMAX];
+#pragma unroll
+            for (int p = 0; p < PB; ++p) {
+                const int b = b0 + p < nb ? b0 + p : nb - 1;
+                const uint8_t* const bp = bt.base[b];
+#pragma unroll
+                for (int j = 0; j < JMAX; ++j) {
+                    rr[p][j] = (b0 + p < nb && (on >> j & 1u)) ? ls[(rc[j] >> 16) * kMaxW + b] : -1;
+                    const uint8_t* src = bp + (int64_t)(rr[p][j] >= 0 ? rr[p][j] : 0) * stride + K +
+                                         (int64_t)(rc[j] & 0xFFFF) * 16;
+                    raw[p][j] = rr[p][j] >= 0 ? ldg16_nt(src) : u32x4{0u, 0u, 0u, 0u};
+                }
+            }
+#pragma unroll
+            for (int p = 0; p < PB; ++p)
+#pragma unroll
+                for (int j = 0; j < JMAX; ++j) {
+                    if (rr[p][j] < 0) continue;
+                    T u[VEC];
+                    unpack<T>(raw[p][j], u);
+#pragma unroll
+                    for (int e = 0; e < VEC; ++e) acc[j][e] = Elem<T>::add(acc[j][e], u[e]);
+                }
+        }
+    }
+#pragma unroll
+    for (int j = 0; j < JMAX; ++j)
+        if (wr >> j & 1u) {
+            T* const op = out_ptr(rc[j] >> 16, rc[j] & 0xFFFF);
+            if (MODE == kPreReduce) stg16(op, pack<T>(acc[j]));
+            else stg16_nt(op, pack<T>(acc[j]));
+        }
 }
 
 // Occupancy cap: dynamic LDS (unused by the kernels) so that at most `bpc`
@@ -910,6 +1071,52 @@ static hipError_t launch_auto(void* shard, int64_t rows, int32_t cols, const Bat
 #undef DML_LF
 }
 
+// k_reduce_flat launch (narrow dense rows, see the kernel): R rows per wave.
+template <typename T, int MODE, int JMAX, int PB>
+static hipError_t launch_flat_t(void* shard, int64_t rows, int32_t cols, const Batch& bt, int nb, int64_t stride,
+                                int K, const int32_t* slot, const uint32_t* rowflag, Ctrl* ctrl, uint64_t tail_cut,
+                                hipStream_t st, int64_t* nblocks_out, LaunchEv ev, RowMap rm) {
+    constexpr int VEC = Elem<T>::VEC;
+    const int NV = cols / VEC;
+    const int R = std::max(1, std::min(16, JMAX * 64 / NV));
+    const int64_t nblocks = ((rows + R - 1) / R + 3) / 4;
+    if (nblocks_out) *nblocks_out = nblocks;
+    if (nblocks <= 0) return hipSuccess;
+    if (ev.start || ev.stop)
+        hipExtLaunchKernelGGL((k_reduce_flat<T, MODE, JMAX, PB>), dim3((unsigned)nblocks), dim3(256), 0, st, ev.start,
+                              ev.stop, 0, (T*)shard, rows, cols, R, bt, nb, stride, K, const_cast<int32_t*>(slot),
+                              rowflag, ctrl, tail_cut, rm);
+    else
+        hipLaunchKernelGGL((k_reduce_flat<T, MODE, JMAX, PB>), dim3((unsigned)nblocks), dim3(256), 0, st, (T*)shard,
+                           rows, cols, R, bt, nb, stride, K, const_cast<int32_t*>(slot), rowflag, ctrl, tail_cut, rm);
+    return hipGetLastError();
+}
+
+// JMAX 8 vectors per lane (R = 10 rows at 200 columns), one push per round:
+// measured within 2 % of 4 x 1, 4 x 2, 8 x 2 and 4 x 4 (config 4, ascending
+// and permuted), and of occupancy caps at 1-3 blocks per CU (all slower).
+template <typename T, int MODE>
+static hipError_t launch_flat(void* shard, int64_t rows, int32_t cols, const Batch& bt, int nb, int64_t stride, int K,
+                              const int32_t* slot, const uint32_t* rowflag, Ctrl* ctrl, uint64_t tail_cut,
+                              hipStream_t st, int64_t* nblocks_out, LaunchEv ev, RowMap rm) {
+    return launch_flat_t<T, MODE, 8, 1>(shard, rows, cols, bt, nb, stride, K, slot, rowflag, ctrl, tail_cut, st,
+                                        nblocks_out, ev, rm);
+}
+
+// The flat narrow-row kernel applies to plain sums of rows narrower than 4 KiB
+// (whole vectors, no speculation) when every push of the chunk lists at least
+// half the rows (dense pushes; sparse ones keep the pair-packed k_reduce_rows).
+bool use_flat(int vtype, int mode, int32_t cols, const Batch& bt, int nb, int64_t rows) {
+    if (mode != kAdd && mode != kPreReduce) return false;
+    if (bt.spec) return false;
+    const int VEC = vtype == kF64 ? 2 : 4;
+    const int elem = vtype == kF64 ? 8 : 4;
+    if (cols % VEC || (int64_t)cols * elem >= 4096 || nb <= 0) return false;
+    for (int b = 0; b < nb; ++b)
+        if (2 * bt.nrec[b] < rows) return false;
+    return true;
+}
+
 bool reduce_clears_slots(int vtype, int mode, int32_t cols) {
     if (mode == kAdaGrad) return vtype == kF32 && cols <= 64 * 4;  // k_reduce, one chunk group per row
     if (mode != kAdd && mode != kPreReduce) return false;
@@ -930,6 +1137,13 @@ hipError_t launch_reduce(int vtype, int mode, void* shard, int64_t rows, int32_t
                          uint64_t tail_cut, const AdaArgs& ada, hipStream_t st, int64_t* nblocks_out, LaunchEv ev,
                          RowMap rm) {
 #define DML_A(T, M) launch_auto<T, M>(shard, rows, cols, bt, nb, stride, K, slot, rowflag, ctrl, tail_cut, ada, st, nblocks_out, ev, rm)
+#define DML_F(T, M) launch_flat<T, M>(shard, rows, cols, bt, nb, stride, K, slot, rowflag, ctrl, tail_cut, st, nblocks_out, ev, rm)
+    if (use_flat(vtype, mode, cols, bt, nb, rm.block ? rm.rows_total : rows)) {
+        if (vtype == kF32) return mode == kAdd ? DML_F(float, kAdd) : DML_F(float, kPreReduce);
+        if (vtype == kI32) return mode == kAdd ? DML_F(int32_t, kAdd) : DML_F(int32_t, kPreReduce);
+        if (vtype == kF64) return mode == kAdd ? DML_F(double, kAdd) : DML_F(double, kPreReduce);
+    }
+#undef DML_F
     if (vtype == kF32) {
         if (mode == kAdd) return DML_A(float, kAdd);
         if (mode == kAdaGrad) return DML_A(float, kAdaGrad);

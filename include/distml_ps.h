@@ -132,7 +132,9 @@ int dml_store_shape(dml_store* s, int64_t* rows, int32_t* cols);
  * to/from host memory; test/oracle access and initial load. */
 int dml_store_read_dense(dml_store* s, void* host_dst, int64_t bytes);
 int dml_store_write_dense(dml_store* s, const void* host_src, int64_t bytes);
-/* Device pointer of the value array (rows*cols elements), valid until destroy. */
+/* Device pointer of the value array (rows*cols elements) as of this call; valid
+ * until the next push (a speculative full-range batch writes the store's second
+ * buffer and commits it) or destroy. */
 int dml_store_device_ptr(dml_store* s, void** dev_ptr);
 /* AdaGrad side arrays (FloatMatrixStoreAdaGrad.java:23-24), f32 row-major. */
 int dml_store_read_adagrad(dml_store* s, float* alpha_dst, float* delta_dst, int64_t elems);

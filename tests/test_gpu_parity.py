@@ -1260,4 +1260,13 @@ def test_identity_speculation_exact(oracle, case):
             st.flush()
         assert (ei.value.key, ei.value.col) == (err[1], err[2])
     assert st.values().tobytes() == o.data.tobytes()
+    if case == "ascending":
+        # the speculative path ran: a verified chunk commits the other shard buffer
+        p0 = st.device_ptr()
+        st.pushDevice([d.data_ptr() for d in dev_all[0]], [d.numel() for d in dev_all[0]])
+        st.flush()
+        assert st.device_ptr() != p0
+        for d in dev_all[0]:
+            assert o.push(d.cpu().numpy().tobytes()) == 0
+        assert st.values().tobytes() == o.data.tobytes()
     st.close()
