@@ -60,19 +60,29 @@ __host__ __device__ inline bool ctrl_abnormal(const Ctrl* c) {
     return c->cutoff != kNoPos || c->neg_pos != kNoPos || c->no_dup == 0u || c->spec_ok == 0u;
 }
 
-// Running AdaGrad maxDelta state (FloatMatrixStoreAdaGrad.java:27-29), device resident.
-struct MaxDelta {
-    float value;
-    int32_t row;
-    int32_t col;
-    int32_t pad;
-};
 // Per-block AdaGrad candidate: the largest final delta of an element whose
 // delta rose in this batch, and the position where it last rose.
 struct DeltaCand {
     float value;
     int32_t valid;
     unsigned long long pos;
+};
+// Running AdaGrad maxDelta state (FloatMatrixStoreAdaGrad.java:27-29), device
+// resident, plus the chunk's best candidate while it waits for the rows a push
+// repeats (replayed in layers): the chunk's candidates are finalized once, so a
+// tie between a repeated and a non-repeated row goes to the earlier position.
+struct MaxDelta {
+    float value;
+    int32_t row;
+    int32_t col;
+    int32_t pad;
+    DeltaCand pend;
+};
+// k_maxdelta finalize modes
+enum MdMode : int {
+    kMdApply = 0,          // merge with the pending candidate, apply (strict >), clear it
+    kMdDefer = 1,          // merge into the pending candidate only
+    kMdDeferIfRepeat = 2,  // kMdDefer when the chunk's index saw a repeated row (ctrl->no_dup == 0)
 };
 
 // Optional row map of a reduce launch (multi-GPU pre-reduce pieces): task row t
@@ -127,7 +137,8 @@ hipError_t launch_rollback_i32(int32_t* shard, int64_t rows, int32_t cols, const
 // `cand` holds n candidates plus kMdParts entries of scratch after them.
 constexpr int kMdParts = 256;
 hipError_t launch_maxdelta_finalize(DeltaCand* cand, int64_t n, MaxDelta* md, const Batch& bt, int nb,
-                                    int64_t stride, int K, int V, hipStream_t st);
+                                    int64_t stride, int K, int V, hipStream_t st, int mode = kMdApply,
+                                    const Ctrl* ctrl = nullptr);
 hipError_t launch_array_validate(const Batch& bt, int nb, int64_t max_nrec, int64_t stride,
                                  int K, int64_t first, int64_t rows, Ctrl* ctrl, uint64_t tail_cut, hipStream_t st);
 hipError_t launch_array_apply(int vtype, void* shard, int64_t rows, const uint8_t* base, int64_t nrec,
@@ -163,6 +174,18 @@ struct SpPlan {
     int64_t rec_base[kMaxW + 1];   // first sequence number of push b (prefix of nrec)
     int64_t nrec, ntiles1, nleaves, max_tiles2;
     int nb, SL, D2, nbins1;        // leaf = row >> SL; 2^D2 leaves per level-1 bin
+    // single-pass partition (no count passes): fixed-capacity bins (cap1 records
+    // per level-1 bin, cap2 per leaf) filled through atomic cursors; an overflow
+    // falls back to the counted partition before the leaf runs
+    int64_t cap1, cap2, tiles2_per_bin;
+    int fast;                      // the leaf reads the fixed-capacity layout
+    uint32_t seq_cut;              // records with sequence >= seq_cut are at / past the cutoff
+};
+// Pinned status of a single-pass partition, read by the host before the leaf launch.
+struct SpStat {
+    unsigned int overflow;         // a bin or leaf exceeded its capacity
+    unsigned int pad;
+    unsigned long long cutoff;     // Ctrl::cutoff after the partition (first key outside the shard)
 };
 // Device-side results of level 1 (bin bounds, level-2 tile table).
 struct SpMeta {
@@ -173,13 +196,19 @@ struct SpMeta {
 // Byte offsets of the partition buffers inside one workspace allocation.
 struct SpLayout {
     size_t meta, comp1, val1, comp2, val2, cnt1, off1, cnt2, off2, leafflag, bounds, scan_tmp, scan_tmp_bytes,
-        total;
+        cur1, cur2, stat, total;
 };
 SpPlan sparse_plan(const Batch& bt, int nb, int64_t rows);
 SpLayout sparse_layout(const SpPlan& pl, int vbytes);
 hipError_t launch_sparse_partition(int vtype, const Batch& bt, const SpPlan& pl, const SpLayout& l, uint8_t* ws,
                                    int64_t stride, int K, int64_t first, int64_t rows, Ctrl* ctrl,
                                    uint64_t tail_cut, hipStream_t st);
+// Single-pass partition into the fixed-capacity layout; copies its SpStat to `hstat` (pinned).
+hipError_t launch_sparse_partition_fast(int vtype, const Batch& bt, const SpPlan& pl, const SpLayout& l, uint8_t* ws,
+                                        int64_t stride, int K, int64_t first, int64_t rows, Ctrl* ctrl,
+                                        uint64_t tail_cut, SpStat* hstat, hipStream_t st);
+// Sequence number of the first record at / past `cut` (a record-start position, or kNoPos).
+uint32_t sparse_seq_cut(const SpPlan& pl, const Batch& bt, uint64_t cut, int64_t stride);
 hipError_t launch_sparse_leaf(int vtype, void* shard, const SpPlan& pl, const SpLayout& l, uint8_t* ws, Ctrl* ctrl,
                               const Ctrl* prev, hipStream_t st, LaunchEv ev);
 hipError_t sparse_replay(int vtype, void* shard, const SpPlan& pl, const SpLayout& l, uint8_t* ws, hipStream_t st);

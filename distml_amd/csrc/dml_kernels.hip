@@ -1197,13 +1197,25 @@ __global__ __launch_bounds__(256) void k_maxdelta_part(DeltaCand* __restrict__ c
 
 __global__ __launch_bounds__(256) void k_maxdelta(const DeltaCand* __restrict__ cand, int64_t n,
                                                   MaxDelta* __restrict__ md, const Batch bt, int nb,
-                                                  int64_t stride, int K, int V) {
+                                                  int64_t stride, int K, int V, int mode,
+                                                  const Ctrl* __restrict__ ctrl) {
     bool ok = false;
     float v = 0.f;
     uint64_t p = kNoPos;
     cand_scan(cand, threadIdx.x, n, 256, ok, v, p);
     cand_block_best<4>(ok, v, p);
-    if (threadIdx.x == 0 && ok && v > md->value) {
+    if (threadIdx.x != 0) return;
+    const DeltaCand pd = md->pend;  // the chunk's candidates so far (main reduce, earlier layers)
+    if (cand_better(pd.valid != 0, pd.value, pd.pos, ok, v, p)) { ok = true; v = pd.value; p = pd.pos; }
+    const bool defer = mode == kMdDefer || (mode == kMdDeferIfRepeat && ctrl && ctrl->no_dup == 0u);
+    if (defer) {
+        DeltaCand c;
+        c.value = v; c.valid = ok; c.pos = p;
+        md->pend = c;
+        return;
+    }
+    md->pend.valid = 0;
+    if (ok && v > md->value) {
         const int gb = (int)(p >> 40);
         int b = 0;
         while (b < nb - 1 && bt.bidx[b] != gb) ++b;
@@ -1216,13 +1228,13 @@ __global__ __launch_bounds__(256) void k_maxdelta(const DeltaCand* __restrict__ 
 }
 
 hipError_t launch_maxdelta_finalize(DeltaCand* cand, int64_t n, MaxDelta* md, const Batch& bt, int nb,
-                                    int64_t stride, int K, int V, hipStream_t st) {
+                                    int64_t stride, int K, int V, hipStream_t st, int mode, const Ctrl* ctrl) {
     if (n > 4 * 256 * kMdParts) {
         hipLaunchKernelGGL(k_maxdelta_part, dim3(kMdParts), dim3(256), 0, st, cand, n);
         hipLaunchKernelGGL(k_maxdelta, dim3(1), dim3(256), 0, st, cand + n, (int64_t)kMdParts, md, bt, nb, stride, K,
-                           V);
+                           V, mode, ctrl);
     } else {
-        hipLaunchKernelGGL(k_maxdelta, dim3(1), dim3(256), 0, st, cand, n, md, bt, nb, stride, K, V);
+        hipLaunchKernelGGL(k_maxdelta, dim3(1), dim3(256), 0, st, cand, n, md, bt, nb, stride, K, V, mode, ctrl);
     }
     return hipGetLastError();
 }

@@ -92,6 +92,7 @@ struct Workspace {
     hipEvent_t done = nullptr;        // copy stream: ctrl copied out (chunk retired-able)
     uint8_t* sp = nullptr;            // sparse partition buffers (SpLayout), grown on demand
     size_t sp_cap = 0;
+    SpStat* hsp = nullptr;            // pinned status of the single-pass sparse partition
     bool clears = false;              // the chunk's reduce leaves its slot table all -1
     bool clean = false;               // slot table all -1 and rowflags 0: only the Ctrl needs a reset
 };
@@ -349,7 +350,9 @@ int launch_apply(dml_store* s, Chunk& c, Workspace& W, const Ctrl* prev) {
         HIPCHK(launch_reduce(vtype_of(s->desc), reduce_mode(s), c.out, s->rows, s->cols, c.bt, c.nb, s->stride,
                              s->K, W.slot, W.rowflag, W.ctrl, c.tail_cut, ada_args(s), s->stream, &nblk, ev));
         if (s->adagrad)
-            HIPCHK(launch_maxdelta_finalize(s->cand, nblk, s->md, c.bt, c.nb, s->stride, s->K, s->V, s->stream));
+            // finalized here unless the index saw a repeated row: then after its replay
+            HIPCHK(launch_maxdelta_finalize(s->cand, nblk, s->md, c.bt, c.nb, s->stride, s->K, s->V, s->stream,
+                                            kMdDeferIfRepeat, W.ctrl));
         if (!inpacket) HIPCHK(hipEventRecord(W.applied, s->stream));
         if (s->timing) s->ev_used.emplace_back(W.kstart, W.applied);
     } else if (c.sorted) {
@@ -425,8 +428,9 @@ int launch_chunk(dml_store* s, Chunk& c, Workspace& W, const Ctrl* prev) {
                 HIPCHK(hipMalloc((void**)&W.sp, c.spl.total));
                 W.sp_cap = c.spl.total;
             }
-            HIPCHK(launch_sparse_partition(vt, c.bt, c.sp, c.spl, W.sp, s->stride, s->K, s->first, s->rows, W.ctrl,
-                                           c.tail_cut, is));
+            if (!W.hsp) HIPCHK(hipHostMalloc((void**)&W.hsp, sizeof(SpStat), hipHostMallocDefault));
+            HIPCHK(launch_sparse_partition_fast(vt, c.bt, c.sp, c.spl, W.sp, s->stride, s->K, s->first, s->rows,
+                                                W.ctrl, c.tail_cut, W.hsp, is));
         }
     }
     HIPCHK(hipEventRecord(W.idx_done, s->istream));
@@ -435,6 +439,20 @@ int launch_chunk(dml_store* s, Chunk& c, Workspace& W, const Ctrl* prev) {
     // directly behind that reduce. A cross-queue barrier packet instead costs
     // ~16 µs of idle GPU between the two reduces (measured).
     HIPCHK(hipEventSynchronize(W.idx_done));
+    if (c.sorted && c.sp.fast) {
+        if (W.hsp->overflow) {
+            // a bin or leaf of the single-pass partition overflowed (skewed keys):
+            // the counted partition, compact layout (still beside the running apply)
+            c.sp.fast = 0;
+            c.sp.seq_cut = kSpSkip;
+            HIPCHK(launch_sparse_partition(vtype_of(s->desc), c.bt, c.sp, c.spl, W.sp, s->stride, s->K, s->first,
+                                           s->rows, W.ctrl, c.tail_cut, s->istream));
+            HIPCHK(hipEventRecord(W.idx_done, s->istream));
+            HIPCHK(hipEventSynchronize(W.idx_done));
+        } else {
+            c.sp.seq_cut = sparse_seq_cut(c.sp, c.bt, std::min<uint64_t>(W.hsp->cutoff, c.tail_cut), s->stride);
+        }
+    }
     return launch_apply(s, c, W, prev);
 }
 
@@ -502,8 +520,13 @@ int replay_rows(dml_store* s, const Chunk& c, Workspace& W, Ctrl* ctl) {
         int64_t nblk = 0;
         HIPCHK(launch_reduce(vtype_of(s->desc), reduce_mode(s), s->data, s->rows, s->cols, vc.bt, vc.nb, s->stride,
                              s->K, W.slot, nullptr, W.ctrl, vc.tail_cut, ada_args(s), s->stream, &nblk));
-        if (s->adagrad)
-            HIPCHK(launch_maxdelta_finalize(s->cand, nblk, s->md, vc.bt, vc.nb, s->stride, s->K, s->V, s->stream));
+        if (s->adagrad)  // the layers' candidates join the chunk's pending one
+            HIPCHK(launch_maxdelta_finalize(s->cand, nblk, s->md, vc.bt, vc.nb, s->stride, s->K, s->V, s->stream,
+                                            kMdDefer));
+        HIPCHK(hipStreamSynchronize(s->stream));
+    }
+    if (s->adagrad) {  // one finalize over the whole chunk: the reference's first position wins a tie
+        HIPCHK(launch_maxdelta_finalize(s->cand, 0, s->md, c.bt, c.nb, s->stride, s->K, s->V, s->stream, kMdApply));
         HIPCHK(hipStreamSynchronize(s->stream));
     }
     if (int rc = read_ctrl(s, W, ctl)) return rc;
@@ -899,6 +922,7 @@ void dml_store_destroy(dml_store* s) {
         for (Workspace& W : s->ws) {
             (void)hipFree(W.base);
             (void)hipFree(W.sp);
+            if (W.hsp) (void)hipHostFree(W.hsp);
             if (W.hctrl) (void)hipHostFree(W.hctrl);
             if (W.idx_done) (void)hipEventDestroy(W.idx_done);
             if (W.done) (void)hipEventDestroy(W.done);

@@ -7,6 +7,7 @@
 #include <algorithm>
 #include <cstdio>
 #include <cstdlib>
+#include <type_traits>
 #include <vector>
 
 #define CK(x)                                                                         \
@@ -46,6 +47,26 @@ __global__ void k_plain4(float* a, const uint32_t* keys, const float* v, int64_t
 #pragma unroll
     for (int j = 0; j < 4; ++j)
         if (i0 + j * stride < n) a[k[j]] = x[j] + u[j];
+}
+// One thread per touched U-float unit (U = 8: 32-B sector, 16: 64 B, 32: 128-B line):
+// load the whole unit, add the unit's records (a run of the globally sorted keys),
+// store the whole unit — full-unit writes instead of one 4-B store per record.
+template <int U>
+__global__ void k_unit(float* a, const uint32_t* unit, const uint32_t* run, const uint32_t* keys, const float* v,
+                       int64_t nu) {
+    int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= nu) return;
+    float4 q[U / 4];
+    float4* p = (float4*)(a + (int64_t)unit[i] * U);
+#pragma unroll
+    for (int j = 0; j < U / 4; ++j) q[j] = p[j];
+    for (uint32_t r = run[i]; r < run[i + 1]; ++r) {
+        const int e = keys[r] % U;
+        float* f = (float*)q;
+        f[e] += v[r];
+    }
+#pragma unroll
+    for (int j = 0; j < U / 4; ++j) p[j] = q[j];
 }
 __global__ void k_read(const float4* p, int64_t n, float* out) {
     float s = 0;
@@ -129,6 +150,28 @@ int main() {
     timeit("plain RMW, 1 launch, globally sorted 32e6", [&] { k_plain<<<gN, 256>>>(a, dg, dv, N); });
     timeit("plain RMW x4, 1 launch, globally sorted", [&] { k_plain4<<<(gN + 3) / 4, 256>>>(a, dg, dv, N); });
     timeit("atomic, 1 launch, globally sorted", [&] { k_atomic<<<gN, 256>>>(a, dg, dv, N); });
+    auto unit_case = [&](auto tag, const char* name) {
+        constexpr int U = decltype(tag)::value;
+        std::vector<uint32_t> hu, hr;
+        for (int64_t r = 0; r < N; ++r) {
+            const uint32_t u = hg[r] / U;
+            if (hu.empty() || hu.back() != u) { hu.push_back(u); hr.push_back((uint32_t)r); }
+        }
+        hr.push_back((uint32_t)N);
+        uint32_t *du, *dr;
+        CK(hipMalloc(&du, hu.size() * 4));
+        CK(hipMalloc(&dr, hr.size() * 4));
+        CK(hipMemcpy(du, hu.data(), hu.size() * 4, hipMemcpyHostToDevice));
+        CK(hipMemcpy(dr, hr.data(), hr.size() * 4, hipMemcpyHostToDevice));
+        const int64_t nu = (int64_t)hu.size();
+        printf("  (%lld units of %d floats touched)\n", (long long)nu, U);
+        timeit(name, [&] { k_unit<U><<<(unsigned)((nu + 255) / 256), 256>>>(a, du, dr, dg, dv, nu); });
+        CK(hipFree(du));
+        CK(hipFree(dr));
+    };
+    unit_case(std::integral_constant<int, 8>{}, "unit RMW 32 B, globally sorted");
+    unit_case(std::integral_constant<int, 16>{}, "unit RMW 64 B, globally sorted");
+    unit_case(std::integral_constant<int, 32>{}, "unit RMW 128 B, globally sorted");
     {
         float ms_best = 1e30f;
         for (int rep = 0; rep < 5; ++rep) {

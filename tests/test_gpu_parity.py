@@ -1270,3 +1270,79 @@ def test_identity_speculation_exact(oracle, case):
             assert o.push(d.cpu().numpy().tobytes()) == 0
         assert st.values().tobytes() == o.data.tobytes()
     st.close()
+
+
+@pytest.mark.parametrize("batched", [True, False])
+def test_adagrad_maxdelta_tie_repeated_row(oracle, batched):
+    """a push that lists row 5 twice reaches delta 2.0 at its second
+    record, before row 2 reaches the same 2.0 at the third record. The reference's
+    strict `deltas[i] > maxDelta` (FloatMatrixStoreAdaGrad.java:273-277) keeps row 5.
+    Row 5 is replayed in layers; its candidate must still win the tie."""
+    from distml_amd import DataDesc, encode_matrix_push
+    rows, cols = 8, 4
+    fmt = DataDesc(1, 0, 1, False, True, True)
+    s, _ = mk_store(fmt, 0, rows - 1, cols)
+    o = oracle_store(oracle, fmt, 0, rows - 1, cols)
+    s.setAlpha(0.025, 0.0001, 1.5)
+    o.set_alpha(0.025, 0.0001, 1.5)
+    one = np.zeros((1, cols), np.float32)
+    one[0, 0] = 1.0
+    p1 = encode_matrix_push([2], one, 0, 1)
+    p2 = encode_matrix_push([5, 5, 2], np.repeat(one, 3, axis=0), 0, 1)
+    for p in (p1, p2):
+        assert o.push(p) == 0
+    if batched:
+        s.handlePushBatch(fmt, [p1, p2])
+    else:
+        s.handlePush(fmt, p1)
+        s.handlePush(fmt, p2)
+    assert o.max_delta() == (2.0, 5, 0)
+    assert s.maxDelta() == o.max_delta()
+    assert kat.bits_equal(s.values(), o.data)
+
+
+@pytest.mark.parametrize("case", ["hot_line", "cutoff", "truncated"])
+def test_sparse_single_pass_partition_exact(oracle, case):
+    """The single-pass sparse partition (fixed-capacity bins, atomic cursors; DESIGN.md
+    §4) against the oracle, bit-exact, where it must fall back or cut: `hot_line` — 40
+    pushes all list keys 777..778 (one 32-row line bucket of a leaf holds > 64
+    records): the leaf kernel flags the leaf and the packed exact replay applies it;
+    `cutoff` — a key outside the shard in the middle of push 3: records from it on
+    are not applied (the sequence cut), error state as the reference's;
+    `truncated` — the last push ends inside a record."""
+    from distml_amd import DataDesc, DistMLException, encode_array_push
+    rng = np.random.default_rng(len(case))
+    first, rows = 3, 2_000_000
+    fmt = DataDesc(0, 1, 1)  # FloatArrayStore, LONG keys
+    s, _ = mk_store(fmt, first, first + rows - 1)
+    o = oracle_store(oracle, fmt, first, first + rows - 1)
+    init = rng.standard_normal((rows, 1)).astype(np.float32)
+    s.load_values(init)
+    o.data[:] = init
+    nb = 40 if case == "hot_line" else 6
+    pushes = []
+    for b in range(nb):
+        keys = rng.choice(rows, size=20_000, replace=False) + first
+        if case == "hot_line":
+            keys[:2] = [777 + first, 778 + first]
+        vals = (rng.standard_normal(len(keys)) * 1e-2).astype(np.float32)
+        p = encode_array_push(keys, vals, 1, 1)
+        if case == "cutoff" and b == 3:
+            bad = encode_array_push([rows + first + 5], [1.0], 1, 1)
+            p = p[:12 * 9000] + bad + p[12 * 9000:]
+        if case == "truncated" and b == nb - 1:
+            p = p[:-7]
+        pushes.append(p)
+    err = None
+    for p in pushes:
+        rc = o.push(p)
+        if rc:
+            err = o.error()
+            break
+    if err is None:
+        s.handlePushBatch(fmt, pushes)
+    else:
+        with pytest.raises(DistMLException) as ei:
+            s.handlePushBatch(fmt, pushes)
+        assert (ei.value.code, ei.value.key) == (err[0], err[1])
+    assert s.values().tobytes() == o.data.tobytes()
