@@ -222,6 +222,8 @@ int64_t reduce_blocks(int vtype, int64_t rows, int32_t cols);
 // True when launch_reduce(vtype, mode, cols) runs k_reduce_rows in a plain-sum mode,
 // which rewrites every slot it reads to -1 (the next batch's index then needs no memset).
 bool reduce_clears_slots(int vtype, int mode, int32_t cols);
+// row shapes whose reduce runs identity-speculative chunks (k_reduce_rows FULL, k_reduce_flat)
+bool spec_shape(int vtype, int32_t cols);
 
 uint64_t splitmix64(uint64_t x);
 

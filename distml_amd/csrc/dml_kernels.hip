@@ -843,8 +843,10 @@ __global__ __launch_bounds__(64 * WPB) void k_reduce_rows(T* __restrict__ shard,
 // contiguous span. The wave's slot rows sit in LDS; per push a lane reads its
 // vector's record from there and issues up to JMAX 16-B loads, then adds them in
 // push order (one IEEE rounding per add, the reference's order per element).
-// Same results as k_reduce_rows bit for bit: same cutoff, repeated-row and
-// pre-reduce row-map rules.
+// Same results as k_reduce_rows bit for bit: same cutoff, repeated-row,
+// pre-reduce row-map and identity-speculation rules (an identity push's record r
+// is row r; lanes 0..R-1 load the R records' keys beside the round's vector loads
+// of the same lines and verify them after the adds).
 template <typename T, int MODE, int JMAX, int PB>
 __global__ __launch_bounds__(256) void k_reduce_flat(T* __restrict__ shard, int64_t rows, int32_t cols, int32_t R,
                                                      const Batch bt, int nb, int64_t stride, int K,
@@ -859,6 +861,18 @@ __global__ __launch_bounds__(256) void k_reduce_flat(T* __restrict__ shard, int6
     const int64_t t0 = ((int64_t)blockIdx.x * 4 + wid) * R;  // first task row of the wave
     if (t0 >= rows) return;
     if (bt.prev && ctrl_abnormal(bt.prev)) return;  // predecessor needs the host first
+    uint64_t cut = ctrl->cutoff;
+    if (tail_cut < cut) cut = tail_cut;
+    uint64_t ident = 0;  // identity speculation (Batch::spec), see k_reduce_rows
+    if constexpr (MODE == kAdd) {
+        if (bt.spec) {
+            if (cut != kNoPos || ctrl->no_dup == 0u) {
+                if (lane == 0) ctrl->spec_ok = 0u;
+                return;
+            }
+            ident = ctrl->ident;
+        }
+    }
     const int NV = cols / VEC;
     const int nrow = (int)(rows - t0 < (int64_t)R ? rows - t0 : (int64_t)R);
     const int ss = slot_stride(nb);
@@ -875,8 +889,12 @@ __global__ __launch_bounds__(256) void k_reduce_flat(T* __restrict__ shard, int6
         const int64_t mr = model_row(t0 + rl);
         int32_t v = -1;
         if (!(rm.block && mr >= rm.rows_total) && !(rowflag && rowflag[mr])) {
-            v = slot[mr * ss + b];
-            slot[mr * ss + b] = -1;
+            if ((ident >> b) & 1ull) {  // identity push: record = row (the index skipped it)
+                v = mr < bt.nrec[b] ? (int32_t)mr : -1;
+            } else {
+                v = slot[mr * ss + b];
+                slot[mr * ss + b] = -1;
+            }
         }
         ls[rl * kMaxW + b] = v;
     }
@@ -903,14 +921,16 @@ __global__ __launch_bounds__(256) void k_reduce_flat(T* __restrict__ shard, int6
         on |= (o ? 1u : 0u) << j;
         wr |= ((v < nvec && (MODE == kPreReduce ? !flagged : o)) ? 1u : 0u) << j;
         if (MODE != kPreReduce && o) {
-            unpack<T>(ldg16((const uint8_t*)out_ptr(rlj, cvj)), acc[j]);
+            // the input row: in place, or the speculative chunk's input buffer
+            const T* const ip = (MODE == kAdd && bt.src) ? (const T*)bt.src + mr * (int64_t)cols + cvj * VEC
+                                                         : out_ptr(rlj, cvj);
+            unpack<T>(ldg16((const uint8_t*)ip), acc[j]);
         } else {
 #pragma unroll
             for (int e = 0; e < VEC; ++e) acc[j][e] = T(0);
         }
     }
-    uint64_t cut = ctrl->cutoff;
-    if (tail_cut < cut) cut = tail_cut;
+    bool bad = false;
     if (cut != kNoPos) {
         // error batch: element by element, pushes in order, up to the cutoff byte
         const int cut_b = (int)(cut >> 40);
@@ -936,10 +956,15 @@ __global__ __launch_bounds__(256) void k_reduce_flat(T* __restrict__ shard, int6
         for (int b0 = 0; b0 < nb; b0 += PB) {
             int32_t rr[PB][JMAX];
             u32x4 raw[PB][JMAX];
+            int64_t kv[PB];  // identity pushes: lane l < nrow holds record t0+l's key
 #pragma unroll
             for (int p = 0; p < PB; ++p) {
                 const int b = b0 + p < nb ? b0 + p : nb - 1;
                 const uint8_t* const bp = bt.base[b];
+                if constexpr (MODE == kAdd) {
+                    const bool kl = b0 + p < nb && ((ident >> b) & 1ull) && lane < nrow;
+                    kv[p] = kl ? ld_key(bp + (t0 + lane) * stride, K) : bt.first + t0 + lane;
+                }
 #pragma unroll
                 for (int j = 0; j < JMAX; ++j) {
                     rr[p][j] = (b0 + p < nb && (on >> j & 1u)) ? ls[(rc[j] >> 16) * kMaxW + b] : -1;
@@ -958,6 +983,11 @@ __global__ __launch_bounds__(256) void k_reduce_flat(T* __restrict__ shard, int6
 #pragma unroll
                     for (int e = 0; e < VEC; ++e) acc[j][e] = Elem<T>::add(acc[j][e], u[e]);
                 }
+            if constexpr (MODE == kAdd)
+                if (ident)
+#pragma unroll
+                    for (int p = 0; p < PB; ++p)
+                        bad |= lane < nrow && row_index(kv[p], bt.first, rows) != t0 + lane;
         }
     }
 #pragma unroll
@@ -967,6 +997,7 @@ __global__ __launch_bounds__(256) void k_reduce_flat(T* __restrict__ shard, int6
             if (MODE == kPreReduce) stg16(op, pack<T>(acc[j]));
             else stg16_nt(op, pack<T>(acc[j]));
         }
+    if (MODE == kAdd && bad) ctrl->spec_ok = 0u;  // an identity push is not: the host re-runs the chunk
 }
 
 // Occupancy cap: dynamic LDS (unused by the kernels) so that at most `bpc`
@@ -1104,17 +1135,25 @@ static hipError_t launch_flat(void* shard, int64_t rows, int32_t cols, const Bat
 }
 
 // The flat narrow-row kernel applies to plain sums of rows narrower than 4 KiB
-// (whole vectors, no speculation) when every push of the chunk lists at least
-// half the rows (dense pushes; sparse ones keep the pair-packed k_reduce_rows).
+// (whole vectors) when every push of the chunk lists at least half the rows
+// (dense pushes; sparse ones keep the pair-packed k_reduce_rows).
 bool use_flat(int vtype, int mode, int32_t cols, const Batch& bt, int nb, int64_t rows) {
     if (mode != kAdd && mode != kPreReduce) return false;
-    if (bt.spec) return false;
     const int VEC = vtype == kF64 ? 2 : 4;
     const int elem = vtype == kF64 ? 8 : 4;
     if (cols % VEC || (int64_t)cols * elem >= 4096 || nb <= 0) return false;
     for (int b = 0; b < nb; ++b)
         if (2 * bt.nrec[b] < rows) return false;
     return true;
+}
+
+// Identity speculation pays where the double-buffered reduce streams as fast as
+// the in-place one (measured): rows of whole 1-KiB chunks
+// (k_reduce_rows FULL) and the flat kernel's rows under 4 KiB.
+bool spec_shape(int vtype, int32_t cols) {
+    const int VEC = vtype == kF64 ? 2 : 4;
+    const int64_t bytes = (int64_t)cols * (vtype == kF64 ? 8 : 4);
+    return bytes % 1024 == 0 || (cols % VEC == 0 && bytes < 4096);
 }
 
 bool reduce_clears_slots(int vtype, int mode, int32_t cols) {

@@ -741,11 +741,10 @@ int run_batch(dml_store* s, const uint8_t* const* dptr, const int64_t* lens, int
             if (rc) { s->pend.clear(); return rc; }
         }
         if (s->err) return set_err(s->err, "store is in a failed state (see dml_store_error_state)");
-        // Identity speculation: plain-sum matrices whose rows are whole
-        // 1-KiB chunks (the double-buffered write of config 4's 800-B rows measured 7 %
-        // slower than its index; config 2's 4-KiB rows 0.4 % faster), when every push
-        // of the chunk is full-range (one record per row, no ragged tail).
-        if (s->is_matrix && reduce_mode(s) == kAdd && ((int64_t)s->cols * s->V) % 1024 == 0 &&
+        // Identity speculation: plain-sum matrices of the spec_shape
+        // widths, when every push of the chunk is full-range (one record per row, no
+        // ragged tail): no key index, the reduce verifies every record's key.
+        if (s->is_matrix && reduce_mode(s) == kAdd && spec_shape(vtype_of(s->desc), s->cols) &&
             c.tail_cut == kNoPos) {
             bool full = true;
             for (int j = 0; j < c.nb && full; ++j) full = c.bt.nrec[j] == s->rows && c.bt.len[j] == s->rows * s->stride;

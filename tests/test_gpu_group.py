@@ -114,6 +114,10 @@ def test_shard_group_hip_multiprocess(tmp_path, oracle, world, vt, rows, pieces,
     err_ref = float(np.max(np.abs(o.data.astype(np.float64) - exact) / terms))
     assert err_ours <= 1e-6, (err_ours, err_ref)
     assert err_ours <= err_ref + 2.0 ** -24, (err_ours, err_ref)
+    # element-wise reading where the sum does not cancel (|exact| >= sum|terms| / 4)
+    m = np.abs(exact) >= 0.25 * terms
+    el_ours = float(np.max(np.abs(got.astype(np.float64) - exact)[m] / np.abs(exact[m])))
+    assert m.sum() > rows * cols // 4 and el_ours <= 1e-6, (el_ours, int(m.sum()))
 
 
 # ---------------------------------------------------------------- exact exchange path

@@ -1196,8 +1196,12 @@ def _sampled_rows(oracle, b, rows):
     return ev | hs
 
 
+SPEC_SHAPES = [(256, 0, 1), (200, 0, 1), (100, 1, 3)]  # (cols, key type, value type)
+
+
+@pytest.mark.parametrize("shape", SPEC_SHAPES, ids=["c256-i32-f32", "c200-i32-f32-flat", "c100-i64-f64-flat"])
 @pytest.mark.parametrize("case", ["ascending", "swapped", "duplicate", "out_of_shard", "mixed_pipelined"])
-def test_identity_speculation_exact(oracle, case):
+def test_identity_speculation_exact(oracle, case, shape):
     """Identity speculation: full-range pushes whose sampled keys are
     ascending skip the key index; the reduce verifies every record's key and a
     chunk with a non-identity push re-runs exactly from its input buffer. Each case
@@ -1205,14 +1209,18 @@ def test_identity_speculation_exact(oracle, case):
     ascending push with two records swapped where the sample cannot see them; one
     with a row listed twice (and one missing: the repeated-row replay); one with an
     out-of-shard key (the cutoff: ArrayIndexOutOfBoundsException state); and
-    several pipelined batches mixing all of them with permuted pushes."""
+    several pipelined batches mixing all of them with permuted pushes. Shapes: whole
+    1-KiB rows (k_reduce_rows FULL) and rows under 4 KiB (k_reduce_flat), int32 and
+    int64 keys."""
     from distml_amd import DataDesc, DataStore, KeyRange, encode_matrix_push, ArrayIndexOutOfBoundsException
-    rows, cols, W = 4000, 256, 6
-    fmt = DataDesc(1, 0, 1)
+    cols, kt, vt = shape
+    rows, W = 4000, 6
+    fmt = DataDesc(1, kt, vt)
+    vdt = np.float64 if vt == 3 else np.float32
     rng = np.random.default_rng(hash(case) % 2**32)
     st = DataStore(fmt, KeyRange(100, 100 + rows - 1), cols, async_push=True)
     o = oracle_store(oracle, fmt, 100, 100 + rows - 1, cols)
-    init = rng.standard_normal((rows, cols)).astype(np.float32)
+    init = rng.standard_normal((rows, cols)).astype(vdt)
     st.load_values(init)
     o.data[:] = init
 
@@ -1231,8 +1239,8 @@ def test_identity_speculation_exact(oracle, case):
         elif kind == "out_of_shard":
             keys = keys.copy()
             keys[free[len(free) // 2]] = rows + 7  # key - first outside the shard
-        v = (rng.standard_normal((rows, cols)) * 1e-3).astype(np.float32)
-        return encode_matrix_push(keys + 100, v, 0, 1)
+        v = (rng.standard_normal((rows, cols)) * 1e-3).astype(vdt)
+        return encode_matrix_push(keys + 100, v, kt, vt)
 
     if case == "mixed_pipelined":
         kinds = [["ascending"] * W, ["ascending", "permuted"] * 3, ["ascending", "swapped"] + ["ascending"] * 4,

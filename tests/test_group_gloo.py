@@ -153,3 +153,8 @@ def test_sharded_full_range_push_gloo(tmp_path, oracle, world, vt):
     err_ref = float(np.max(np.abs(o.data.astype(np.float64) - exact) / terms))
     assert err_ours <= 1e-6, (err_ours, err_ref)
     assert err_ours <= err_ref + 2.0 ** -24, (err_ours, err_ref)
+    # element-wise reading of the same bound, where the sum does not cancel
+    # (|exact| >= sum|terms| / 4): relative to each element's own exact value
+    m = np.abs(exact) >= 0.25 * terms
+    el_ours = float(np.max(np.abs(got.astype(np.float64) - exact)[m] / np.abs(exact[m])))
+    assert m.sum() > rows * cols // 4 and el_ours <= 1e-6, (el_ours, int(m.sum()))
