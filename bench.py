@@ -412,7 +412,9 @@ def sparse_leg(ctx: Ctx, L, steps: int, cpu: bool):
     out = {"workload": "config3: 1e9-dim fp32 array shard, 32 pushes x 1e6 unique int64 keys, ordered scatter-add",
            "value": round(steps * algo / el / 2**30, 2), "unit": "GiB/s (algorithmic)", "steps": steps,
            "ms_per_step": round(el / steps * 1e3, 3), "algorithmic_bytes_per_step": algo,
-           "apply_kernel_us_avg": round(k_ms / max(k_n, 1) * 1e3, 2), "apply_launches": k_n}
+           "apply_kernel_us_avg": round(k_ms / max(k_n, 1) * 1e3, 2), "apply_launches": k_n,
+           # PMC HBM bytes per dispatch (profiles/pmc_traffic.json): leaf RMW and the two partition passes
+           "traffic": {k: load_traffic(k) for k in ("sparse", "sparse_l1", "sparse_l2")}}
     store.close()
     del bufs
     torch.cuda.empty_cache()
@@ -509,7 +511,7 @@ def leg_config4(ctx: Ctx, L, args) -> dict:
         k_s = k_ms / k_n / 1e3
         out["roofline"] = {"bound": "hbm", "achieved": round(algo / k_s / 1e9, 1), "peak": HBM_PEAK_GBS,
                            "unit": "GB/s", "frac": round(algo / k_s / 1e9 / HBM_PEAK_GBS, 4),
-                           "traffic": None, "kernel": "k_reduce_rows<float,kAdd> (200-col rows)",
+                           "traffic": load_traffic("leg4"), "kernel": "k_reduce_rows<float,kAdd> (200-col rows)",
                            "avg_kernel_us": round(k_s * 1e6, 1), "launches": k_n}
     elif pre_n:
         out["roofline"] = prereduce_roofline(L, ctx, args.pieces, pre_ms, pre_n,
@@ -591,7 +593,8 @@ def leg_config5(ctx: Ctx, L, args) -> dict:
     if k_n:
         k_s = k_ms / k_n / 1e3
         out["roofline"] = {"bound": "hbm", "achieved": round(algo / k_s / 1e9, 1), "peak": HBM_PEAK_GBS,
-                           "unit": "GB/s", "frac": round(algo / k_s / 1e9 / HBM_PEAK_GBS, 4), "traffic": None,
+                           "unit": "GB/s", "frac": round(algo / k_s / 1e9 / HBM_PEAK_GBS, 4),
+                           "traffic": load_traffic("leg5") if world == 1 else None,
                            "kernel": f"k_reduce_rows<int,kAddCheckI32> (rank {rank})",
                            "avg_kernel_us": round(k_s * 1e6, 1), "launches": k_n}
     store.close()
@@ -733,7 +736,7 @@ def run_shard_config(which: str, cpu_s: float, no_cpu: bool) -> dict:
             "roofline": {"bound": "hbm", "achieved": round(algo / k_s / 1e9, 1) if k_n else None,
                          "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": round(algo / k_s / 1e9 / HBM_PEAK_GBS, 4) if k_n else None,
-                         "kernel_us_avg": round(k_s * 1e6, 1), "traffic": load_traffic(which)}}
+                         "kernel_us_avg": round(k_s * 1e6, 1), "traffic": load_traffic("cfg" + which)}}
     if not no_cpu:
         line["cpu_baseline"] = shard_cpu_baseline(c, cpu_s)
     return line

@@ -1084,7 +1084,15 @@ static hipError_t launch_auto(void* shard, int64_t rows, int32_t cols, const Bat
 #define DML_LFN(G, CPW, RPW) launch_reduce_t<T, MODE, G, true, 4, 1, CPW, RPW, true>(shard, rows, cols, bt, nb, \
                                                      stride, K, slot, rowflag, ctrl, tail_cut, ada, st, nblocks_out, ev, rm, 0)
         if (MODE != kPreReduce) {
-            if (nchunks >= 4) return DML_LN(3, 4, 4);
+            // Rows of >= 4 chunks that do not fill them (config 5's 4000-B int32 rows in
+            // 4004-B records): cached record loads (the line two neighbouring records
+            // share is fetched once) and 2-wave blocks (a finished block frees its slot
+            // sooner): config 5 428 -> 400 us, 0.565 -> 0.604 of peak, measured against
+            // nt loads, 1/4/8-wave blocks, CPW 1/2, RPW 2, cached stores.
+            if (nchunks >= 4)
+                return launch_reduce_t<T, MODE, 3, false, 2, 1, 4, 4>(shard, rows, cols, bt, nb, stride, K, slot,
+                                                                     rowflag, ctrl, tail_cut, ada, st, nblocks_out,
+                                                                     ev, rm);
             if (cols % (64 * VEC * 2) == 0) return DML_LFN(1, 2, 4);
             if (nchunks >= 2) return DML_LN(3, 2, 4);
             if (cols % (64 * VEC) == 0) return DML_LFN(1, 1, 4);
@@ -1125,7 +1133,8 @@ static hipError_t launch_flat_t(void* shard, int64_t rows, int32_t cols, const B
 
 // JMAX 8 vectors per lane (R = 10 rows at 200 columns), one push per round:
 // measured within 2 % of 4 x 1, 4 x 2, 8 x 2 and 4 x 4 (config 4, ascending
-// and permuted), and of occupancy caps at 1-3 blocks per CU (all slower).
+// and permuted), and of occupancy caps at 1-3 blocks per CU (all slower);
+// nt record loads 2-3 % faster than cached ones.
 template <typename T, int MODE>
 static hipError_t launch_flat(void* shard, int64_t rows, int32_t cols, const Batch& bt, int nb, int64_t stride, int K,
                               const int32_t* slot, const uint32_t* rowflag, Ctrl* ctrl, uint64_t tail_cut,
