@@ -17,6 +17,10 @@ Legs reported in the same JSON line (same N, same process group):
              W full-range pushes per GPU ([int32][200 x f32] = 804 B records);
              N=1 one store, N>1 linearSplit + pre-reduce + reduce-scatter
              (weak scaling: W pushes per GPU at every N).
+  "config4_ada": config 4's AdaGrad variant (FloatMatrixStoreAdaGrad, 10M x 200:
+             data + alpha + delta), W full-range pushes per GPU through the exact
+             exchange path (split by owner, all-to-all, ordered owner apply; the
+             reduce-scatter cannot reproduce AdaGrad's per-push updates).
   "config5": BASELINE config 5, LDA IntMatrixStore 1M x 1000 int32 (4 GB),
              32 pushes of 65 536 distinct vocabulary rows, split per shard the
              way the reference's client splits them (SparseMatrix.java:46-60),
@@ -526,6 +530,69 @@ def leg_config4(ctx: Ctx, L, args) -> dict:
     return out
 
 
+# ---------------------------------------------------------------- config 4, AdaGrad (model level)
+def leg_config4_ada(ctx: Ctx, L, args) -> dict:
+    """Config 4's AdaGrad store (FloatMatrixStoreAdaGrad.java:239-284) at N GPUs:
+    rows linearSplit(N); every rank holds W full-range ascending pushes of the 10M x
+    200 model; a step = ShardGroup.push_exchange (dml_shard_split by owner, RCCL
+    all-to-all, every owner applies the N x W slices in rank-major push order with
+    the exact AdaGrad reduce). Weak scaling (W pushes per GPU). Algorithmic bytes
+    per rank: its push bytes + the shard's data/alpha/delta read and written."""
+    torch = ctx.torch
+    from distml_amd import DataDesc
+    from distml_amd.group import ShardGroup
+    world, rank = ctx.world, ctx.rank
+    rows, cols, w = C4_ROWS, C4_COLS, args.c4a_pushes
+    rec = 4 + 4 * cols
+    fmt = DataDesc(DataDesc.DATA_TYPE_MATRIX, DataDesc.KEY_TYPE_INT, DataDesc.ELEMENT_TYPE_FLOAT, False, True, True)
+    st = torch.cuda.current_stream().cuda_stream
+    bufs = []
+    for b in range(w):
+        t = torch.empty(rows * rec, dtype=torch.uint8, device="cuda")
+        assert L.dml_synth_dense_bucket(t.data_ptr(), C.byref(fmt.to_c()), 0, rows, rows, cols, 5000 + 64 * rank + b,
+                                        1, 0, C.c_void_p(st)) == 0
+        bufs.append(t)
+    torch.cuda.synchronize()
+    ptrs, lens = [b.data_ptr() for b in bufs], [b.numel() for b in bufs]
+    group = ShardGroup(fmt, rows, cols, rank, world, device=ctx.local, exchange_only=True)
+    store = group.store
+    store.setAlpha(0.025, 0.0001, 1.0)
+    store.synth_fill(13)
+
+    def step():
+        group.push_exchange(ptrs, lens)
+
+    for _ in range(args.c4a_warmup):
+        step()
+    group.flush()
+    store.set_timing(True)
+    el = timed_steps(ctx, step, group.flush, args.c4a_steps, 0, reset=lambda: store.kernel_time(reset=True))
+    k_ms, k_n = store.kernel_time(reset=True)
+    store.set_timing(False)
+    S = group.shard.size()
+    algo = w * rows * rec + 2 * 3 * S * cols * 4
+    out = {"workload": f"config4 AdaGrad: FloatMatrixStoreAdaGrad {rows}x{cols} fp32 (data + alpha + delta), {w} "
+                       f"full-range pushes per GPU (rows ascending), exact exchange path",
+           "value": round(algo * world * args.c4a_steps / el / 2**30, 2), "unit": "GiB/s", "n_gpus": world,
+           "pushes_per_gpu": w, "steps": args.c4a_steps, "ms_per_step": round(el / args.c4a_steps * 1e3, 3),
+           "scaling": "weak", "dtype": "f32",
+           "parallelism": "single shard (local exchange)" if world == 1 else
+                          f"linearSplit({world}) + dml_shard_split + RCCL all-to-all + ordered owner apply",
+           "algorithmic_bytes_per_step_per_gpu": algo}
+    if k_n:
+        k_s = k_ms / k_n / 1e3
+        owner = world * w * S * rec + 2 * 3 * S * cols * 4  # one owner launch: every rank's slices + state RMW
+        out["roofline"] = {"bound": "hbm", "achieved": round(owner / k_s / 1e9, 1), "peak": HBM_PEAK_GBS,
+                           "unit": "GB/s", "frac": round(owner / k_s / 1e9 / HBM_PEAK_GBS, 4), "traffic": None,
+                           "kernel": f"k_reduce<float,kAdaGrad> + maxDelta, owner apply (rank {rank})",
+                           "avg_kernel_us": round(k_s * 1e6, 1), "launches": k_n}
+    group.close()
+    del bufs, ptrs
+    torch.cuda.synchronize()
+    torch.cuda.empty_cache()
+    return out
+
+
 # ---------------------------------------------------------------- config 5 (model level)
 def leg_config5(ctx: Ctx, L, args) -> dict:
     """BASELINE config 5: LDA word-topic counts, IntMatrixStore 1M x 1000 int32,
@@ -773,12 +840,15 @@ def main():
     ap.add_argument("--pieces", type=int, default=4, help="pre-reduce row slices per call (sharded path)")
     ap.add_argument("--group", action="store_true",
                     help="use the sharded pre-reduce/reduce-scatter path even at N=1 (path check)")
-    ap.add_argument("--legs", default="4,5", help="model-level config legs in the line ('' = none)")
+    ap.add_argument("--legs", default="4,5,4a", help="model-level config legs in the line (4, 5, 4a; '' = none)")
     ap.add_argument("--c4-pushes", type=int, default=16, help="config-4 full-range pushes per GPU (8.04 GB each)")
     ap.add_argument("--c4-order", choices=["asc", "perm"], default="asc",
                     help="config-4 row order per push: ascending (SURVEY §8d, keys implicit = row) or permuted")
     ap.add_argument("--c4-steps", type=int, default=5)
     ap.add_argument("--c4-warmup", type=int, default=2)
+    ap.add_argument("--c4a-pushes", type=int, default=2, help="config-4 AdaGrad full-range pushes per GPU")
+    ap.add_argument("--c4a-steps", type=int, default=3)
+    ap.add_argument("--c4a-warmup", type=int, default=1)
     ap.add_argument("--c5-steps", type=int, default=20)
     ap.add_argument("--c5-warmup", type=int, default=4)
     ap.add_argument("--config", choices=["2", "4", "4-perm", "4-32", "4-256", "4-ada", "5"], default="2",
@@ -826,6 +896,8 @@ def main():
         line["config4"] = leg_config4(ctx, L, args)
     if "5" in legs:
         line["config5"] = leg_config5(ctx, L, args)
+    if "4a" in legs:
+        line["config4_ada"] = leg_config4_ada(ctx, L, args)
     if world == 1 and not args.group and args.sparse_steps > 0:
         line["sparse"] = sparse_leg(ctx, L, args.sparse_steps, cpu=not args.no_cpu)
     if rank == 0 and world == 1 and not args.no_cpu and not args.group:

@@ -90,7 +90,7 @@ class HipOps:
 class ShardGroup:
     def __init__(self, fmt: DataDesc, total_rows: int, cols: int, rank: int, world: int,
                  device: Optional[int] = None, ops=None, store_factory=None, pieces: int = 4,
-                 reduce_scatter=None):
+                 reduce_scatter=None, exchange_only: bool = False):
         import torch
         import torch.distributed as dist
         self.torch, self.dist = torch, dist
@@ -108,8 +108,11 @@ class ShardGroup:
         self.store = (store_factory or (lambda: DataStore(fmt, self.shard, cols, device=device)))()
         self.dtype = {0: torch.int32, 1: torch.float32, 3: torch.float64}[fmt.valueType]
         dev = torch.device("cuda", device) if device is not None else torch.device("cpu")
-        self.partial = torch.empty(world * self.step_rows * cols, dtype=self.dtype, device=dev)
-        self.recv = torch.empty(self.step_rows * cols, dtype=self.dtype, device=dev)
+        # exchange_only: a group that only runs push_exchange / push_local (AdaGrad,
+        # int32 with intermediate checks) holds no full-model partial buffers
+        self.exchange_only = exchange_only
+        self.partial = torch.empty(0 if exchange_only else world * self.step_rows * cols, dtype=self.dtype, device=dev)
+        self.recv = torch.empty(0 if exchange_only else self.step_rows * cols, dtype=self.dtype, device=dev)
         # pipelining of the full-range path: P row slices, reduce-scattered on a comm stream;
         # calls alternate between two partial/recv buffer sets so call k+1's key index
         # (side stream) and pre-reduce overlap call k's reduce-scatter and apply
@@ -147,6 +150,8 @@ class ShardGroup:
     def push_full_range(self, dev_ptrs: Sequence[int], lens: Sequence[int], stream: int = 0) -> None:
         """Ordered local pre-reduce -> reduce-scatter -> owner apply (see module doc)."""
         torch = self.torch
+        if self.exchange_only:
+            raise RuntimeError("push_full_range on an exchange_only ShardGroup (no partial buffers)")
         if getattr(self, "_held", None) is not None:  # an exchange call's slices come first (call order)
             if self.partial.is_cuda:
                 torch.cuda.current_stream(self.partial.device).synchronize()

@@ -152,7 +152,7 @@ def _xworker(rank, world, port, vt, out_dir):
     torch.cuda.set_device(0)
     dist.init_process_group("gloo", rank=rank, world_size=world)
     fmt = DataDesc(1, 0, vt, False, True, vt == 1)
-    g = ShardGroup(fmt, XR, XC, rank, world, device=0)
+    g = ShardGroup(fmt, XR, XC, rank, world, device=0, exchange_only=(world == 3))  # no partial buffers
     sh = g.shard
     g.store.load_values(_init(vt, XR, XC)[sh.firstKey:sh.lastKey + 1])
     if vt == 1:

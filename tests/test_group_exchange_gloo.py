@@ -114,7 +114,9 @@ def _worker(rank, world, port, vt, out_dir):
             holder["g"] = self
             super().__init__(*a, **k)
 
-    g = G(fmt, ROWS, COLS, rank, world, device=None, ops=SplitOps(), store_factory=factory)
+    g = G(fmt, ROWS, COLS, rank, world, device=None, ops=SplitOps(), store_factory=factory, exchange_only=True)
+    with pytest.raises(RuntimeError):
+        g.push_full_range([], [])  # an exchange-only group holds no partial buffers
     for call in range(CALLS):
         bufs = [torch.from_numpy(b) for b in _buckets(vt, rank, call)]
         g.push_exchange([b.data_ptr() for b in bufs], [b.numel() for b in bufs])
