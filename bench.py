@@ -515,7 +515,8 @@ def leg_config4(ctx: Ctx, L, args) -> dict:
         k_s = k_ms / k_n / 1e3
         out["roofline"] = {"bound": "hbm", "achieved": round(algo / k_s / 1e9, 1), "peak": HBM_PEAK_GBS,
                            "unit": "GB/s", "frac": round(algo / k_s / 1e9 / HBM_PEAK_GBS, 4),
-                           "traffic": load_traffic("leg4"), "kernel": "k_reduce_rows<float,kAdd> (200-col rows)",
+                           "traffic": load_traffic("leg4"),
+                           "kernel": "k_reduce_flat<float,kAdd> (200-col rows, identity-speculative: no key index)",
                            "avg_kernel_us": round(k_s * 1e6, 1), "launches": k_n}
     elif pre_n:
         out["roofline"] = prereduce_roofline(L, ctx, args.pieces, pre_ms, pre_n,
