@@ -342,7 +342,7 @@ def headline(ctx: Ctx, L, args, out_line: dict):
         out_line["roofline"] = {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS,
                                 "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4),
                                 "traffic": load_traffic("config2"),
-                                "kernel": "k_reduce_rows<float,kAdd> (2 rows x 4 KiB per wave)",
+                                "kernel": "k_reduce_rows<float,kAdd> (4 rows x 4 KiB per wave)",
                                 "avg_kernel_us": round(avg_s * 1e6, 2), "launches": k_n,
                                 "measured_read_peak": round(pk["read"], 1),
                                 "frac_of_measured_read": round(achieved / pk["read"], 4),

@@ -1071,10 +1071,11 @@ static hipError_t launch_auto(void* shard, int64_t rows, int32_t cols, const Bat
         return DML_L(8, 1, 1);
     } else {
         if (cols < VEC) return DML_L(16, 1, 1);  // narrower than one vector: k_reduce's generic path
-        // whole 4-KiB rows: two rows per wave and at most 8 waves per CU (64 KiB of
-        // loads in flight per CU) measured 3.5-5 % faster than 4 rows per wave at the
-        // register-limited 12-24 waves
-        if (cols % (64 * VEC * 4) == 0) return DML_LF(1, 4, 2, 2);
+        // whole 4-KiB rows: four rows per wave and at most 8 waves per CU (128 KiB of
+        // loads in flight per CU): config 2 355.7-358.3 us against 362.6-367.7 us for
+        // two rows at 8 waves, 381 us for four rows uncapped or at 12 waves, 367 us at
+        // 6 waves; 1-wave blocks at 8 per CU equal
+        if (cols % (64 * VEC * 4) == 0) return DML_LF(1, 4, 4, 2);
         // Other widths: pair-packed load groups (DEPTH 3) over 4 rows per wave.
         // Non-temporal shard stores (the rows are written once per batch): config 5
         // 460 -> 433 us; config 2's FULL shape measured no gain. Pre-reduce partials
