@@ -1000,6 +1000,195 @@ __global__ __launch_bounds__(256) void k_reduce_flat(T* __restrict__ shard, int6
     if (MODE == kAdd && bad) ctrl->spec_ok = 0u;  // an identity push is not: the host re-runs the chunk
 }
 
+// k_ada_flat: FloatMatrixStoreAdaGrad's push (FloatMatrixStoreAdaGrad.java:262-277)
+// in k_reduce_flat's layout, for rows narrower than 4 KiB whose pushes list most
+// rows (config 4's AdaGrad variant: 800-B rows). k_reduce gives such a row one
+// wave with 50 of 64 lanes busy and a few KiB of traffic — 10 M short waves per
+// batch; here a wave owns R neighbouring rows as one flat run of 16-B vectors
+// (JMAX per lane) and keeps, per element, data, delta, the last delta above 1
+// (alpha at write-back) and the last strict rise of delta (its maxDelta
+// candidate, with the push that made it; the position is rebuilt from the slot
+// rows in LDS at the end). Same per-element arithmetic and order as k_reduce, so
+// the results (data, alpha, delta, maxDelta/row/col) are the same bit for bit.
+template <int JMAX, int PB>
+__global__ __launch_bounds__(256) void k_ada_flat(float* __restrict__ shard, int64_t rows, int32_t cols, int32_t R,
+                                                  const Batch bt, int nb, int64_t stride, int K,
+                                                  int32_t* __restrict__ slot, const uint32_t* __restrict__ rowflag,
+                                                  Ctrl* __restrict__ ctrl, uint64_t tail_cut, AdaArgs ada) {
+    constexpr int VEC = 4;
+    constexpr int RMAX = 16;
+    __shared__ int32_t s_slot[4][RMAX * kMaxW];  // per wave: [row][push], -1 = no record / skipped row
+    const int lane = threadIdx.x & 63;
+    const int wid = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    const int64_t t0 = ((int64_t)blockIdx.x * 4 + wid) * R;  // first row of the wave
+    float cand_v = 0.f;
+    uint64_t cand_p = kNoPos;
+    bool cand_ok = false;
+    if (t0 < rows && !(bt.prev && ctrl_abnormal(bt.prev))) do {
+        const int NV = cols / VEC;
+        const int nrow = (int)(rows - t0 < (int64_t)R ? rows - t0 : (int64_t)R);
+        const int ss = slot_stride(nb);
+        int32_t* const ls = s_slot[wid];
+        // the wave's slot rows into LDS, handed back clean (-1) for the next batch;
+        // rows a push repeats stay -1 here (the host replays them exactly)
+        for (int e = lane; e < nrow * nb; e += 64) {
+            const int rl = e / nb, b = e - rl * nb;
+            const int64_t r = t0 + rl;
+            int32_t v = -1;
+            if (!(rowflag && rowflag[r])) {
+                v = slot[r * ss + b];
+                slot[r * ss + b] = -1;
+            }
+            ls[rl * kMaxW + b] = v;
+        }
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+        __builtin_amdgcn_wave_barrier();
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+
+        int rc[JMAX];  // (row << 16 | vector within the row)
+        uint32_t on = 0, tch = 0;
+        float acc[JMAX][VEC], dl[JMAX][VEC], lg[JMAX][VEC], rv[JMAX][VEC];
+        int rb[JMAX][VEC];  // chunk push index of the element's last strict rise (-1: none)
+        const int nvec = nrow * NV;
+#pragma unroll
+        for (int j = 0; j < JMAX; ++j) {
+            const int v = j * 64 + lane;
+            const int rlj = v < nvec ? v / NV : 0;
+            const int cvj = v < nvec ? v - rlj * NV : 0;
+            rc[j] = (rlj << 16) | cvj;
+            const int64_t ei = (t0 + rlj) * (int64_t)cols + cvj * VEC;
+            const bool o = v < nvec && !(rowflag && rowflag[t0 + rlj]);
+            on |= (o ? 1u : 0u) << j;
+            if (o) {
+                unpack<float>(ldg16_nt((const uint8_t*)(shard + ei)), acc[j]);
+                unpack<float>(ldg16_nt((const uint8_t*)(ada.delta + ei)), dl[j]);
+            } else {
+#pragma unroll
+                for (int e = 0; e < VEC; ++e) acc[j][e] = dl[j][e] = 0.f;
+            }
+#pragma unroll
+            for (int e = 0; e < VEC; ++e) {
+                lg[j][e] = 0.f;
+                rv[j][e] = 0.f;
+                rb[j][e] = -1;
+            }
+        }
+        // one contribution u of push b to element (j, e): k_reduce's apply()
+        auto upd = [&](int j, int e, float u, int b) {
+            acc[j][e] = __fadd_rn(acc[j][e], u);
+            const float nd = __fadd_rn(dl[j][e], __fmul_rn(u, u));
+            if (nd > dl[j][e]) { rv[j][e] = nd; rb[j][e] = b; }
+            if (nd > 1.0f) lg[j][e] = nd;
+            dl[j][e] = nd;
+        };
+        uint64_t cut = ctrl->cutoff;
+        if (tail_cut < cut) cut = tail_cut;
+        if (cut != kNoPos) {
+            // error batch: element by element, pushes in order, up to the cutoff byte
+            const int cut_b = (int)(cut >> 40);
+            const uint64_t cut_off = cut & kOffMask;
+            // j and e unrolled: the per-element state stays in registers (a runtime
+            // index would move the arrays to scratch for the whole kernel)
+#pragma unroll
+            for (int j = 0; j < JMAX; ++j) {
+                if (!(on >> j & 1u)) continue;
+                for (int b = 0; b < nb; ++b) {
+                    const int gb = bt.bidx[b];
+                    if (gb > cut_b) break;
+                    const int32_t rr = ls[(rc[j] >> 16) * kMaxW + b];
+                    if (rr < 0) continue;
+#pragma unroll
+                    for (int e = 0; e < VEC; ++e) {
+                        const uint64_t off = (uint64_t)((int64_t)rr * stride + K +
+                                                        (int64_t)((rc[j] & 0xFFFF) * VEC + e) * 4);
+                        if (!(gb == cut_b && off >= cut_off)) {
+                            tch |= 1u << j;
+                            upd(j, e, Elem<float>::load(bt.base[b] + off), b);
+                        }
+                    }
+                }
+            }
+        } else {
+            // PB pushes per round: all their loads in flight, then applied push by push
+#pragma unroll 1
+            for (int b0 = 0; b0 < nb; b0 += PB) {
+                int32_t rr[PB][JMAX];
+                u32x4 raw[PB][JMAX];
+#pragma unroll
+                for (int q = 0; q < PB; ++q) {
+                    const int b = b0 + q < nb ? b0 + q : nb - 1;
+                    const uint8_t* const bp = bt.base[b];
+#pragma unroll
+                    for (int j = 0; j < JMAX; ++j) {
+                        rr[q][j] = (b0 + q < nb && (on >> j & 1u)) ? ls[(rc[j] >> 16) * kMaxW + b] : -1;
+                        const uint8_t* src =
+                            bp + (int64_t)(rr[q][j] >= 0 ? rr[q][j] : 0) * stride + K + (int64_t)(rc[j] & 0xFFFF) * 16;
+                        raw[q][j] = rr[q][j] >= 0 ? ldg16_nt(src) : u32x4{0u, 0u, 0u, 0u};
+                    }
+                }
+#pragma unroll
+                for (int q = 0; q < PB; ++q)
+#pragma unroll
+                    for (int j = 0; j < JMAX; ++j) {
+                        if (rr[q][j] < 0) continue;
+                        tch |= 1u << j;
+                        float u[VEC];
+                        unpack<float>(raw[q][j], u);
+#pragma unroll
+                        for (int e = 0; e < VEC; ++e) upd(j, e, u[e], b0 + q);
+                    }
+            }
+        }
+        // write-back of the touched vectors: data, delta, alpha where the last delta
+        // a push left above 1 sets it (FloatMatrixStoreAdaGrad.java:268-272), and
+        // this lane's maxDelta candidate
+#pragma unroll
+        for (int j = 0; j < JMAX; ++j) {
+            if (!(tch >> j & 1u)) continue;
+            const int rl = rc[j] >> 16, cv = rc[j] & 0xFFFF;
+            const int64_t ei = (t0 + rl) * (int64_t)cols + cv * VEC;
+            stg16_nt(shard + ei, pack<float>(acc[j]));
+            stg16_nt(ada.delta + ei, pack<float>(dl[j]));
+            float na[VEC];
+            bool all_a = true;
+#pragma unroll
+            for (int e = 0; e < VEC; ++e) {
+                na[e] = 0.f;
+                if (lg[j][e] > 1.0f) {
+                    na[e] = (float)((double)ada.initial_alpha / ((double)ada.factor * sqrt((double)lg[j][e])));
+                    if (na[e] < ada.min_alpha) na[e] = ada.min_alpha;
+                } else {
+                    all_a = false;
+                }
+            }
+            if (all_a) stg16_nt(ada.alpha + ei, pack<float>(na));
+#pragma unroll
+            for (int e = 0; e < VEC; ++e) {
+                if (!all_a && lg[j][e] > 1.0f) ada.alpha[ei + e] = na[e];
+                if (rb[j][e] >= 0) {
+                    const int b = rb[j][e];
+                    const int32_t rr = ls[rl * kMaxW + b];
+                    const uint64_t p = pos_of((uint64_t)bt.bidx[b],
+                                              (uint64_t)((int64_t)rr * stride + K + (int64_t)(cv * VEC + e) * 4));
+                    if (!cand_ok || rv[j][e] > cand_v || (rv[j][e] == cand_v && p < cand_p)) {
+                        cand_ok = true;
+                        cand_v = rv[j][e];
+                        cand_p = p;
+                    }
+                }
+            }
+        }
+    } while (0);
+    cand_block_best<4>(cand_ok, cand_v, cand_p);
+    if (threadIdx.x == 0) {
+        DeltaCand c;
+        c.value = cand_v;
+        c.valid = cand_ok;
+        c.pos = cand_p;
+        ada.cand[blockIdx.x] = c;
+    }
+}
+
 // Occupancy cap: dynamic LDS (unused by the kernels) so that at most `bpc`
 // 256-thread blocks fit on a CU (160 KiB of LDS per CU). 0 = no cap.
 constexpr unsigned kLdsPerCU = 160 * 1024;
@@ -1144,11 +1333,12 @@ static hipError_t launch_flat(void* shard, int64_t rows, int32_t cols, const Bat
                                         nblocks_out, ev, rm);
 }
 
-// The flat narrow-row kernel applies to plain sums of rows narrower than 4 KiB
-// (whole vectors) when every push of the chunk lists at least half the rows
-// (dense pushes; sparse ones keep the pair-packed k_reduce_rows).
+// The flat narrow-row kernels apply to plain sums (and AdaGrad chunks of at most 4
+// pushes) of rows narrower than 4 KiB (whole vectors) when every push of the chunk
+// lists at least half the rows (dense pushes; sparse ones keep the pair-packed
+// k_reduce_rows / k_reduce).
 bool use_flat(int vtype, int mode, int32_t cols, const Batch& bt, int nb, int64_t rows) {
-    if (mode != kAdd && mode != kPreReduce) return false;
+    if (mode != kAdd && mode != kPreReduce && !(mode == kAdaGrad && vtype == kF32 && nb <= 4)) return false;
     const int VEC = vtype == kF64 ? 2 : 4;
     const int elem = vtype == kF64 ? 8 : 4;
     if (cols % VEC || (int64_t)cols * elem >= 4096 || nb <= 0) return false;
@@ -1164,6 +1354,38 @@ bool spec_shape(int vtype, int32_t cols) {
     const int VEC = vtype == kF64 ? 2 : 4;
     const int64_t bytes = (int64_t)cols * (vtype == kF64 ? 8 : 4);
     return bytes % 1024 == 0 || (cols % VEC == 0 && bytes < 4096);
+}
+
+// k_ada_flat launch: R rows per wave (R = 5 at 200 columns).
+template <int JMAX, int PB>
+static hipError_t launch_ada_flat_t(void* shard, int64_t rows, int32_t cols, const Batch& bt, int nb, int64_t stride,
+                                    int K, const int32_t* slot, const uint32_t* rowflag, Ctrl* ctrl,
+                                    uint64_t tail_cut, const AdaArgs& ada, hipStream_t st, int64_t* nblocks_out,
+                                    LaunchEv ev) {
+    const int NV = cols / 4;
+    const int R = std::max(1, std::min(16, JMAX * 64 / NV));
+    const int64_t nblocks = ((rows + R - 1) / R + 3) / 4;
+    if (nblocks_out) *nblocks_out = nblocks;
+    if (nblocks <= 0) return hipSuccess;
+    if (ev.start || ev.stop)
+        hipExtLaunchKernelGGL((k_ada_flat<JMAX, PB>), dim3((unsigned)nblocks), dim3(256), 0, st, ev.start, ev.stop, 0,
+                              (float*)shard, rows, cols, R, bt, nb, stride, K, const_cast<int32_t*>(slot), rowflag,
+                              ctrl, tail_cut, ada);
+    else
+        hipLaunchKernelGGL((k_ada_flat<JMAX, PB>), dim3((unsigned)nblocks), dim3(256), 0, st, (float*)shard, rows, cols, R,
+                           bt, nb, stride, K, const_cast<int32_t*>(slot), rowflag, ctrl, tail_cut, ada);
+    return hipGetLastError();
+}
+
+// JMAX 4 vectors per lane (R = 5 rows at 200 columns), two pushes per round: for
+// chunks of at most 4 pushes (the exact exchange path's slices at low W) 17.3 ms
+// per 10 M-row config-4 AdaGrad apply of 2 pushes against 19.1 ms for k_reduce;
+// with 8 pushes k_reduce (8 pushes in flight per wave) stays ahead (2.6 vs 2.95 ms).
+static hipError_t launch_ada_flat(void* shard, int64_t rows, int32_t cols, const Batch& bt, int nb, int64_t stride,
+                                  int K, const int32_t* slot, const uint32_t* rowflag, Ctrl* ctrl, uint64_t tail_cut,
+                                  const AdaArgs& ada, hipStream_t st, int64_t* nblocks_out, LaunchEv ev) {
+    return launch_ada_flat_t<4, 2>(shard, rows, cols, bt, nb, stride, K, slot, rowflag, ctrl, tail_cut, ada, st,
+                                   nblocks_out, ev);
 }
 
 bool reduce_clears_slots(int vtype, int mode, int32_t cols) {
@@ -1188,6 +1410,10 @@ hipError_t launch_reduce(int vtype, int mode, void* shard, int64_t rows, int32_t
 #define DML_A(T, M) launch_auto<T, M>(shard, rows, cols, bt, nb, stride, K, slot, rowflag, ctrl, tail_cut, ada, st, nblocks_out, ev, rm)
 #define DML_F(T, M) launch_flat<T, M>(shard, rows, cols, bt, nb, stride, K, slot, rowflag, ctrl, tail_cut, st, nblocks_out, ev, rm)
     if (use_flat(vtype, mode, cols, bt, nb, rm.block ? rm.rows_total : rows)) {
+        if (mode == kAdaGrad)  // the AdaGrad store runs no row map (exchange path only)
+            return rm.block || rm.out ? hipErrorInvalidValue
+                                      : launch_ada_flat(shard, rows, cols, bt, nb, stride, K, slot, rowflag, ctrl,
+                                                        tail_cut, ada, st, nblocks_out, ev);
         if (vtype == kF32) return mode == kAdd ? DML_F(float, kAdd) : DML_F(float, kPreReduce);
         if (vtype == kI32) return mode == kAdd ? DML_F(int32_t, kAdd) : DML_F(int32_t, kPreReduce);
         if (vtype == kF64) return mode == kAdd ? DML_F(double, kAdd) : DML_F(double, kPreReduce);

@@ -119,6 +119,7 @@ class ShardGroup:
         self.pieces = pieces
         self._pending: list = []  # pre-reduce handles whose errors are not yet collected
         self._xbufs: list = []    # exchange receive buffers the store may still read: (event, recv, send)
+        self._xpool: list = []    # exchange buffers the store has passed: reused by the next calls
         self._held = None         # the last exchange call's slices, handed to the store next call / flush
         self._k = 0
         if self.partial.is_cuda:
@@ -247,7 +248,7 @@ class ShardGroup:
         stride = self.record_stride()
         dev = self.partial.device
         cap = int(sum(lens))
-        send = torch.empty(max(cap, 1), dtype=torch.uint8, device=dev)
+        send = self._xalloc(max(cap, 1), dev)
         st = torch.cuda.current_stream(dev).cuda_stream if send.is_cuda else 0
         counts = self.ops.split(self.fmt, self.cols, self.total_rows, world, list(dev_ptrs), list(lens),
                                 send.data_ptr(), cap, st) if n else []
@@ -269,14 +270,15 @@ class ShardGroup:
         send_sizes = [int(mine[d].sum()) * stride for d in range(world)]
         recv_sizes = [int(theirs[q].sum()) * stride for q in range(world)]
         nsend, nrecv = sum(send_sizes), sum(recv_sizes)
-        recv = torch.empty(max(nrecv, 1), dtype=torch.uint8, device=dev)
         if world == 1:
-            recv[:nrecv].copy_(send[:nsend])
+            recv = send  # the one owner: the split's owner-major layout is the receive layout
         elif host_a2a and send.is_cuda:
+            recv = self._xalloc(max(nrecv, 1), dev)
             hr = torch.empty(nrecv, dtype=torch.uint8)
             dist.all_to_all_single(hr, send[:nsend].cpu(), recv_sizes, send_sizes)
             recv[:nrecv].copy_(hr)
         else:
+            recv = self._xalloc(max(nrecv, 1), dev)
             dist.all_to_all_single(recv[:nrecv], send[:nsend], recv_sizes, send_sizes)
         ptrs, ls, off = [], [], 0
         for q in range(world):
@@ -305,11 +307,36 @@ class ShardGroup:
             return
         ev = self.torch.cuda.Event()
         ev.record(self._store_stream)
-        # keep the buffers until the store's stream has passed them
-        keep = [x for x in self._xbufs if not x[0].query()] + [(ev, recv, send)]
+        # keep the buffers until the store's stream has passed them; passed ones go back
+        # to the pool the next calls allocate from (no allocator churn on GB buffers)
+        keep = []
+        for x in self._xbufs:
+            if x[0].query():
+                self._xrelease(x[1], x[2])
+            else:
+                keep.append(x)
+        keep.append((ev, recv, send))
         while len(keep) > 3:  # bound the memory held for the asynchronous store
-            keep.pop(0)[0].synchronize()
+            x = keep.pop(0)
+            x[0].synchronize()
+            self._xrelease(x[1], x[2])
         self._xbufs = keep
+
+    def _xalloc(self, n: int, dev):
+        """An exchange buffer of at least n bytes: the smallest free pooled one, or new."""
+        fit = [t for t in self._xpool if t.numel() >= n]
+        if fit:
+            t = min(fit, key=lambda x: x.numel())
+            self._xpool.remove(t)
+            return t
+        return self.torch.empty(n, dtype=self.torch.uint8, device=dev)
+
+    def _xrelease(self, *bufs) -> None:
+        for t in bufs:
+            if all(t is not u for u in self._xpool):
+                self._xpool.append(t)
+        while len(self._xpool) > 4:  # keep the largest few
+            self._xpool.remove(min(self._xpool, key=lambda x: x.numel()))
 
     def push_local(self, dev_ptrs: Sequence[int], lens: Sequence[int]) -> None:
         """Pushes already split to this shard: exact ordered apply, no exchange."""
@@ -338,6 +365,7 @@ class ShardGroup:
         finally:
             self.store.flush()
             self._xbufs.clear()
+            self._xpool.clear()
 
     def close(self) -> None:
         """Flush, then release the shard store and the partial / receive buffers."""

@@ -1354,3 +1354,57 @@ def test_sparse_single_pass_partition_exact(oracle, case):
             s.handlePushBatch(fmt, pushes)
         assert (ei.value.code, ei.value.key) == (err[0], err[1])
     assert s.values().tobytes() == o.data.tobytes()
+
+
+@pytest.mark.parametrize("cols", [200, 64])
+@pytest.mark.parametrize("W", [1, 2, 4])
+@pytest.mark.parametrize("case", ["plain", "large", "cutoff", "repeat"])
+def test_adagrad_flat_exact(oracle, case, W, cols):
+    """k_ada_flat (AdaGrad chunks of <= 4 dense pushes, rows under 4 KiB)
+    bit-exact against the oracle: data, alpha, delta, maxDelta/row/col and error
+    state. `large`: gradients that drive delta past 1 (alpha written at write-back),
+    plus a NaN and an Inf element; `cutoff`: a key outside the shard in the middle of
+    the second push (ArrayIndexOutOfBoundsException state); `repeat`: the first push
+    lists a row twice (the host's exact replay layers, maxDelta finalized after them)."""
+    from distml_amd import DataDesc, DistMLException, encode_matrix_push
+    rng = np.random.default_rng(1000 * W + cols + len(case))
+    first, rows = 50, 3000
+    fmt = DataDesc(1, 0, 1, False, True, True)
+    s, _ = mk_store(fmt, first, first + rows - 1, cols)
+    o = oracle_store(oracle, fmt, first, first + rows - 1, cols)
+    s.setAlpha(0.025, 0.0001, 1.5)
+    o.set_alpha(0.025, 0.0001, 1.5)
+    init = rng.standard_normal((rows, cols)).astype(np.float32)
+    s.load_values(init)
+    o.data[:] = init
+    pushes = []
+    for b in range(W):
+        keys = rng.permutation(rows)
+        scale = 0.7 if case == "large" else 1e-2
+        v = (rng.standard_normal((rows, cols)) * scale).astype(np.float32)
+        if case == "large" and b == 0:
+            v[10, 3], v[11, 5] = np.nan, np.inf
+        if case == "repeat" and b == 0:
+            keys[100] = keys[200]
+        p = encode_matrix_push(keys + first, v, 0, 1)
+        if case == "cutoff" and b == min(1, W - 1):
+            rec = 4 + 4 * cols
+            bad = encode_matrix_push([first + rows + 9], np.ones((1, cols), np.float32), 0, 1)
+            p = p[:rec * 1500] + bad + p[rec * 1500:]
+        pushes.append(p)
+    err = None
+    for p in pushes:
+        if o.push(p):
+            err = o.error()
+            break
+    if err is None:
+        s.handlePushBatch(fmt, pushes)
+    else:
+        with pytest.raises(DistMLException):
+            s.handlePushBatch(fmt, pushes)
+        assert s.error_state() == (err[0], err[1], err[2])
+    assert kat.bits_equal(s.values(), o.data)
+    a, d = s.adagrad_state()
+    assert kat.bits_equal(a, o.alpha) and kat.bits_equal(d, o.delta)
+    assert s.maxDelta() == o.max_delta()
+    s.close()
