@@ -121,9 +121,13 @@ class Ctx:
     def max(self, x: float) -> float:
         if self.world == 1:
             return x
-        t = self.torch.tensor([x], dtype=self.torch.float64, device="cuda")
+        t = self.torch.tensor([x], dtype=self.torch.float64, device=self.coll_device())
         self.dist.all_reduce(t, op=self.dist.ReduceOp.MAX)
         return float(t.item())
+
+    def coll_device(self) -> str:
+        """Device of small collective tensors: the GPU under RCCL, the host under gloo."""
+        return "cpu" if self.dist.get_backend() == "gloo" else "cuda"
 
 
 def timed_steps(ctx: Ctx, step, finish, steps: int, warmup: int, ramp_s: float = 0.0, reset=None) -> float:
@@ -653,7 +657,7 @@ def leg_config5(ctx: Ctx, L, args) -> dict:
     algo = C5_W * nrec * rec + 2 * 4 * cols * touched
     algo_all = algo
     if world > 1:
-        t = torch.tensor([float(algo)], dtype=torch.float64, device="cuda")
+        t = torch.tensor([float(algo)], dtype=torch.float64, device=ctx.coll_device())
         ctx.dist.all_reduce(t)
         algo_all = float(t.item())
     out = {"workload": f"config5: LDA IntMatrixStore {C5_ROWS}x{cols} int32 (negativity check), {C5_W} pushes x "
@@ -861,6 +865,9 @@ def main():
                     help="2 = the headline line (default); 4, 4-32, 4-ada, 5 = one GPU's shard of those configs")
     ap.add_argument("--cpu-seconds", type=float, default=8.0, help="CPU baseline budget for --config 4/5")
     ap.add_argument("--launcher-check", action="store_true", help=argparse.SUPPRESS)
+    # rehearsal of the N-rank legs on a one-GPU box: every rank on cuda:0, gloo collectives
+    # (RCCL refuses two ranks on one device); numbers from it are not measurements
+    ap.add_argument("--rehearse-gloo", action="store_true", help=argparse.SUPPRESS)
     args = ap.parse_args()
     if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
         sys.exit(launch_ranks(args.gpus, sys.argv[1:]))
@@ -885,8 +892,12 @@ def main():
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
     assert world == args.gpus, f"--gpus {args.gpus} but WORLD_SIZE={world}"
+    if args.rehearse_gloo:
+        local = 0
     torch.cuda.set_device(local)
-    if world > 1:
+    if world > 1 and args.rehearse_gloo:
+        dist.init_process_group("gloo")
+    elif world > 1:
         dist.init_process_group("nccl", device_id=torch.device("cuda", local))
     elif args.group:
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
