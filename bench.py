@@ -592,8 +592,10 @@ def leg_config4_ada(ctx: Ctx, L, args) -> dict:
         k_s = k_ms / k_n / 1e3
         owner = world * w * S * rec + 4 * S * cols * 4  # one owner launch: every rank's slices + data/delta RMW
         out["roofline"] = {"bound": "hbm", "achieved": round(owner / k_s / 1e9, 1), "peak": HBM_PEAK_GBS,
-                           "unit": "GB/s", "frac": round(owner / k_s / 1e9 / HBM_PEAK_GBS, 4), "traffic": None,
-                           "kernel": f"k_reduce<float,kAdaGrad> + maxDelta, owner apply (rank {rank})",
+                           "unit": "GB/s", "frac": round(owner / k_s / 1e9 / HBM_PEAK_GBS, 4),
+                           "traffic": load_traffic("leg4a") if world == 1 else None,
+                           "kernel": f"AdaGrad owner apply + maxDelta (k_ada_flat for <= 4 slices, else k_reduce; "
+                                     f"rank {rank})",
                            "avg_kernel_us": round(k_s * 1e6, 1), "launches": k_n}
     group.close()
     del bufs, ptrs
