@@ -335,7 +335,7 @@ class ShardGroup:
         for t in bufs:
             if all(t is not u for u in self._xpool):
                 self._xpool.append(t)
-        while len(self._xpool) > 4:  # keep the largest few
+        while len(self._xpool) > 2:  # keep the largest two (a send and a receive buffer)
             self._xpool.remove(min(self._xpool, key=lambda x: x.numel()))
 
     def push_local(self, dev_ptrs: Sequence[int], lens: Sequence[int]) -> None:
