@@ -820,9 +820,12 @@ def test_shard_split_rejects_partial_records():
         HipOps().split(DataDesc(1, 0, 1), 200, 100, 2, [d.data_ptr()], [805], d.data_ptr(), 805, 0)
 
 
-def test_exchange_rccl_world1_adagrad(oracle):
+@pytest.mark.parametrize("calls", [1, 4])
+def test_exchange_rccl_world1_adagrad(oracle, calls):
     """ShardGroup.push_exchange at world 1 over RCCL: dml_shard_split, the all-to-all
-    and the ordered AdaGrad apply; bit-exact (data, alpha, delta, maxDelta)."""
+    and the ordered AdaGrad apply; bit-exact (data, alpha, delta, maxDelta). With 4
+    calls of different sizes back to back (no flush between), the pooled send /
+    receive buffers are reused across calls of other sizes."""
     import socket
     import torch.distributed as dist
     from distml_amd import DataDesc, encode_matrix_push
@@ -836,7 +839,7 @@ def test_exchange_rccl_world1_adagrad(oracle):
     try:
         rows, cols, W = 3000, 200, 5
         fmt = DataDesc(1, 0, 1, False, True, True)
-        g = ShardGroup(fmt, rows, cols, 0, 1, device=0)
+        g = ShardGroup(fmt, rows, cols, 0, 1, device=0, exchange_only=calls > 1)
         g.store.setAlpha(0.025, 0.0001, 1.5)
         rng = np.random.default_rng(77)
         host = []
@@ -846,7 +849,9 @@ def test_exchange_rccl_world1_adagrad(oracle):
             host.append(encode_matrix_push(keys, vals, 0, 1))
         dev = [torch.frombuffer(bytearray(h), dtype=torch.uint8).cuda() for h in host]
         torch.cuda.synchronize()
-        g.push_exchange([d.data_ptr() for d in dev], [d.numel() for d in dev])
+        cuts = [0, W] if calls == 1 else [0, 1, 3, 4, W]
+        for c0, c1 in zip(cuts, cuts[1:]):
+            g.push_exchange([d.data_ptr() for d in dev[c0:c1]], [d.numel() for d in dev[c0:c1]])
         g.flush()
         o = oracle_store(oracle, fmt, 0, rows - 1, cols)
         o.set_alpha(0.025, 0.0001, 1.5)
