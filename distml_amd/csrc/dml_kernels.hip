@@ -603,10 +603,10 @@ __global__ __launch_bounds__(64 * WPB) void k_reduce_rows(T* __restrict__ shard,
         vslot[r] = ((live >> r & 1u) && lane < nb)
                        ? (lane_ident ? (row[r] < bt.nrec[lane] ? (int32_t)row[r] : -1) : slot[row[r] * slot_stride(nb) + lane])
                        : -1;
-    if constexpr (MODE != kAddCheckI32) {
+    {
         // Hand the slot rows back as the next batch's index expects them (-1 = no
-        // record), so the host skips the slot-table memset (reduce_clears_slots). The
-        // int32-check mode keeps them: its rollback re-reads the table. Identity
+        // record), so the host skips the slot-table memset (reduce_clears_slots); the
+        // int32 rollback (rare) rebuilds the table with a second index. Identity
         // pushes never wrote theirs.
 #pragma unroll
         for (int r = 0; r < RPW; ++r)
@@ -1390,7 +1390,7 @@ static hipError_t launch_ada_flat(void* shard, int64_t rows, int32_t cols, const
 
 bool reduce_clears_slots(int vtype, int mode, int32_t cols) {
     if (mode == kAdaGrad) return vtype == kF32 && cols <= 64 * 4;  // k_reduce, one chunk group per row
-    if (mode != kAdd && mode != kPreReduce) return false;
+    if (mode != kAdd && mode != kPreReduce && mode != kAddCheckI32) return false;
     const int VEC = vtype == kF64 ? 2 : 4;
     if (cols < VEC) return false;  // k_reduce's generic path
     return true;

@@ -655,6 +655,11 @@ int retire_front(dml_store* s) {
         HIPCHK(sparse_replay(vtype_of(s->desc), s->data, c.sp, c.spl, W.sp, s->stream));
     } else if (ctl.neg_pos != kNoPos) {
         if (s->is_matrix) {
+            // the reduce handed its slot rows back clean: rebuild the table (no row
+            // repeats here, so the rowflags stay zero; the index leaves neg_pos alone)
+            HIPCHK(hipMemsetAsync(W.slot, 0xFF, s->slot_bytes, s->stream));
+            HIPCHK(launch_index(c.bt, c.nb, c.max_nrec, s->stride, s->K, s->first, s->rows, W.slot, W.rowflag, W.ctrl,
+                                c.tail_cut, s->stream));
             HIPCHK(launch_rollback_i32((int32_t*)s->data, s->rows, s->cols, c.bt, c.nb, s->stride, s->K, W.slot,
                                        W.rowflag, W.ctrl, c.tail_cut, s->stream));
         } else {
