@@ -849,7 +849,7 @@ def main():
     ap.add_argument("--no-cpu", action="store_true", help="skip the CPU baseline legs")
     ap.add_argument("--no-timing", action="store_true", help="no kernel timing events in the timed region")
     ap.add_argument("--sparse-steps", type=int, default=20, help="config-3 sparse leg steps (0 = skip; N=1 only)")
-    ap.add_argument("--pieces", type=int, default=4, help="pre-reduce row slices per call (sharded path)")
+    ap.add_argument("--pieces", type=int, default=1, help="pre-reduce row slices per call (sharded path)")
     ap.add_argument("--group", action="store_true",
                     help="use the sharded pre-reduce/reduce-scatter path even at N=1 (path check)")
     ap.add_argument("--legs", default="4,5,4a", help="model-level config legs in the line (4, 5, 4a; '' = none)")
