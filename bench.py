@@ -565,8 +565,12 @@ def leg_config4_ada(ctx: Ctx, L, args) -> dict:
     store.setAlpha(0.025, 0.0001, 1.0)
     store.synth_fill(13)
 
+    calls = []  # host time of each call (diagnostic: the split's counts and the exchange wait there)
+
     def step():
+        t = time.perf_counter()
         group.push_exchange(ptrs, lens)
+        calls.append(time.perf_counter() - t)
 
     for _ in range(args.c4a_warmup):
         step()
@@ -587,7 +591,8 @@ def leg_config4_ada(ctx: Ctx, L, args) -> dict:
            "scaling": "weak", "dtype": "f32",
            "parallelism": "single shard (local exchange)" if world == 1 else
                           f"linearSplit({world}) + dml_shard_split + RCCL all-to-all + ordered owner apply",
-           "algorithmic_bytes_per_step_per_gpu": algo}
+           "algorithmic_bytes_per_step_per_gpu": algo,
+           "host_ms_per_call": [round(x * 1e3, 2) for x in calls[-args.c4a_steps:]]}
     if k_n:
         k_s = k_ms / k_n / 1e3
         owner = world * w * S * rec + 4 * S * cols * 4  # one owner launch: every rank's slices + data/delta RMW
