@@ -532,7 +532,17 @@ def leg_config4(ctx: Ctx, L, args) -> dict:
     del bufs, ptrs
     torch.cuda.synchronize()
     torch.cuda.empty_cache()
+    if world == 1 and not args.no_cpu:
+        out["cpu_baseline"] = leg_cpu_baseline("4")
     return out
+
+
+def leg_cpu_baseline(which: str, budget_s: float = 3.0) -> dict:
+    """The oracle on one linearSplit(8) shard of the leg's workload (SURVEY §8(d):
+    configs 4 and 5 time one shard on the CPU; the whole model is 8 such shards)."""
+    b = shard_cpu_baseline(SHARD_CONFIGS[which], budget_s)
+    b["sample"] = "one 1/8 shard of the model (" + SHARD_CONFIGS[which]["name"] + "): " + b["sample"]
+    return b
 
 
 # ---------------------------------------------------------------- config 4, AdaGrad (model level)
@@ -684,6 +694,8 @@ def leg_config5(ctx: Ctx, L, args) -> dict:
     del pos, neg, sets
     torch.cuda.synchronize()
     torch.cuda.empty_cache()
+    if world == 1 and not args.no_cpu:
+        out["cpu_baseline"] = leg_cpu_baseline("5")
     return out
 
 
