@@ -877,7 +877,7 @@ def main():
     ap.add_argument("--c4-warmup", type=int, default=2)
     ap.add_argument("--c4a-pushes", type=int, default=2, help="config-4 AdaGrad full-range pushes per GPU")
     ap.add_argument("--c4a-steps", type=int, default=3)
-    ap.add_argument("--c4a-warmup", type=int, default=1)
+    ap.add_argument("--c4a-warmup", type=int, default=3, help="(the exchange buffer pool fills in the first calls)")
     ap.add_argument("--c5-steps", type=int, default=20)
     ap.add_argument("--c5-warmup", type=int, default=4)
     ap.add_argument("--config", choices=["2", "4", "4-perm", "4-32", "4-256", "4-ada", "5"], default="2",

@@ -327,6 +327,13 @@ class ShardGroup:
 
     def _xalloc(self, n: int, dev):
         """An exchange buffer of at least n bytes: the smallest free pooled one, or new."""
+        keep = []
+        for x in self._xbufs:  # buffers the store has passed since the last hand-over
+            if x[0].query():
+                self._xrelease(x[1], x[2])
+            else:
+                keep.append(x)
+        self._xbufs = keep
         fit = [t for t in self._xpool if t.numel() >= n]
         if fit:
             t = min(fit, key=lambda x: x.numel())
