@@ -179,8 +179,14 @@ struct SpPlan {
     // falls back to the counted partition before the leaf runs
     int64_t cap1, cap2, tiles2_per_bin;
     int fast;                      // the leaf reads the fixed-capacity layout
+    // compact records (fp32, single-pass, no cutoff): one 8-B word per record,
+    // row within its level-1 bin << 38 | chunk push << 32 | value bits; the push
+    // index orders a row's adds (a push listing a row twice sends its leaf to the
+    // exact replay, which re-partitions with full sequence numbers)
+    int compact;
     uint32_t seq_cut;              // records with sequence >= seq_cut are at / past the cutoff
 };
+constexpr int kSpCompactRowBits = 26;  // SL + D2 limit of the compact word
 // Pinned status of a single-pass partition, read by the host before the leaf launch.
 struct SpStat {
     unsigned int overflow;         // a bin or leaf exceeded its capacity
@@ -211,7 +217,11 @@ hipError_t launch_sparse_partition_fast(int vtype, const Batch& bt, const SpPlan
 uint32_t sparse_seq_cut(const SpPlan& pl, const Batch& bt, uint64_t cut, int64_t stride);
 hipError_t launch_sparse_leaf(int vtype, void* shard, const SpPlan& pl, const SpLayout& l, uint8_t* ws, Ctrl* ctrl,
                               const Ctrl* prev, hipStream_t st, LaunchEv ev);
-hipError_t sparse_replay(int vtype, void* shard, const SpPlan& pl, const SpLayout& l, uint8_t* ws, hipStream_t st);
+// Exact replay of the leaves the leaf kernel flagged. A compact chunk is first
+// re-partitioned (counted, full sequence numbers) from its pushes.
+hipError_t sparse_replay(int vtype, void* shard, const SpPlan& pl, const SpLayout& l, uint8_t* ws, const Batch& bt,
+                         int64_t stride, int K, int64_t first, int64_t rows, Ctrl* ctrl, uint64_t tail_cut,
+                         hipStream_t st);
 
 hipError_t launch_stream(bool copy, void* dst, const void* src, int64_t n16, hipStream_t st, LaunchEv ev);
 hipError_t launch_rand(int vtype, void* p, int64_t rows, int32_t cols, uint64_t s0, hipStream_t st);

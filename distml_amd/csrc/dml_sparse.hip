@@ -28,6 +28,7 @@
 #include <hipcub/hipcub.hpp>
 
 #include <algorithm>
+#include <type_traits>
 
 namespace dml {
 
@@ -86,10 +87,15 @@ struct SpStage {
     uint32_t gstart[256];  // global start of this tile's segment of each bin
     uint32_t wsum[4];
 };
+// Compact records (SpPlan::compact): the value travels inside the 8-B word.
+struct SpStageC {
+    uint64_t c[kSpTile];
+    uint32_t cnt[256], lstart[257], gstart[256], wsum[4];
+};
 
 // Exclusive scan of st.cnt[0..255] into st.lstart (256 threads), cnt := lstart.
-template <typename T>
-__device__ inline void sp_stage_scan(SpStage<T>& st) {
+template <typename S>
+__device__ inline void sp_stage_scan(S& st) {
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     const uint32_t a = st.cnt[tid];
     uint32_t x = a;
@@ -317,45 +323,59 @@ constexpr int kSpLeafThreads = 512;  // 8 waves per leaf
 constexpr int kSpLines = 2 * kSpLeafThreads;
 constexpr int kSpBucketMax = 64;
 
-// A repeated row's records in ascending comp (= sequence) order, added to x.
-template <typename T>
+// A leaf record's fields. Full records: comp = row << 32 | sequence (+ value in
+// val[]); compact records (CMP): row within the level-1 bin << 38 | push << 32 |
+// value bits, ordered within a row by push.
+template <bool CMP>
+struct LeafRec {
+    uint64_t rowb0;     // CMP: first row of the leaf's level-1 bin
+    uint32_t seq_cut;   // full records: sequences at / past it are never applied
+    __device__ uint64_t row(uint64_t c) const { return CMP ? rowb0 + (c >> 38) : c >> 32; }
+    __device__ uint64_t key(uint64_t c) const { return CMP ? c >> 32 : c; }  // add order within a row
+    __device__ bool applied(uint64_t c) const { return CMP || (uint32_t)c < seq_cut; }
+};
+
+// A repeated row's records in ascending key (= push / sequence) order, added to x.
+template <typename T, bool CMP>
 __device__ inline T leaf_chain(T x, uint64_t row, uint64_t row0, int bshift, const uint32_t* bstart,
-                               const uint16_t* perm, const uint64_t* sc, const T* sv, uint32_t seq_cut,
-                               bool started = false,
-                               uint64_t last = 0) {  // started: records up to comp `last` are in x
+                               const uint16_t* perm, const uint64_t* sc, const T* sv, const LeafRec<CMP>& lr) {
     const uint32_t b = (uint32_t)((row - row0) >> bshift);
     const uint32_t bs = bstart[b], be = bstart[b + 1];
+    bool started = false;
+    uint64_t last = 0;  // started: records up to key `last` are in x
     for (;;) {
         uint64_t best = ~0ull;
         int bj = -1;
         for (uint32_t q = bs; q < be; ++q) {
             const int j = perm[q];
-            const uint64_t cj = sc[j];
-            if ((cj >> 32) == row && (uint32_t)cj < seq_cut && (!started || cj > last) && cj < best) {
-                best = cj;
+            const uint64_t cj = sc[j], kj = lr.key(cj);
+            if (lr.row(cj) == row && lr.applied(cj) && (!started || kj > last) && kj < best) {
+                best = kj;
                 bj = j;
             }
         }
         if (bj < 0) break;
-        x = Elem<T>::add(x, sv[bj]);
+        if constexpr (CMP) x = Elem<T>::add(x, __uint_as_float((uint32_t)sc[bj]));
+        else x = Elem<T>::add(x, sv[bj]);
         last = best;
         started = true;
     }
     return x;
 }
 
-template <typename T>
+template <typename T, bool CMP>
 __global__ __launch_bounds__(kSpLeafThreads) void k_sp_leaf(T* __restrict__ shard, const int64_t* __restrict__ bounds,
                                                             const uint32_t* __restrict__ cnt2, int64_t cap2,
                                                             const uint64_t* __restrict__ comp,
-                                                            const T* __restrict__ val, int SL, int bshift,
+                                                            const T* __restrict__ val, int SL, int D2, int bshift,
                                                             uint32_t seq_cut, uint8_t* __restrict__ leafflag,
                                                             Ctrl* __restrict__ ctrl, const Ctrl* __restrict__ prev) {
     constexpr int kT = kSpLeafThreads;
     constexpr int kPer = kSpLeafCap / kT;
     static_assert(kSpLines == 2 * kT, "the scan gives each thread two buckets");
+    static_assert(!CMP || sizeof(T) == 4, "compact records carry fp32 values");
     __shared__ uint64_t sc[kSpLeafCap];
-    __shared__ T sv[kSpLeafCap];
+    __shared__ T sv[CMP ? 1 : kSpLeafCap];
     __shared__ uint16_t perm[kSpLeafCap];
     __shared__ uint32_t bstart[kSpLines + 1];
     __shared__ uint32_t cur[kSpLines];
@@ -379,6 +399,9 @@ __global__ __launch_bounds__(kSpLeafThreads) void k_sp_leaf(T* __restrict__ shar
         return;
     }
     const uint64_t row0 = (uint64_t)L << SL;
+    LeafRec<CMP> lr;
+    lr.rowb0 = (uint64_t)(L >> D2) << (SL + D2);
+    lr.seq_cut = seq_cut;
     for (int i = tid; i < kSpLines; i += kT) cur[i] = 0;
     if (tid == 0) s_over = 0;
     // loads from clamped in-range indices, all in flight before the first use
@@ -390,16 +413,17 @@ __global__ __launch_bounds__(kSpLeafThreads) void k_sp_leaf(T* __restrict__ shar
     for (int k = 0; k < kPer; ++k) {
         const int i = min(tid + k * kT, n - 1);
         c[k] = comp[lo + i];
-        u[k] = val[lo + i];
+        if constexpr (!CMP) u[k] = val[lo + i];
     }
     T x0[kPer];
 #pragma unroll
-    for (int k = 0; k < kPer; ++k) x0[k] = shard[c[k] >> 32];  // every comp row lies in this leaf
+    for (int k = 0; k < kPer; ++k) x0[k] = shard[lr.row(c[k])];  // every record's row lies in this leaf
 #pragma unroll
     for (int k = 0; k < kPer; ++k) {
         const int i = tid + k * kT;
-        bk[k] = (uint32_t)(((c[k] >> 32) - row0) >> bshift);
-        if (i < n) sv[i] = u[k];
+        bk[k] = (uint32_t)((lr.row(c[k]) - row0) >> bshift);
+        if constexpr (CMP) u[k] = __uint_as_float((uint32_t)c[k]);
+        else if (i < n) sv[i] = u[k];
     }
     __syncthreads();
 #pragma unroll
@@ -450,17 +474,22 @@ __global__ __launch_bounds__(kSpLeafThreads) void k_sp_leaf(T* __restrict__ shar
         if (p >= n) continue;
         const int i = perm[p];
         ri[k] = i;
-        const uint64_t ci = sc[i], row = ci >> 32;
-        if ((uint32_t)ci >= seq_cut) continue;  // at / past the cutoff: never applied
+        const uint64_t ci = sc[i], row = lr.row(ci), ki = lr.key(ci);
+        if (!lr.applied(ci)) continue;  // at / past the cutoff: never applied
         const uint32_t b = (uint32_t)((row - row0) >> bshift);
         const uint32_t bs = bstart[b], be = bstart[b + 1];
         if (be - bs > (uint32_t)kSpBucketMax) s_over = 1;
         bool first = true, dup = false;
         for (uint32_t q = bs; q < be; ++q) {
-            const uint64_t cj = sc[perm[q]];
-            if (cj != ci && (cj >> 32) == row && (uint32_t)cj < seq_cut) {
+            const int j = perm[q];
+            const uint64_t cj = sc[j];
+            if (j != i && lr.row(cj) == row && lr.applied(cj)) {
+                const uint64_t kj = lr.key(cj);
                 dup = true;
-                first &= cj > ci;
+                first &= kj > ki;
+                // compact: one push lists the row twice; only the replay's full
+                // sequence numbers order those adds
+                if (CMP && kj == ki) s_over = 1;
             }
         }
         own[k] = first;
@@ -483,12 +512,12 @@ __global__ __launch_bounds__(kSpLeafThreads) void k_sp_leaf(T* __restrict__ shar
         if (i >= n) continue;
         const uint8_t f = oflag[i];
         if (!(f & 1)) continue;
-        const uint64_t ci = sc[i], row = ci >> 32;
+        const uint64_t row = lr.row(sc[i]);
         T x = x0[k];
         if (!(f & 2)) {
             x = Elem<T>::add(x, u[k]);
         } else {
-            x = leaf_chain(x, row, row0, bshift, bstart, perm, sc, sv, seq_cut);
+            x = leaf_chain<T, CMP>(x, row, row0, bshift, bstart, perm, sc, sv, lr);
         }
         shard[row] = x;
     }
@@ -527,7 +556,7 @@ __global__ __launch_bounds__(256) void k_sp_runs(T* __restrict__ shard, const ui
 // partition (same box, 2 rounds): config 3 step 1.46 / 1.56 ms vs 1.69 / 1.62 ms;
 // a count-free variant with tile-local level-1 output and a gathering level 2:
 // 1.64 / 1.75 ms.
-template <typename T>
+template <typename T, bool CMP>
 __global__ __launch_bounds__(256) void k_sp_l1_fast(const Batch bt, const SpPlan pl, int64_t stride, int K,
                                                     int64_t first, int64_t rows, Ctrl* __restrict__ ctrl,
                                                     uint64_t tail_cut, uint32_t* __restrict__ cur1,
@@ -583,17 +612,24 @@ __global__ __launch_bounds__(256) void k_sp_l1_fast(const Batch bt, const SpPlan
         const int64_t q = (int64_t)base[bin] + rank[i];
         if (q >= pl.cap1) continue;
         const int64_t at = (int64_t)bin * pl.cap1 + q;
-        comp[at] = ((uint64_t)row[i] << 32) | (uint64_t)(pl.rec_base[b] + r0 + i * 256);
-        val[at] = u[i];
+        if constexpr (CMP) {
+            const int64_t rb = (int64_t)bin << (pl.SL + pl.D2);
+            comp[at] = ((uint64_t)(row[i] - rb) << 38) | ((uint64_t)b << 32) | (uint64_t)__float_as_uint(u[i]);
+        } else {
+            comp[at] = ((uint64_t)row[i] << 32) | (uint64_t)(pl.rec_base[b] + r0 + i * 256);
+            val[at] = u[i];
+        }
     }
 }
-template <typename T>
+template <typename T, bool CMP>
 __global__ __launch_bounds__(256) void k_sp_l2_fast(const SpPlan pl, const uint32_t* __restrict__ cur1,
                                                     const uint64_t* __restrict__ comp_in,
                                                     const T* __restrict__ val_in, uint32_t* __restrict__ cur2,
                                                     uint64_t* __restrict__ comp_out, T* __restrict__ val_out,
                                                     SpStat* __restrict__ stat) {
-    __shared__ SpStage<T> st;
+    using Stage = std::conditional_t<CMP, SpStageC, SpStage<T>>;
+    __shared__ Stage st;
+    constexpr int kRowShift = CMP ? 38 : 32;  // the record's row (within its level-1 bin if CMP)
     const int tid = threadIdx.x;
     const int bin = (int)(blockIdx.x / pl.tiles2_per_bin);
     const int64_t t = blockIdx.x - (int64_t)bin * pl.tiles2_per_bin;
@@ -611,13 +647,13 @@ __global__ __launch_bounds__(256) void k_sp_l2_fast(const SpPlan pl, const uint3
     for (int i = 0; i < kPer; ++i) {
         const int64_t j = lo + i * 256 + tid;
         c[i] = j < hi ? comp_in[src0 + j] : 0;
-        u[i] = j < hi ? val_in[src0 + j] : T(0);
+        if constexpr (!CMP) u[i] = j < hi ? val_in[src0 + j] : T(0);
     }
     st.cnt[tid] = 0u;
     __syncthreads();
 #pragma unroll
     for (int i = 0; i < kPer; ++i)
-        if (lo + i * 256 + tid < hi) atomicAdd(&st.cnt[(uint32_t)(c[i] >> (32 + pl.SL)) & mask], 1u);
+        if (lo + i * 256 + tid < hi) atomicAdd(&st.cnt[(uint32_t)(c[i] >> (kRowShift + pl.SL)) & mask], 1u);
     __syncthreads();
     {
         const uint32_t cn = st.cnt[tid];
@@ -633,21 +669,21 @@ __global__ __launch_bounds__(256) void k_sp_l2_fast(const SpPlan pl, const uint3
 #pragma unroll
     for (int i = 0; i < kPer; ++i) {
         if (lo + i * 256 + tid >= hi) continue;
-        const uint32_t d = (uint32_t)(c[i] >> (32 + pl.SL)) & mask;
+        const uint32_t d = (uint32_t)(c[i] >> (kRowShift + pl.SL)) & mask;
         const uint32_t q = atomicAdd(&st.cnt[d], 1u);
         st.c[q] = c[i];
-        st.v[q] = u[i];
+        if constexpr (!CMP) st.v[q] = u[i];
     }
     __syncthreads();
     const uint32_t nloc = st.lstart[256];
     for (uint32_t i = tid; i < nloc; i += 256) {
         const uint64_t cc = st.c[i];
-        const uint32_t d = (uint32_t)(cc >> (32 + pl.SL)) & mask;
+        const uint32_t d = (uint32_t)(cc >> (kRowShift + pl.SL)) & mask;
         const int64_t q = (int64_t)st.gstart[d] + (i - st.lstart[d]);
         if (q >= pl.cap2) continue;
         const int64_t at = (((int64_t)bin << pl.D2) + d) * pl.cap2 + q;
         comp_out[at] = cc;
-        val_out[at] = st.v[i];
+        if constexpr (!CMP) val_out[at] = st.v[i];
     }
 }
 
@@ -761,7 +797,8 @@ SpLayout sparse_layout(const SpPlan& pl, int vbytes) {
 
 template <typename T>
 static hipError_t partition_t(const Batch& bt, const SpPlan& pl, const SpLayout& l, uint8_t* ws, int64_t stride,
-                              int K, int64_t first, int64_t rows, Ctrl* ctrl, uint64_t tail_cut, hipStream_t st) {
+                              int K, int64_t first, int64_t rows, Ctrl* ctrl, uint64_t tail_cut, hipStream_t st,
+                              bool clear_flags = true) {
     SpMeta* m = (SpMeta*)(ws + l.meta);
     uint64_t* comp1 = (uint64_t*)(ws + l.comp1);
     uint64_t* comp2 = (uint64_t*)(ws + l.comp2);
@@ -773,7 +810,7 @@ static hipError_t partition_t(const Batch& bt, const SpPlan& pl, const SpLayout&
     uint32_t* off2 = (uint32_t*)(ws + l.off2);
     const int cells1 = (int)((int64_t)pl.nbins1 * pl.ntiles1 + 1);
     const int cells2 = (int)((pl.max_tiles2 << pl.D2) + 1);
-    hipError_t e = hipMemsetAsync(ws + l.leafflag, 0, (size_t)pl.nleaves, st);
+    hipError_t e = clear_flags ? hipMemsetAsync(ws + l.leafflag, 0, (size_t)pl.nleaves, st) : hipSuccess;
     if (e == hipSuccess) e = hipMemsetAsync(cnt1, 0, (size_t)cells1 * 4, st);
     if (e == hipSuccess) e = hipMemsetAsync(cnt2, 0, (size_t)cells2 * 4, st);
     if (e != hipSuccess) return e;
@@ -813,6 +850,15 @@ static hipError_t partition_t(const Batch& bt, const SpPlan& pl, const SpLayout&
     return hipGetLastError();
 }
 
+// Status + the partition's cutoff for the host (read before the leaf launch).
+static hipError_t finish_fast(uint8_t* ws, const SpLayout& l, Ctrl* ctrl, SpStat* hstat, hipStream_t st) {
+    hipError_t e = hipGetLastError();
+    if (e != hipSuccess) return e;
+    if ((e = hipMemcpyAsync(hstat, ws + l.stat, sizeof(unsigned int), hipMemcpyDeviceToHost, st)) != hipSuccess)
+        return e;
+    return hipMemcpyAsync(&hstat->cutoff, &ctrl->cutoff, sizeof(unsigned long long), hipMemcpyDeviceToHost, st);
+}
+
 template <typename T>
 static hipError_t partition_fast_t(const Batch& bt, const SpPlan& pl, const SpLayout& l, uint8_t* ws, int64_t stride,
                                    int K, int64_t first, int64_t rows, Ctrl* ctrl, uint64_t tail_cut, SpStat* hstat,
@@ -826,19 +872,28 @@ static hipError_t partition_fast_t(const Batch& bt, const SpPlan& pl, const SpLa
     if (e == hipSuccess) e = hipMemsetAsync(stat, 0, sizeof(SpStat), st);
     if (e != hipSuccess) return e;
     if (pl.ntiles1 > 0) {
-        hipLaunchKernelGGL(k_sp_l1_fast<T>, dim3((unsigned)pl.ntiles1), dim3(256), 0, st, bt, pl, stride, K, first,
-                           rows, ctrl, tail_cut, cur1, (uint64_t*)(ws + l.comp1), (T*)(ws + l.val1), stat);
-        hipLaunchKernelGGL(k_sp_l2_fast<T>, dim3((unsigned)(pl.nbins1 * pl.tiles2_per_bin)), dim3(256), 0, st, pl,
-                           (const uint32_t*)cur1, (const uint64_t*)(ws + l.comp1), (const T*)(ws + l.val1), cur2,
-                           (uint64_t*)(ws + l.comp2), (T*)(ws + l.val2), stat);
+        const dim3 g1((unsigned)pl.ntiles1), g2((unsigned)(pl.nbins1 * pl.tiles2_per_bin));
+        uint64_t* c1 = (uint64_t*)(ws + l.comp1);
+        uint64_t* c2 = (uint64_t*)(ws + l.comp2);
+        if constexpr (sizeof(T) == 4) {
+            if (pl.compact) {
+                hipLaunchKernelGGL((k_sp_l1_fast<T, true>), g1, dim3(256), 0, st, bt, pl, stride, K, first, rows, ctrl,
+                                   tail_cut, cur1, c1, (T*)nullptr, stat);
+                hipLaunchKernelGGL((k_sp_l2_fast<T, true>), g2, dim3(256), 0, st, pl, (const uint32_t*)cur1,
+                                   (const uint64_t*)c1, (const T*)nullptr, cur2, c2, (T*)nullptr, stat);
+                return finish_fast(ws, l, ctrl, hstat, st);
+            }
+        }
+        hipLaunchKernelGGL((k_sp_l1_fast<T, false>), g1, dim3(256), 0, st, bt, pl, stride, K, first, rows, ctrl,
+                           tail_cut, cur1, c1, (T*)(ws + l.val1), stat);
+        hipLaunchKernelGGL((k_sp_l2_fast<T, false>), g2, dim3(256), 0, st, pl, (const uint32_t*)cur1,
+                           (const uint64_t*)c1, (const T*)(ws + l.val1), cur2, c2, (T*)(ws + l.val2), stat);
         if ((e = hipGetLastError()) != hipSuccess) return e;
     } else if (tail_cut != kNoPos) {  // no complete record: only the truncation position
         if ((e = hipMemcpyAsync(&ctrl->cutoff, &tail_cut, sizeof tail_cut, hipMemcpyHostToDevice, st)) != hipSuccess)
             return e;
     }
-    // status + the partition's cutoff for the host (read before the leaf launch)
-    if ((e = hipMemcpyAsync(hstat, stat, sizeof(unsigned int), hipMemcpyDeviceToHost, st)) != hipSuccess) return e;
-    return hipMemcpyAsync(&hstat->cutoff, &ctrl->cutoff, sizeof(unsigned long long), hipMemcpyDeviceToHost, st);
+    return finish_fast(ws, l, ctrl, hstat, st);
 }
 
 hipError_t launch_sparse_partition_fast(int vtype, const Batch& bt, const SpPlan& pl, const SpLayout& l, uint8_t* ws,
@@ -868,13 +923,17 @@ hipError_t launch_sparse_leaf(int vtype, void* shard, const SpPlan& pl, const Sp
     // line buckets: leaf rows >> bshift < kSpLines
     int bshift = 0;
     while ((((int64_t)1 << pl.SL) >> bshift) > kSpLines) ++bshift;
-    if (vtype == kF32)
-        hipExtLaunchKernelGGL(k_sp_leaf<float>, grid, dim3(kSpLeafThreads), 0, st, ev.start, ev.stop, 0,
-                              (float*)shard, bounds, cnt2, pl.cap2, comp2, (const float*)(ws + l.val2), pl.SL, bshift,
+    if (vtype == kF32 && pl.compact)
+        hipExtLaunchKernelGGL((k_sp_leaf<float, true>), grid, dim3(kSpLeafThreads), 0, st, ev.start, ev.stop, 0,
+                              (float*)shard, bounds, cnt2, pl.cap2, comp2, (const float*)nullptr, pl.SL, pl.D2, bshift,
                               pl.seq_cut, flag, ctrl, prev);
+    else if (vtype == kF32)
+        hipExtLaunchKernelGGL((k_sp_leaf<float, false>), grid, dim3(kSpLeafThreads), 0, st, ev.start, ev.stop, 0,
+                              (float*)shard, bounds, cnt2, pl.cap2, comp2, (const float*)(ws + l.val2), pl.SL, pl.D2,
+                              bshift, pl.seq_cut, flag, ctrl, prev);
     else if (vtype == kF64)
-        hipExtLaunchKernelGGL(k_sp_leaf<double>, grid, dim3(kSpLeafThreads), 0, st, ev.start, ev.stop, 0,
-                              (double*)shard, bounds, cnt2, pl.cap2, comp2, (const double*)(ws + l.val2), pl.SL,
+        hipExtLaunchKernelGGL((k_sp_leaf<double, false>), grid, dim3(kSpLeafThreads), 0, st, ev.start, ev.stop, 0,
+                              (double*)shard, bounds, cnt2, pl.cap2, comp2, (const double*)(ws + l.val2), pl.SL, pl.D2,
                               bshift, pl.seq_cut, flag, ctrl, prev);
     else
         return hipErrorInvalidValue;
@@ -883,8 +942,20 @@ hipError_t launch_sparse_leaf(int vtype, void* shard, const SpPlan& pl, const Sp
 
 // Flagged (oversized) leaves, exactly: sort every kept record by (row, seq) and
 // run-apply the rows of flagged leaves. Synchronous; a rare path (skewed keys).
-hipError_t sparse_replay(int vtype, void* shard, const SpPlan& pl, const SpLayout& l, uint8_t* ws, hipStream_t st) {
+hipError_t sparse_replay(int vtype, void* shard, const SpPlan& pl_in, const SpLayout& l, uint8_t* ws, const Batch& bt,
+                         int64_t stride, int K, int64_t first, int64_t rows, Ctrl* ctrl, uint64_t tail_cut,
+                         hipStream_t st) {
     hipError_t e = hipSuccess;
+    SpPlan pl = pl_in;
+    if (pl.compact) {
+        // compact words order a row's adds by push only: re-partition the chunk with
+        // full sequence numbers (counted, compact layout), keeping the leaf flags
+        pl.compact = 0;
+        pl.fast = 0;
+        pl.seq_cut = kSpSkip;
+        if ((e = partition_t<float>(bt, pl, l, ws, stride, K, first, rows, ctrl, tail_cut, st, false)) != hipSuccess)
+            return e;
+    }
     int64_t nk = 0;
     uint64_t* kin = (uint64_t*)(ws + l.comp2);
     uint64_t* kout = (uint64_t*)(ws + l.comp1);

@@ -396,6 +396,9 @@ int launch_apply(dml_store* s, Chunk& c, Workspace& W, const Ctrl* prev) {
 // Index on the side stream (overlaps the previous chunk's apply), then apply.
 int launch_chunk(dml_store* s, Chunk& c, Workspace& W, const Ctrl* prev) {
     hipStream_t is = s->istream;
+#ifdef DML_SP_SERIAL
+    if (!s->is_matrix && (vtype_of(s->desc) == kF32 || vtype_of(s->desc) == kF64)) is = s->stream;
+#endif
     // A workspace whose last chunk retired normally through a slot-clearing reduce
     // (k_reduce_rows, plain-sum modes) already holds an all -1 slot table and zero
     // rowflags: only its Ctrl is reset (the 4 MiB-class memsets otherwise compete
@@ -419,6 +422,8 @@ int launch_chunk(dml_store* s, Chunk& c, Workspace& W, const Ctrl* prev) {
                                          c.tail_cut, is));
         if (c.sorted) {
             c.sp = sparse_plan(c.bt, c.nb, s->rows);
+            // one 8-B word per fp32 record through the partition
+            c.sp.compact = vt == kF32 && c.sp.SL + c.sp.D2 <= kSpCompactRowBits && c.tail_cut == kNoPos;
             c.spl = sparse_layout(c.sp, s->V);
             if (W.sp_cap < c.spl.total) {
                 HIPCHK(hipStreamSynchronize(s->stream));  // W's previous chunk is retired; be safe
@@ -433,24 +438,27 @@ int launch_chunk(dml_store* s, Chunk& c, Workspace& W, const Ctrl* prev) {
                                                 W.ctrl, c.tail_cut, W.hsp, is));
         }
     }
-    HIPCHK(hipEventRecord(W.idx_done, s->istream));
+    HIPCHK(hipEventRecord(W.idx_done, is));
     // The index (tens of µs) finishes while the previous chunk's reduce (hundreds
     // of µs) still runs: wait for it on the host and enqueue this chunk's apply
     // directly behind that reduce. A cross-queue barrier packet instead costs
     // ~16 µs of idle GPU between the two reduces (measured).
     HIPCHK(hipEventSynchronize(W.idx_done));
     if (c.sorted && c.sp.fast) {
-        if (W.hsp->overflow) {
-            // a bin or leaf of the single-pass partition overflowed (skewed keys):
-            // the counted partition, compact layout (still beside the running apply)
+        const uint64_t pcut = std::min<uint64_t>(W.hsp->cutoff, c.tail_cut);
+        if (W.hsp->overflow || (c.sp.compact && pcut != kNoPos)) {
+            // a bin or leaf of the single-pass partition overflowed (skewed keys), or
+            // compact records met a cutoff (they carry no sequence to cut at): the
+            // counted partition, compact layout (still beside the running apply)
             c.sp.fast = 0;
+            c.sp.compact = 0;
             c.sp.seq_cut = kSpSkip;
             HIPCHK(launch_sparse_partition(vtype_of(s->desc), c.bt, c.sp, c.spl, W.sp, s->stride, s->K, s->first,
-                                           s->rows, W.ctrl, c.tail_cut, s->istream));
-            HIPCHK(hipEventRecord(W.idx_done, s->istream));
+                                           s->rows, W.ctrl, c.tail_cut, is));
+            HIPCHK(hipEventRecord(W.idx_done, is));
             HIPCHK(hipEventSynchronize(W.idx_done));
         } else {
-            c.sp.seq_cut = sparse_seq_cut(c.sp, c.bt, std::min<uint64_t>(W.hsp->cutoff, c.tail_cut), s->stride);
+            c.sp.seq_cut = sparse_seq_cut(c.sp, c.bt, pcut, s->stride);
         }
     }
     return launch_apply(s, c, W, prev);
@@ -652,7 +660,8 @@ int retire_front(dml_store* s) {
         HIPCHK(hipStreamSynchronize(s->stream));
     } else if (!s->is_matrix && ctl.no_dup == 0u) {
         // leaves too large for the LDS sort were skipped by the leaf kernel: apply them exactly
-        HIPCHK(sparse_replay(vtype_of(s->desc), s->data, c.sp, c.spl, W.sp, s->stream));
+        HIPCHK(sparse_replay(vtype_of(s->desc), s->data, c.sp, c.spl, W.sp, c.bt, s->stride, s->K, s->first, s->rows,
+                             W.ctrl, c.tail_cut, s->stream));
     } else if (ctl.neg_pos != kNoPos) {
         if (s->is_matrix) {
             // the reduce handed its slot rows back clean: rebuild the table (no row

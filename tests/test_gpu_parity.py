@@ -1314,7 +1314,7 @@ def test_adagrad_maxdelta_tie_repeated_row(oracle, batched):
     assert kat.bits_equal(s.values(), o.data)
 
 
-@pytest.mark.parametrize("case", ["hot_line", "cutoff", "truncated"])
+@pytest.mark.parametrize("case", ["hot_line", "cutoff", "truncated", "push_repeat", "f64"])
 def test_sparse_single_pass_partition_exact(oracle, case):
     """The single-pass sparse partition (fixed-capacity bins, atomic cursors; DESIGN.md
     §4) against the oracle, bit-exact, where it must fall back or cut: `hot_line` — 40
@@ -1322,14 +1322,19 @@ def test_sparse_single_pass_partition_exact(oracle, case):
     records): the leaf kernel flags the leaf and the packed exact replay applies it;
     `cutoff` — a key outside the shard in the middle of push 3: records from it on
     are not applied (the sequence cut), error state as the reference's;
-    `truncated` — the last push ends inside a record."""
+    `truncated` — the last push ends inside a record; `push_repeat` — push 2 lists
+    one key twice (fp32 compact records order a row's adds by push only, so the leaf
+    goes to the replay, which re-partitions with full sequence numbers); `f64` —
+    DoubleArrayStore (full records) with cross-push repeats only."""
     from distml_amd import DataDesc, DistMLException, encode_array_push
     rng = np.random.default_rng(len(case))
     first, rows = 3, 2_000_000
-    fmt = DataDesc(0, 1, 1)  # FloatArrayStore, LONG keys
+    vt = 3 if case == "f64" else 1
+    dt = np.float64 if vt == 3 else np.float32
+    fmt = DataDesc(0, 1, vt)  # Float/DoubleArrayStore, LONG keys
     s, _ = mk_store(fmt, first, first + rows - 1)
     o = oracle_store(oracle, fmt, first, first + rows - 1)
-    init = rng.standard_normal((rows, 1)).astype(np.float32)
+    init = rng.standard_normal((rows, 1)).astype(dt)
     s.load_values(init)
     o.data[:] = init
     nb = 40 if case == "hot_line" else 6
@@ -1338,8 +1343,10 @@ def test_sparse_single_pass_partition_exact(oracle, case):
         keys = rng.choice(rows, size=20_000, replace=False) + first
         if case == "hot_line":
             keys[:2] = [777 + first, 778 + first]
-        vals = (rng.standard_normal(len(keys)) * 1e-2).astype(np.float32)
-        p = encode_array_push(keys, vals, 1, 1)
+        if case == "push_repeat" and b == 2:
+            keys[17] = keys[5]
+        vals = (rng.standard_normal(len(keys)) * 1e-2).astype(dt)
+        p = encode_array_push(keys, vals, 1, vt)
         if case == "cutoff" and b == 3:
             bad = encode_array_push([rows + first + 5], [1.0], 1, 1)
             p = p[:12 * 9000] + bad + p[12 * 9000:]
