@@ -396,9 +396,6 @@ int launch_apply(dml_store* s, Chunk& c, Workspace& W, const Ctrl* prev) {
 // Index on the side stream (overlaps the previous chunk's apply), then apply.
 int launch_chunk(dml_store* s, Chunk& c, Workspace& W, const Ctrl* prev) {
     hipStream_t is = s->istream;
-#ifdef DML_SP_SERIAL
-    if (!s->is_matrix && (vtype_of(s->desc) == kF32 || vtype_of(s->desc) == kF64)) is = s->stream;
-#endif
     // A workspace whose last chunk retired normally through a slot-clearing reduce
     // (k_reduce_rows, plain-sum modes) already holds an all -1 slot table and zero
     // rowflags: only its Ctrl is reset (the 4 MiB-class memsets otherwise compete
