@@ -31,6 +31,62 @@ __device__ inline void st_nt(uint8_t* p, u32x4 v) { __builtin_nontemporal_store(
 // Each wave reads NB blocks (block ids idx[w*NB + k]) of `bsz` bytes at `stride`
 // (4 x 1 KiB per lane group, like CPW = 4) and, if ROW, reads and writes row w of
 // `rows` (rsz bytes). XOR-folds into sink so nothing is dead.
+// Config 4 AdaGrad pattern (k_ada_flat's traffic, bare): a wave owns R = 5
+// neighbouring 800-B rows; it reads data and delta, streams the W pushes' 5
+// records, and writes data and delta back. SLOT: a dependent per-wave index load
+// first (k_ada_flat reads its slot rows before the push loads); PERSIST: a fixed
+// grid whose waves walk groups with the next group's index prefetched.
+template <int W, bool SLOT, bool PERSIST>
+__global__ __launch_bounds__(256) void k_ada(const uint8_t* __restrict__ pushes, int64_t push_bytes,
+                                             uint8_t* __restrict__ data, uint8_t* __restrict__ delta,
+                                             const int32_t* __restrict__ idx, int64_t nwaves) {
+    const int lane = threadIdx.x & 63;
+    const int64_t w0 = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+    const int64_t step = PERSIST ? (int64_t)gridDim.x * 4 : nwaves;
+    constexpr int R = 5, REC = 804, ROW = 800, J = 4;  // 4 x 64 x 16 B >= 4 000 B
+    int32_t nx = (SLOT && w0 < nwaves) ? idx[w0] : (int32_t)w0;
+    for (int64_t w = w0; w < nwaves; w += step) {
+        const int32_t g = nx;
+        if (PERSIST && SLOT && w + step < nwaves) nx = idx[w + step];
+        else if (PERSIST) nx = (int32_t)(w + step);
+        u32x4 a[J], d[J];
+        uint8_t* dp = data + w * (int64_t)(R * ROW);
+        uint8_t* ep = delta + w * (int64_t)(R * ROW);
+#pragma unroll
+        for (int j = 0; j < J; ++j) {
+            const int o = (j * 64 + lane) * 16;
+            a[j] = o < R * ROW ? ld_nt(dp + o) : u32x4{0, 0, 0, 0};
+            d[j] = o < R * ROW ? ld_nt(ep + o) : u32x4{0, 0, 0, 0};
+        }
+        u32x4 raw[W][J];
+#pragma unroll
+        for (int b = 0; b < W; ++b) {
+            const uint8_t* bp = pushes + b * push_bytes + (int64_t)g * (R * REC) + 4;
+#pragma unroll
+            for (int j = 0; j < J; ++j) {
+                const int o = (j * 64 + lane) * 16;
+                raw[b][j] = o < R * REC - 16 ? ld_nt(bp + o) : u32x4{0, 0, 0, 0};
+            }
+        }
+#pragma unroll
+        for (int b = 0; b < W; ++b)
+#pragma unroll
+            for (int j = 0; j < J; ++j) {
+                a[j] += raw[b][j];
+                d[j] += raw[b][j] * raw[b][j];
+            }
+#pragma unroll
+        for (int j = 0; j < J; ++j) {
+            const int o = (j * 64 + lane) * 16;
+            if (o < R * ROW) {
+                st_nt(dp + o, a[j]);
+                st_nt(ep + o, d[j]);
+            }
+        }
+        if (!PERSIST) break;
+    }
+}
+
 template <int NB, bool ROW, bool NT>
 __global__ __launch_bounds__(128) void k_blocks(const uint8_t* __restrict__ src, const int32_t* __restrict__ idx,
                                                 int64_t stride, int bsz, uint8_t* __restrict__ rows, int rsz,
@@ -195,6 +251,47 @@ int main() {
         const double by = 8.0 * pb + 2.0 * r4 * 800;
         printf("%-44s %8.1f us  %7.1f GB/s\n", "config-4 shard pattern (8 asc pushes, R=10)", best * 1e3,
                by / (best * 1e-3) / 1e9);
+    }
+    // config 4 AdaGrad: 2 pushes of 10 000 000 x 804 B, data + delta 10 000 000 x 800 B
+    {
+        const int64_t r4 = 10000000, pb = r4 * 804;
+        uint8_t *pp, *da, *de;
+        int32_t* ix;
+        CK(hipMalloc(&pp, 2 * pb + 64));
+        CK(hipMalloc(&da, r4 * 800 + 64));
+        CK(hipMalloc(&de, r4 * 800 + 64));
+        const int64_t nw = r4 / 5;
+        std::vector<int32_t> hi(nw);
+        std::iota(hi.begin(), hi.end(), 0);
+        CK(hipMalloc(&ix, nw * 4));
+        CK(hipMemcpy(ix, hi.data(), nw * 4, hipMemcpyHostToDevice));
+        CK(hipMemset(pp, 0, 2 * pb + 64));
+        CK(hipMemset(da, 0, r4 * 800 + 64));
+        CK(hipMemset(de, 0, r4 * 800 + 64));
+        const double by = 2.0 * pb + 4.0 * r4 * 800;
+        auto go = [&](const char* name, auto kern, unsigned grid) {
+            hipEvent_t a, b;
+            CK(hipEventCreate(&a));
+            CK(hipEventCreate(&b));
+            float best = 1e30f;
+            for (int rep = 0; rep < 5; ++rep) {
+                CK(hipEventRecord(a));
+                hipLaunchKernelGGL(kern, dim3(grid), dim3(256), 0, 0, pp, pb, da, de, ix, nw);
+                CK(hipEventRecord(b));
+                CK(hipEventSynchronize(b));
+                float ms;
+                CK(hipEventElapsedTime(&ms, a, b));
+                if (rep) best = std::min(best, ms);
+            }
+            printf("%-44s %8.1f us  %7.1f GB/s\n", name, best * 1e3, by / (best * 1e-3) / 1e9);
+        };
+        const unsigned full = (unsigned)((nw + 3) / 4);
+        go("ada pattern: 2 pushes, one group per wave", k_ada<2, false, false>, full);
+        go("ada pattern: + dependent index load", k_ada<2, true, false>, full);
+        go("ada pattern: persistent 256x8 blocks", k_ada<2, false, true>, 2048u);
+        go("ada pattern: persistent + index prefetch", k_ada<2, true, true>, 2048u);
+        go("ada pattern: persistent 256x12 blocks + idx", k_ada<2, true, true>, 3072u);
+        go("ada pattern: persistent 256x4 blocks + idx", k_ada<2, true, true>, 1024u);
     }
     return 0;
 }

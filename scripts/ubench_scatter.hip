@@ -68,6 +68,14 @@ __global__ void k_unit(float* a, const uint32_t* unit, const uint32_t* run, cons
 #pragma unroll
     for (int j = 0; j < U / 4; ++j) p[j] = q[j];
 }
+// the same with non-temporal shard load and store
+__global__ void k_plain_nt(float* a, const uint32_t* keys, const float* v, int64_t n) {
+    int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i < n) {
+        uint32_t k = keys[i];
+        __builtin_nontemporal_store(__builtin_nontemporal_load(&a[k]) + v[i], &a[k]);
+    }
+}
 __global__ void k_read(const float4* p, int64_t n, float* out) {
     float s = 0;
     for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
@@ -150,6 +158,7 @@ int main() {
     timeit("plain RMW, 1 launch, globally sorted 32e6", [&] { k_plain<<<gN, 256>>>(a, dg, dv, N); });
     timeit("plain RMW x4, 1 launch, globally sorted", [&] { k_plain4<<<(gN + 3) / 4, 256>>>(a, dg, dv, N); });
     timeit("atomic, 1 launch, globally sorted", [&] { k_atomic<<<gN, 256>>>(a, dg, dv, N); });
+    timeit("plain RMW nt, 1 launch, globally sorted", [&] { k_plain_nt<<<gN, 256>>>(a, dg, dv, N); });
     auto unit_case = [&](auto tag, const char* name) {
         constexpr int U = decltype(tag)::value;
         std::vector<uint32_t> hu, hr;
