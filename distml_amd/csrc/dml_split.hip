@@ -16,8 +16,8 @@
 //                    histogram in LDS -> blkcnt[push][block][dest]
 //   k_split_scan     per (push, dest): exclusive scan of the block counts
 //   k_split_scatter  per block: the owner and the stable rank of each of its 256
-//                    records (LDS), then each wave copies 64 records, one record
-//                    at a time as 64-lane dword runs (256 B per instruction)
+//                    records (LDS), then the block's records move as one flat run
+//                    of 16-B chunks, stored as vectors where the output is contiguous
 #include <algorithm>
 #include <vector>
 
@@ -98,14 +98,53 @@ __global__ __launch_bounds__(kSplitBlock) void k_split_scatter(const Batch bt, i
         pos[threadIdx.x] = -1;
     }
     __syncthreads();
-    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+    // Copy: the block's records are one contiguous source range; it moves as a flat
+    // run of 16-B chunks (chunk c = dwords 4c..4c+3 of the range; U chunks per thread,
+    // all loads in flight before the stores). A chunk spans at most two records
+    // (records are >= 2 dwords); it is stored as one 16-B vector when its records are
+    // neighbours in the output (the common case: a run of one owner's records), else
+    // dword by dword. Records are 4-byte aligned only: unaligned vector accesses.
     const int64_t nw = stride / 4;  // records are whole dwords (K and V are 4 or 8 bytes)
-    for (int i = w * 64; i < (w + 1) * 64; ++i) {
-        const int64_t p = pos[i];
-        if (p < 0) continue;  // wave-uniform
-        const uint32_t* s = (const uint32_t*)(src + (r0 + i) * stride);
-        uint32_t* o = (uint32_t*)(out + p * stride);
-        for (int64_t j = lane; j < nw; j += 64) o[j] = __builtin_nontemporal_load(s + j);
+    const int64_t nr = nrec - r0 < kSplitBlock ? nrec - r0 : kSplitBlock;
+    const int64_t ndw = nr > 0 ? nr * nw : 0;
+    const int64_t nch = (ndw + 3) / 4;
+    const uint8_t* sb = src + r0 * stride;
+    constexpr int U = 8;
+    for (int64_t c0 = threadIdx.x; c0 < nch; c0 += (int64_t)kSplitBlock * U) {
+        u32x4 v[U];
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            const int64_t c = c0 + (int64_t)u * kSplitBlock;
+            if (c + 1 < nch || (c + 1 == nch && (ndw & 3) == 0)) {
+                v[u] = ldg16_nt(sb + c * 16);
+            } else if (c < nch) {  // the range's last, partial chunk: no read past its end
+                v[u] = u32x4{0u, 0u, 0u, 0u};
+#pragma unroll
+                for (int k = 0; k < 4; ++k)
+                    if (4 * c + k < ndw) v[u][k] = ldg32(sb + (4 * c + k) * 4);
+            }
+        }
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            const int64_t c = c0 + (int64_t)u * kSplitBlock;
+            if (c >= nch) break;
+            const int64_t x = 4 * c;
+            const int i0 = (int)(x / nw);
+            const int64_t p0 = pos[i0];
+            const int64_t last = x + 3 < ndw ? x + 3 : ndw - 1;
+            const int i1 = (int)(last / nw);
+            if (last == x + 3 && p0 >= 0 && (i1 == i0 || pos[i1] == p0 + 1)) {
+                stg16(out + (p0 * nw + (x - (int64_t)i0 * nw)) * 4, v[u]);
+            } else {
+#pragma unroll
+                for (int k = 0; k < 4; ++k) {
+                    if (x + k >= ndw) break;
+                    const int i = (int)((x + k) / nw);
+                    const int64_t p = pos[i];
+                    if (p >= 0) *(DML_GLOBAL uint32_t*)(out + (p * nw + (x + k - (int64_t)i * nw)) * 4) = v[u][k];
+                }
+            }
+        }
     }
 }
 

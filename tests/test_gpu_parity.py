@@ -784,21 +784,28 @@ def _np_split(recs_list, K, total_rows, world):
     (1, 1, 3, 10, 784, 2, 4, 300),      # MLR DoubleMatrix (LONG keys)
     (0, 1, 1, 1, 10**9, 5, 2, 20000),   # sparse float array, long keys
     (1, 0, 1, 64, 100, 64, 1, 257),     # 64 owners, ragged last block
+    (1, 0, 1, 200, 5003, 8, 3, 5003, "asc"),  # full-range ascending pushes: owner runs (vector copies)
+    (0, 1, 1, 1, 40000, 3, 2, 40000, "asc"),  # 12-B records in owner runs
+    (1, 0, 1, 200, 4000, 1, 2, 4000, "asc"),  # world 1: the split is one copy
 ])
 def test_shard_split_kernel(case):
     """dml_shard_split against a numpy stable partition: counts and bytes equal; keys
-    outside [0, total_rows) dropped."""
+    outside [0, total_rows) dropped. `asc`: every push lists the keys in ascending
+    order (each owner's records form one run)."""
     from distml_amd import DataDesc
     from distml_amd.group import HipOps
-    dtp, kt, vt, cols, total, world, n, nrec = case
+    dtp, kt, vt, cols, total, world, n, nrec = case[:8]
+    asc = len(case) > 8
     fmt = DataDesc(dtp, kt, vt)
     K, V = (4 if kt == 0 else 8), (4 if vt in (0, 1) else 8)
     stride = K + (V * cols if dtp == 1 else V)
-    rng = np.random.default_rng(sum(case))
+    rng = np.random.default_rng(sum(case[:8]))
     recs = []
     for b in range(n):
         r = rng.integers(0, 256, size=(nrec + b, stride), dtype=np.uint8)
         keys = rng.integers(-3, total + 3, size=nrec + b).astype("<i4" if K == 4 else "<i8")
+        if asc:
+            keys = (np.arange(nrec + b) - b).astype(keys.dtype)  # push b: one key below 0 (dropped)
         r[:, :K] = keys.view(np.uint8).reshape(-1, K)
         recs.append(r)
     dev = [torch.from_numpy(r.reshape(-1)).cuda() for r in recs]
