@@ -916,12 +916,18 @@ def main():
     torch.cuda.set_device(local)
     if world > 1 and args.rehearse_gloo:
         dist.init_process_group("gloo")
-    elif world > 1:
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
-    elif args.group:
-        os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
-        os.environ.setdefault("MASTER_PORT", str(_free_port()))
-        dist.init_process_group("nccl", rank=0, world_size=1, device_id=torch.device("cuda", local))
+    elif world > 1 or args.group:
+        # RCCL's collectives run on a high-priority stream: when a reduce-scatter and
+        # the next call's pre-reduce compete for CUs, the collective's blocks go first
+        opts = dist.ProcessGroupNCCL.Options()
+        opts.is_high_priority_stream = True
+        if world == 1:
+            os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+            os.environ.setdefault("MASTER_PORT", str(_free_port()))
+            dist.init_process_group("nccl", rank=0, world_size=1, device_id=torch.device("cuda", local),
+                                    pg_options=opts)
+        else:
+            dist.init_process_group("nccl", device_id=torch.device("cuda", local), pg_options=opts)
     L = _lib.load()
     ctx = Ctx(torch, dist, world, rank, local)
 
