@@ -122,7 +122,9 @@ int group_init(dml_group* g, const uint8_t* unique_id) {
     GHIP(hipDeviceGetStreamPriorityRange(&lo, &hi));
     GHIP(hipStreamCreateWithFlags(&g->cstream, hipStreamNonBlocking));
     GHIP(hipStreamCreateWithPriority(&g->istream, hipStreamNonBlocking, hi));
-    GHIP(hipStreamCreateWithFlags(&g->rstream, hipStreamNonBlocking));
+    // RCCL's stream is high-priority too: a reduce-scatter's blocks are dispatched
+    // ahead of the next call's pre-reduce blocks when both wait for CUs
+    GHIP(hipStreamCreateWithPriority(&g->rstream, hipStreamNonBlocking, hi));
     // linearSplit(world): every rank's slice of the partial is step_rows long
     std::vector<int64_t> f((size_t)g->world), l((size_t)g->world);
     GRC(dml_linear_split(0, g->total_rows - 1, g->world, f.data(), l.data()));
