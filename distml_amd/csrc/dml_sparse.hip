@@ -912,6 +912,19 @@ hipError_t launch_sparse_partition(int vtype, const Batch& bt, const SpPlan& pl,
     return hipErrorInvalidValue;
 }
 
+// Leaf blocks per CU: 2. Unused dynamic LDS on top of the kernel's static arrays
+// keeps a third leaf block off a CU, so the next chunk's partition blocks (on the
+// index stream) find wave slots and LDS beside the running leaf: same box, 3
+// rounds, config-3 step 1.455 -> 1.422 ms and 1.348 -> 1.328 ms on a second box;
+// 3 blocks 1.443, 1 block 1.67 (all 4 fit otherwise: 8-wave blocks, 32 waves).
+template <typename T, bool CMP>
+constexpr unsigned leaf_lds_pad() {
+    constexpr unsigned kLds = 160u * 1024u, kBlocks = 2;
+    constexpr unsigned stat = 8u * kSpLeafCap + (CMP ? 4u : (unsigned)sizeof(T) * kSpLeafCap) + 2u * kSpLeafCap +
+                              4u * (kSpLines + 1) + 4u * kSpLines + 4u * (kSpLeafThreads / 64) + 4u + kSpLeafCap;
+    return kLds / (kBlocks + 1) + 256u - stat;
+}
+
 hipError_t launch_sparse_leaf(int vtype, void* shard, const SpPlan& pl, const SpLayout& l, uint8_t* ws, Ctrl* ctrl,
                               const Ctrl* prev, hipStream_t st, LaunchEv ev) {
     if (pl.nleaves <= 0) return hipSuccess;
@@ -924,15 +937,18 @@ hipError_t launch_sparse_leaf(int vtype, void* shard, const SpPlan& pl, const Sp
     int bshift = 0;
     while ((((int64_t)1 << pl.SL) >> bshift) > kSpLines) ++bshift;
     if (vtype == kF32 && pl.compact)
-        hipExtLaunchKernelGGL((k_sp_leaf<float, true>), grid, dim3(kSpLeafThreads), 0, st, ev.start, ev.stop, 0,
+        hipExtLaunchKernelGGL((k_sp_leaf<float, true>), grid, dim3(kSpLeafThreads), leaf_lds_pad<float, true>(), st,
+                              ev.start, ev.stop, 0,
                               (float*)shard, bounds, cnt2, pl.cap2, comp2, (const float*)nullptr, pl.SL, pl.D2, bshift,
                               pl.seq_cut, flag, ctrl, prev);
     else if (vtype == kF32)
-        hipExtLaunchKernelGGL((k_sp_leaf<float, false>), grid, dim3(kSpLeafThreads), 0, st, ev.start, ev.stop, 0,
+        hipExtLaunchKernelGGL((k_sp_leaf<float, false>), grid, dim3(kSpLeafThreads), leaf_lds_pad<float, false>(), st,
+                              ev.start, ev.stop, 0,
                               (float*)shard, bounds, cnt2, pl.cap2, comp2, (const float*)(ws + l.val2), pl.SL, pl.D2,
                               bshift, pl.seq_cut, flag, ctrl, prev);
     else if (vtype == kF64)
-        hipExtLaunchKernelGGL((k_sp_leaf<double, false>), grid, dim3(kSpLeafThreads), 0, st, ev.start, ev.stop, 0,
+        hipExtLaunchKernelGGL((k_sp_leaf<double, false>), grid, dim3(kSpLeafThreads), leaf_lds_pad<double, false>(), st,
+                              ev.start, ev.stop, 0,
                               (double*)shard, bounds, cnt2, pl.cap2, comp2, (const double*)(ws + l.val2), pl.SL, pl.D2,
                               bshift, pl.seq_cut, flag, ctrl, prev);
     else
