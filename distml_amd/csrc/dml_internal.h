@@ -30,7 +30,7 @@ constexpr uint64_t kOffMask = (1ull << 40) - 1;
 struct Ctrl {
     unsigned long long cutoff;   // first key-out-of-shard position (exclusive apply limit)
     unsigned long long neg_pos;  // first add that left an int32 counter negative
-    unsigned long long ident;    // speculative chunk: bit b = push b taken as identity (record r is row r)
+    unsigned long long ident;    // speculative chunk: bit b = push b verified in the reduce (identity: record r is row r; or slot reuse)
     unsigned int no_dup;         // 0xFFFFFFFF = no row repeated inside one push; 0 = repeat seen
     unsigned int spec_ok;        // speculative chunk: 0xFFFFFFFF = every identity record verified; 0 = not
 };
@@ -51,6 +51,17 @@ struct Batch {
     const void* src;      // input shard (null: in place)
     int64_t first;        // key of row 0 (KeyRange first), for the verification
     int32_t spec;         // 1: speculative chunk
+    // Slot reuse (speculative chunks reduced by k_reduce_rows): bit b = push b's
+    // column of the workspace's slot table still holds the permutation the push at
+    // position b of the workspace's previous chunk listed. A push whose sampled keys
+    // match it skips the key index; the reduce reads its slots from the table and
+    // verifies every record's key like an identity push's.
+    uint64_t reuse;
+    // 1: such a chunk (its table may hold kept columns, so a stale entry is no
+    // repeat): the key index does not look for repeated rows, and the reduce
+    // verifies the record of every row of every push instead (all pushes are
+    // full-range, so a repeat leaves another row without its record).
+    int32_t keeps;
 };
 
 // A chunk whose predecessor ended abnormally (error, rows to replay, or a failed
@@ -125,8 +136,8 @@ hipError_t launch_index(const Batch& bt, int nb, int64_t max_nrec, int64_t strid
                         uint64_t tail_cut, hipStream_t st);
 // Identity speculation: clears ctrl->ident bit b unless push b is full-range and
 // every sampled record r of it has row_index(key) == r (Ctrl reset to all ones).
-hipError_t launch_ident_check(const Batch& bt, int nb, int64_t stride, int K, int64_t first, int64_t rows, Ctrl* ctrl,
-                              hipStream_t st);
+hipError_t launch_ident_check(const Batch& bt, int nb, int64_t stride, int K, int64_t first, int64_t rows,
+                              const int32_t* slot, Ctrl* ctrl, hipStream_t st);
 hipError_t launch_reduce(int vtype, int mode, void* shard, int64_t rows, int32_t cols, const Batch& bt,
                          int nb, int64_t stride, int K, const int32_t* slot, const uint32_t* rowflag, Ctrl* ctrl,
                          uint64_t tail_cut, const AdaArgs& ada, hipStream_t st, int64_t* nblocks_out,
@@ -232,6 +243,8 @@ int64_t reduce_blocks(int vtype, int64_t rows, int32_t cols);
 // True when launch_reduce(vtype, mode, cols) runs k_reduce_rows in a plain-sum mode,
 // which rewrites every slot it reads to -1 (the next batch's index then needs no memset).
 bool reduce_clears_slots(int vtype, int mode, int32_t cols);
+// The chunk's plain-sum reduce is k_reduce_flat (narrow dense rows), not k_reduce_rows.
+bool use_flat(int vtype, int mode, int32_t cols, const Batch& bt, int nb, int64_t rows);
 // row shapes whose reduce runs identity-speculative chunks (k_reduce_rows FULL, k_reduce_flat)
 bool spec_shape(int vtype, int32_t cols);
 

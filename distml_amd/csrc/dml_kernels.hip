@@ -77,7 +77,7 @@ __global__ __launch_bounds__(256) void k_index(const Batch bt, int64_t stride, i
         return;
     }
     const int32_t old = atomicExch(&slot[idx * slot_stride((int)gridDim.y) + b], (int32_t)r);
-    if (old != -1) {
+    if (old != -1 && !bt.keeps) {
         rowflag[idx] = 1u;
         ctrl->no_dup = 0u;  // benign race: every writer stores the same value
     }
@@ -86,15 +86,21 @@ __global__ __launch_bounds__(256) void k_index(const Batch bt, int64_t stride, i
 // k_ident_check: one 64-lane block per push of a speculative chunk. Push b stays
 // an identity candidate if it is full-range (nrec == rows) and the records at 32
 // evenly spaced positions (first and last included) plus 32 hashed ones hold row
-// r at record r. Cheap (64 key lines per push); the reduce verifies every record.
+// r at record r — or, for a slot-reuse candidate (Batch::reuse), the row the kept
+// slot column maps to record r. Cheap (64 key lines per push); the reduce
+// verifies every record.
 __global__ __launch_bounds__(64) void k_ident_check(const Batch bt, int64_t stride, int K, int64_t first, int64_t rows,
-                                                    Ctrl* __restrict__ ctrl) {
+                                                    const int32_t* __restrict__ slot, Ctrl* __restrict__ ctrl) {
     const int b = blockIdx.x, t = threadIdx.x;
     bool ok = bt.nrec[b] == rows && rows > 0;
     if (ok) {
         const int64_t r = t < 32 ? (rows > 1 ? (int64_t)t * (rows - 1) / 31 : 0)
                                  : (int64_t)(splitmix64_dev(((uint64_t)b << 32) + (uint64_t)t) % (uint64_t)rows);
-        ok = row_index(ld_key(bt.base[b] + r * stride, K), first, rows) == r;
+        const int64_t idx = row_index(ld_key(bt.base[b] + r * stride, K), first, rows);
+        if ((bt.reuse >> b) & 1ull)
+            ok = idx >= 0 && slot[idx * slot_stride((int)gridDim.x) + b] == (int32_t)r;
+        else
+            ok = idx == r;
     }
     const bool all = __ballot(!ok) == 0ull;
     if (t == 0) {
@@ -103,10 +109,10 @@ __global__ __launch_bounds__(64) void k_ident_check(const Batch bt, int64_t stri
         if (clear) atomicAnd(&ctrl->ident, ~clear);
     }
 }
-hipError_t launch_ident_check(const Batch& bt, int nb, int64_t stride, int K, int64_t first, int64_t rows, Ctrl* ctrl,
-                              hipStream_t st) {
+hipError_t launch_ident_check(const Batch& bt, int nb, int64_t stride, int K, int64_t first, int64_t rows,
+                              const int32_t* slot, Ctrl* ctrl, hipStream_t st) {
     if (nb <= 0) return hipSuccess;
-    hipLaunchKernelGGL(k_ident_check, dim3((unsigned)nb), dim3(64), 0, st, bt, stride, K, first, rows, ctrl);
+    hipLaunchKernelGGL(k_ident_check, dim3((unsigned)nb), dim3(64), 0, st, bt, stride, K, first, rows, slot, ctrl);
     return hipGetLastError();
 }
 
@@ -597,20 +603,23 @@ __global__ __launch_bounds__(64 * WPB) void k_reduce_rows(T* __restrict__ shard,
     int32_t vslot[RPW];
     // lanes >= nb read past the row's entries (another row's): masked to -1;
     // an identity push (speculation) holds row r at record r when r < nrec
-    const bool lane_ident = lane < nb && ((ident >> lane) & 1ull);
+    // a slot-reuse push (Batch::reuse) is verified like an identity push but takes
+    // its slots from the kept table
+    const bool lane_ident = lane < nb && ((ident >> lane) & 1ull) && !((bt.reuse >> lane) & 1ull);
 #pragma unroll
     for (int r = 0; r < RPW; ++r)
         vslot[r] = ((live >> r & 1u) && lane < nb)
                        ? (lane_ident ? (row[r] < bt.nrec[lane] ? (int32_t)row[r] : -1) : slot[row[r] * slot_stride(nb) + lane])
                        : -1;
-    {
+    if (!bt.spec) {
         // Hand the slot rows back as the next batch's index expects them (-1 = no
         // record), so the host skips the slot-table memset (reduce_clears_slots); the
-        // int32 rollback (rare) rebuilds the table with a second index. Identity
-        // pushes never wrote theirs.
+        // int32 rollback (rare) rebuilds the table with a second index. A speculative
+        // chunk keeps its table: its full-range columns are permutations the next
+        // chunk in this workspace may reuse (Batch::reuse).
 #pragma unroll
         for (int r = 0; r < RPW; ++r)
-            if ((live >> r & 1u) && lane < nb && !lane_ident) slot[row[r] * slot_stride(nb) + lane] = -1;
+            if ((live >> r & 1u) && lane < nb) slot[row[r] * slot_stride(nb) + lane] = -1;
     }
     const uint64_t vbase = lane < nb ? (uint64_t)bt.base[lane] : 0ull;
     // Speculative chunks verify identity records through lane 63 of the wave's last
@@ -748,6 +757,8 @@ __global__ __launch_bounds__(64 * WPB) void k_reduce_rows(T* __restrict__ shard,
             rr[r] = __builtin_amdgcn_readlane(vslot[r], b);
             has |= (rr[r] >= 0 ? 1u : 0u) << r;
         }
+        // a slot-keeping chunk: every live row of every (full-range) push has a record
+        if (MODE == kAdd && bt.keeps && (has & live) != live) bad = true;
         if (!has) continue;
         touched |= has;
         const uint8_t* bp = (const uint8_t*)(((uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)vbase, b)) |
@@ -758,7 +769,8 @@ __global__ __launch_bounds__(64 * WPB) void k_reduce_rows(T* __restrict__ shard,
         for (int r = 0; r < RPW; ++r) {
             if constexpr (MODE == kAdd) {
                 // identity push: verify the key of every record taken as row r
-                kv[r] = ((ident >> b) & 1ull) && rr[r] >= 0 ? ld_key(bp + (int64_t)rr[r] * stride, K) : bt.first + row[r];
+                kv[r] = (bt.keeps || ((ident >> b) & 1ull)) && rr[r] >= 0 ? ld_key(bp + (int64_t)rr[r] * stride, K)
+                                                                         : bt.first + row[r];
             }
             if constexpr (FULL) {
                 // one address per row; the chunks are immediate offsets of the loads

@@ -67,6 +67,7 @@ struct Chunk {
     SpPlan sp{};
     SpLayout spl{};
     bool spec = false;     // identity speculation (full-range plain-sum chunk, Batch::spec)
+    bool keeps = false;    // speculative chunk reduced by k_reduce_rows: its slot table is kept (Batch::reuse)
     void* in = nullptr;    // matrix shard the chunk reads (the previous chunk's output)
     void* out = nullptr;   // and writes: == in, or the other buffer of a speculative chunk
 };
@@ -95,6 +96,13 @@ struct Workspace {
     SpStat* hsp = nullptr;            // pinned status of the single-pass sparse partition
     bool clears = false;              // the chunk's reduce leaves its slot table all -1
     bool clean = false;               // slot table all -1 and rowflags 0: only the Ctrl needs a reset
+    // Kept slot table (the last chunk here was a verified speculative chunk reduced by
+    // k_reduce_rows): rowflags 0, and column b of [rows][slot_stride(kept_nb)] is the
+    // permutation push b listed when bit b of `perm` is set (indexed or reused, not
+    // identity); other columns hold no meaning
+    bool kept = false;
+    int kept_nb = 0;
+    uint64_t perm = 0;
 };
 
 struct Pending {
@@ -400,12 +408,18 @@ int launch_chunk(dml_store* s, Chunk& c, Workspace& W, const Ctrl* prev) {
     // (k_reduce_rows, plain-sum modes) already holds an all -1 slot table and zero
     // rowflags: only its Ctrl is reset (the 4 MiB-class memsets otherwise compete
     // with the running reduce).
-    const bool clean = W.clean;
-    W.clean = false;
-    HIPCHK(hipMemsetAsync(W.base, 0xFF, sizeof(Ctrl) + (clean ? 0 : s->slot_bytes), is));
+    const bool clean = W.clean, kept = W.kept;
+    W.clean = W.kept = false;
+    // A speculative k_reduce_rows chunk needs no -1 table either: its pushes are
+    // full-range, so the index rewrites every row of each column it builds (a push
+    // that is no permutation fails the chunk, and the re-run starts from a memset),
+    // and identity / reused columns are not rebuilt.
+    const bool slots_ok = clean || (kept && c.keeps);
+    HIPCHK(hipMemsetAsync(W.base, 0xFF, sizeof(Ctrl) + (slots_ok ? 0 : s->slot_bytes), is));
     if (s->is_matrix) {
-        if (!clean) HIPCHK(hipMemsetAsync(W.rowflag, 0, (size_t)s->rows * sizeof(uint32_t), is));
-        if (c.spec) HIPCHK(launch_ident_check(c.bt, c.nb, s->stride, s->K, s->first, s->rows, W.ctrl, is));
+        if (!(clean || kept)) HIPCHK(hipMemsetAsync(W.rowflag, 0, (size_t)s->rows * sizeof(uint32_t), is));
+        if (c.spec)
+            HIPCHK(launch_ident_check(c.bt, c.nb, s->stride, s->K, s->first, s->rows, W.slot, W.ctrl, is));
         HIPCHK(launch_index(c.bt, c.nb, c.max_nrec, s->stride, s->K, s->first, s->rows, W.slot, W.rowflag, W.ctrl,
                             c.tail_cut, is));
     } else {
@@ -603,6 +617,9 @@ void set_buffers(dml_store* s, Chunk& c, void* in) {
 int rerun_unspeculated(dml_store* s, Chunk& c, Workspace& W, Ctrl* ctl) {
     c.spec = false;
     c.bt.spec = 0;
+    c.keeps = false;
+    c.bt.reuse = 0;
+    c.bt.keeps = 0;
     c.bt.prev = nullptr;
     set_buffers(s, c, s->data);
     HIPCHK(hipMemsetAsync(W.base, 0xFF, sizeof(Ctrl) + s->slot_bytes, s->stream));
@@ -635,6 +652,12 @@ int retire_front(dml_store* s) {
     W.clean = s->is_matrix && !abnormal && W.clears;
     if (c.spec && ctl.spec_ok != 0u) {
         std::swap(s->data, s->data_alt);  // every identity record verified: the output is the shard
+        if (c.keeps) {  // the reduce left the slot table as built: the next chunk here may reuse it
+            W.clean = false;
+            W.kept = true;
+            W.kept_nb = c.nb;
+            W.perm = (~ctl.ident | c.bt.reuse) & (c.nb >= 64 ? ~0ull : (1ull << c.nb) - 1ull);
+        }
     } else if (c.spec) {
         // An identity push was not (or the chunk met a cutoff / repeated row): the
         // output is discarded and the chunk re-runs exactly, in place on its input
@@ -767,6 +790,17 @@ int run_batch(dml_store* s, const uint8_t* const* dptr, const int64_t* lens, int
             c.spec = full && s->data_alt;
         }
         c.bt.spec = c.spec ? 1 : 0;
+        // Slot reuse: a speculative chunk reduced by k_reduce_rows may take
+        // a push's slots from the column its workspace kept for the push at the same
+        // position, when that push's sampled keys match it (k_ident_check)
+        c.bt.reuse = 0;
+        c.keeps = c.spec && !use_flat(vtype_of(s->desc), reduce_mode(s), s->cols, c.bt, c.nb, s->rows);
+        c.bt.keeps = c.keeps ? 1 : 0;
+        if (c.keeps) {
+            const Workspace& Wn = s->ws[s->next_ws];
+            if (Wn.kept && slot_stride(Wn.kept_nb) == slot_stride(c.nb))
+                c.bt.reuse = Wn.perm & (c.nb >= 64 ? ~0ull : (1ull << c.nb) - 1ull);
+        }
         c.bt.first = s->first;
         const Ctrl* prev = s->pend.empty() ? nullptr : s->ws[s->pend.back().w].ctrl;
         set_buffers(s, c, s->pend.empty() ? s->data : s->pend.back().c.out);

@@ -1427,3 +1427,75 @@ def test_adagrad_flat_exact(oracle, case, W, cols):
     assert kat.bits_equal(a, o.alpha) and kat.bits_equal(d, o.delta)
     assert s.maxDelta() == o.max_delta()
     s.close()
+
+
+@pytest.mark.parametrize("cols", [1024, 256])
+@pytest.mark.parametrize("case", ["same_order", "swapped_late", "duplicate_late", "out_of_shard_late", "order_change",
+                                  "nb_change"])
+def test_slot_reuse_exact(oracle, case, cols):
+    """Slot reuse: a speculative k_reduce_rows chunk keeps its slot
+    table, and the chunk three batches later in the same workspace takes a push's
+    slots from the column of the push at the same position when its sampled keys
+    match (k_ident_check); the reduce verifies every record's key and a mismatch
+    re-runs the chunk exactly. Seven batches of six full-range permuted pushes (new
+    values each batch), bit-exact against the oracle, error state included. Batch 3
+    (the first that can reuse) varies by case: the same orders; push 2 with two
+    records swapped where the sample cannot see them; with a row listed twice; with
+    an out-of-shard key there; all new orders (batch 6 then repeats batch 3's); nine
+    pushes (another slot-table stride, no reuse)."""
+    from distml_amd import DataDesc, DataStore, KeyRange, encode_matrix_push, ArrayIndexOutOfBoundsException
+    rows, W = 4000, 6
+    fmt = DataDesc(1, 0, 1)
+    rng = np.random.default_rng(len(case) * 7 + cols)
+    st = DataStore(fmt, KeyRange(100, 100 + rows - 1), cols, async_push=True)
+    o = oracle_store(oracle, fmt, 100, 100 + rows - 1, cols)
+    init = rng.standard_normal((rows, cols)).astype(np.float32)
+    st.load_values(init)
+    o.data[:] = init
+    perms = [rng.permutation(rows) for _ in range(9)]
+    new_perms = [rng.permutation(rows) for _ in range(9)]
+    err = raised = None
+    keep = []
+    for bi in range(7):
+        n = 9 if (case == "nb_change" and bi == 3) else W
+        order = new_perms if (case == "order_change" and bi in (3, 6)) else perms
+        host = []
+        for b in range(n):
+            keys = order[b].copy()
+            if bi == 3 and b == 2 and case.endswith("_late"):
+                free = sorted(set(range(rows)) - _sampled_rows(oracle, b, rows))
+                i, j = free[len(free) // 2], free[len(free) // 2 + 3]
+                if case == "swapped_late":
+                    keys[i], keys[j] = keys[j], keys[i]
+                elif case == "duplicate_late":
+                    keys[i] = keys[j]
+                else:
+                    keys[i] = rows + 11  # key - first outside the shard
+            v = (rng.standard_normal((rows, cols)) * 1e-3).astype(np.float32)
+            host.append(np.frombuffer(encode_matrix_push(keys + 100, v, 0, 1), np.uint8).copy())
+        dev = [torch.from_numpy(h).cuda() for h in host]
+        keep.append(dev)
+        torch.cuda.synchronize()
+        try:
+            st.pushDevice([d.data_ptr() for d in dev], [d.numel() for d in dev])
+        except ArrayIndexOutOfBoundsException as e:  # an earlier batch's error, surfaced at retire
+            assert err is not None
+            raised = e
+            break
+        if err is None:
+            for h in host:
+                if o.push(h.tobytes()):
+                    err = o.error()
+                    break
+    if err is None:
+        st.flush()
+    elif raised is None:
+        with pytest.raises(ArrayIndexOutOfBoundsException) as ei:
+            st.flush()
+        raised = ei.value
+    if err is not None:
+        assert (raised.key, raised.col) == (err[1], err[2])
+    got = st.values()
+    bad_rows = np.nonzero((got.view(np.uint32) != o.data.view(np.uint32)).any(axis=1))[0]
+    assert len(bad_rows) == 0, (len(bad_rows), bad_rows[:8])
+    st.close()
