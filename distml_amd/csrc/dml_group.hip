@@ -286,6 +286,23 @@ int dml_group_push_exchange(dml_group* g, const void* const* dev_bufs, const int
     const int64_t K = g->desc.key_type == 0 ? 4 : 8;
     const int64_t stride = g->desc.data_type == DML_DATA_TYPE_MATRIX ? K + (int64_t)g->vbytes * g->cols
                                                                       : K + (int64_t)g->vbytes;
+    if (W == 1 && n > 0) {
+        // one owner and every key inside the matrix: the split would copy each push whole
+        // and nothing crosses a link, so the store takes the pushes themselves (they stay
+        // valid until dml_group_flush, the group's contract)
+        std::vector<int64_t> cnt((size_t)n);
+        GRC(dml_shard_split(&g->desc, g->cols, g->total_rows, 1, dev_bufs, lens, n, nullptr, 0, cnt.data(),
+                            g->cstream));
+        bool whole = true;
+        for (int b = 0; b < n; ++b) whole = whole && cnt[(size_t)b] * stride == lens[b];
+        if (whole) {
+            if (g->xheld) {  // the previous exchange call's slices come first
+                GHIP(hipStreamSynchronize(g->rstream));
+                GRC(hand_over(g));
+            }
+            return dml_store_push_batch_device(g->store, dev_bufs, lens, n);
+        }
+    }
     // Pipelined over calls (two buffer sets): this call's split runs while the
     // previous call's all-to-all moves its slices; the previous slices reach the
     // store once this call's count exchange (queued behind that all-to-all on the

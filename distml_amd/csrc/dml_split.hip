@@ -219,9 +219,10 @@ extern "C" int dml_shard_split(const dml_desc* desc, int32_t cols, int64_t total
                 hbase[(size_t)(b * world + d)] = run;
                 run += c;
             }
-        if (run * stride > out_cap) rc = set_error(DML_E_CAPACITY, "split output buffer too small");
+        if (dev_out && run * stride > out_cap) rc = set_error(DML_E_CAPACITY, "split output buffer too small");
     }
-    if (rc == DML_OK && hip(hipMemcpyAsync(dbase, hbase.data(), base_bytes, hipMemcpyHostToDevice, st), "H2D")) {
+    if (rc == DML_OK && dev_out &&
+        hip(hipMemcpyAsync(dbase, hbase.data(), base_bytes, hipMemcpyHostToDevice, st), "H2D")) {
         hipLaunchKernelGGL(k_split_scatter, dim3((unsigned)nblk, (unsigned)n), dim3(kSplitBlock), 0, st, bt, stride, K,
                            total_rows, step, world, nblk, blkoff, dbase, (uint8_t*)dev_out);
         hip(hipGetLastError(), "k_split_scatter");

@@ -245,11 +245,20 @@ class ShardGroup:
         exchange call (once its count exchange, queued behind the previous data
         exchange, has completed) or at flush(), so this call's split overlaps the
         previous all-to-all and the store's apply overlaps this call's all-to-all.
-        The caller's push buffers are free when the call returns (the split copied them)."""
+        The push buffers follow the module's contract (allocated and unmodified until
+        flush()): at world 1 with every key inside the matrix they go to the store as they
+        are, since the split would copy each push whole and nothing crosses a link."""
         torch, dist = self.torch, self.dist
         n, world = len(dev_ptrs), self.world
         stride = self.record_stride()
         dev = self.partial.device
+        if world == 1 and n and self.partial.is_cuda and self._whole_shard(dev_ptrs, lens, stride):
+            # one owner and every key inside the matrix: the split would copy each push
+            # whole and nothing crosses a link, so the store takes the pushes themselves
+            # (they stay allocated and unmodified until flush(), the module's contract)
+            self._hand_over()
+            self.store.pushDevice(list(dev_ptrs), list(lens))
+            return
         cap = int(sum(lens))
         send = self._xalloc(max(cap, 1), dev)
         st = torch.cuda.current_stream(dev).cuda_stream if send.is_cuda else 0
@@ -293,6 +302,12 @@ class ShardGroup:
                 off += ln
         # held until the next call / flush; `send` stays alive until the exchange ran
         self._held = (ptrs, ls, recv, send)
+
+    def _whole_shard(self, dev_ptrs, lens, stride) -> bool:
+        """World 1: every record's key lies in [0, total_rows) (dml_shard_split, counts only)."""
+        st = self.torch.cuda.current_stream(self.partial.device).cuda_stream
+        counts = self.ops.split(self.fmt, self.cols, self.total_rows, 1, list(dev_ptrs), list(lens), 0, 0, st)
+        return all(counts[b][0] * stride == int(lens[b]) for b in range(len(lens)))
 
     def _hand_over(self) -> None:
         """Push the last exchange call's received slices into the store (asynchronous

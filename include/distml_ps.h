@@ -248,7 +248,8 @@ int dml_prereduce_kernel_time(double* ms, int64_t* launches, int32_t reset);
  * counts[b*world + d] (host, n*world) receives the record count of push b for
  * dest d. Keys outside [0, total_rows) are dropped (the client's p.contains(k)).
  * Kernels run on `stream`; the call returns when dev_out is written.
- * DML_E_CAPACITY when out_cap is smaller than the kept bytes; world <= 64, n <= 64. */
+ * DML_E_CAPACITY when out_cap is smaller than the kept bytes; world <= 64, n <= 64.
+ * dev_out == NULL: counts only (nothing is copied). */
 int dml_shard_split(const dml_desc* desc, int32_t cols, int64_t total_rows, int32_t world,
                     const void* const* dev_bufs, const int64_t* lens, int32_t n, void* dev_out,
                     int64_t out_cap, int64_t* counts, void* stream);

@@ -827,12 +827,14 @@ def test_shard_split_rejects_partial_records():
         HipOps().split(DataDesc(1, 0, 1), 200, 100, 2, [d.data_ptr()], [805], d.data_ptr(), 805, 0)
 
 
-@pytest.mark.parametrize("calls", [1, 4])
+@pytest.mark.parametrize("calls", [1, 4, "mixed"])
 def test_exchange_rccl_world1_adagrad(oracle, calls):
     """ShardGroup.push_exchange at world 1 over RCCL: dml_shard_split, the all-to-all
     and the ordered AdaGrad apply; bit-exact (data, alpha, delta, maxDelta). With 4
     calls of different sizes back to back (no flush between), the pooled send /
-    receive buffers are reused across calls of other sizes."""
+    receive buffers are reused across calls of other sizes. `mixed`: pushes 0 and 3
+    hold only keys inside the matrix, so calls 1 and 3 hand their pushes to the
+    store as they are and calls 2 and 4 split, in one ordered sequence."""
     import socket
     import torch.distributed as dist
     from distml_amd import DataDesc, encode_matrix_push
@@ -846,17 +848,21 @@ def test_exchange_rccl_world1_adagrad(oracle, calls):
     try:
         rows, cols, W = 3000, 200, 5
         fmt = DataDesc(1, 0, 1, False, True, True)
-        g = ShardGroup(fmt, rows, cols, 0, 1, device=0, exchange_only=calls > 1)
+        g = ShardGroup(fmt, rows, cols, 0, 1, device=0, exchange_only=calls != 1)
         g.store.setAlpha(0.025, 0.0001, 1.5)
         rng = np.random.default_rng(77)
         host = []
         for b in range(W):
             keys = rng.permutation(rows + 50)[: rows // 2] - 25  # some keys outside the matrix: dropped
+            if calls == "mixed" and b in (0, 3):
+                keys = rng.permutation(rows)[: rows // 2]
             vals = (rng.standard_normal((len(keys), cols)) * 0.6).astype(np.float32)
             host.append(encode_matrix_push(keys, vals, 0, 1))
         dev = [torch.frombuffer(bytearray(h), dtype=torch.uint8).cuda() for h in host]
         torch.cuda.synchronize()
         cuts = [0, W] if calls == 1 else [0, 1, 3, 4, W]
+        if calls == "mixed":
+            torch.cuda.synchronize()
         for c0, c1 in zip(cuts, cuts[1:]):
             g.push_exchange([d.data_ptr() for d in dev[c0:c1]], [d.numel() for d in dev[c0:c1]])
         g.flush()
