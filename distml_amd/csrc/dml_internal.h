@@ -62,6 +62,11 @@ struct Batch {
     // verifies the record of every row of every push instead (all pushes are
     // full-range, so a repeat leaves another row without its record).
     int32_t keeps;
+    // 1: the Ctrl::ident pushes were verified record by record before this launch
+    // (k_ident_full; the sharded pre-reduce, whose partial the reduce-scatter takes
+    // before a speculative verdict could be read): the reduce takes slot = row for
+    // them and verifies nothing.
+    int32_t ident_ok;
 };
 
 // A chunk whose predecessor ended abnormally (error, rows to replay, or a failed
@@ -138,6 +143,10 @@ hipError_t launch_index(const Batch& bt, int nb, int64_t max_nrec, int64_t strid
 // every sampled record r of it has row_index(key) == r (Ctrl reset to all ones).
 hipError_t launch_ident_check(const Batch& bt, int nb, int64_t stride, int K, int64_t first, int64_t rows,
                               const int32_t* slot, Ctrl* ctrl, hipStream_t st);
+// Complete identity check (Ctrl::ident reset to all ones, or as k_ident_check left
+// it): clears ctrl->ident bit b unless every record r of push b has row_index(key) == r.
+hipError_t launch_ident_full(const Batch& bt, int nb, int64_t max_nrec, int64_t stride, int K, int64_t first,
+                             int64_t rows, Ctrl* ctrl, hipStream_t st);
 hipError_t launch_reduce(int vtype, int mode, void* shard, int64_t rows, int32_t cols, const Batch& bt,
                          int nb, int64_t stride, int K, const int32_t* slot, const uint32_t* rowflag, Ctrl* ctrl,
                          uint64_t tail_cut, const AdaArgs& ada, hipStream_t st, int64_t* nblocks_out,

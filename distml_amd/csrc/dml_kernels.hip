@@ -68,7 +68,8 @@ __global__ __launch_bounds__(256) void k_index(const Batch bt, int64_t stride, i
     const int64_t r = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (r == 0 && b == 0 && tail_cut != kNoPos) atomicMin(&ctrl->cutoff, (unsigned long long)tail_cut);
     if (r >= bt.nrec[b]) return;
-    if (bt.spec && ((ctrl->ident >> b) & 1ull)) return;  // identity push: the reduce verifies its keys
+    // identity push: the reduce verifies its keys (spec), or k_ident_full did (ident_ok)
+    if ((bt.spec || bt.ident_ok) && ((ctrl->ident >> b) & 1ull)) return;
     const int64_t off = r * stride;
     const int64_t key = ld_key(bt.base[b] + off, K);
     const int64_t idx = row_index(key, first, rows);
@@ -113,6 +114,25 @@ hipError_t launch_ident_check(const Batch& bt, int nb, int64_t stride, int K, in
                               const int32_t* slot, Ctrl* ctrl, hipStream_t st) {
     if (nb <= 0) return hipSuccess;
     hipLaunchKernelGGL(k_ident_check, dim3((unsigned)nb), dim3(64), 0, st, bt, stride, K, first, rows, slot, ctrl);
+    return hipGetLastError();
+}
+
+// k_ident_full: one thread per record of a push still marked identity; any record r
+// whose key is not row r clears the push's bit (the push's later blocks then stop
+// at the bit).
+__global__ __launch_bounds__(256) void k_ident_full(const Batch bt, int64_t stride, int K, int64_t first, int64_t rows,
+                                                    Ctrl* __restrict__ ctrl) {
+    const int b = blockIdx.y;
+    const int64_t r = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (r >= bt.nrec[b] || !((ctrl->ident >> b) & 1ull)) return;
+    if (row_index(ld_key(bt.base[b] + r * stride, K), first, rows) != r)
+        atomicAnd(&ctrl->ident, ~(1ull << b));
+}
+hipError_t launch_ident_full(const Batch& bt, int nb, int64_t max_nrec, int64_t stride, int K, int64_t first,
+                             int64_t rows, Ctrl* ctrl, hipStream_t st) {
+    if (nb <= 0 || max_nrec <= 0) return hipSuccess;
+    dim3 grid((unsigned)((max_nrec + 255) / 256), (unsigned)nb);
+    hipLaunchKernelGGL(k_ident_full, grid, dim3(256), 0, st, bt, stride, K, first, rows, ctrl);
     return hipGetLastError();
 }
 
@@ -542,6 +562,8 @@ __global__ __launch_bounds__(64 * WPB) void k_reduce_rows(T* __restrict__ shard,
             ident = ctrl->ident;
         }
     }
+    if constexpr (MODE == kPreReduce)
+        if (bt.ident_ok) ident = ctrl->ident;  // verified before the launch: slot = row, no key checks
 
     if (cut != kNoPos) {
         // Error batch: element-wise RMW of the wave's rows in place, pushes in order,
@@ -885,6 +907,8 @@ __global__ __launch_bounds__(256) void k_reduce_flat(T* __restrict__ shard, int6
             ident = ctrl->ident;
         }
     }
+    if constexpr (MODE == kPreReduce)
+        if (bt.ident_ok) ident = ctrl->ident;  // verified before the launch (k_ident_full)
     const int NV = cols / VEC;
     const int nrow = (int)(rows - t0 < (int64_t)R ? rows - t0 : (int64_t)R);
     const int ss = slot_stride(nb);

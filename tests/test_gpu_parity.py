@@ -1505,3 +1505,43 @@ def test_slot_reuse_exact(oracle, case, cols):
     bad_rows = np.nonzero((got.view(np.uint32) != o.data.view(np.uint32)).any(axis=1))[0]
     assert len(bad_rows) == 0, (len(bad_rows), bad_rows[:8])
     st.close()
+
+
+@pytest.mark.parametrize("rows,cols", [(3000, 1024), (2_200_000, 4), (2_200_000, 256)])
+@pytest.mark.parametrize("case", ["ascending", "swapped", "rotated"])
+def test_prereduce_verified_identity(case, rows, cols):
+    """The sharded pre-reduce's identity pushes (dml_prereduce_begin): when the slot
+    table is beyond the caches (rows x stride x 4 B > 64 MB: the 2.2 M-row cases),
+    full-range pushes whose records are rows in order skip the key index after a
+    complete key check, and the pieces take slot = row for them; the 3 000-row case
+    keeps the index. The partial equals the ordered float32 sum of the pushes from
+    zero, bit for bit: ascending pushes; push 1 with two records swapped (the check
+    sends it to the index); push 1 rotated by one record. Rows of 16 B
+    (k_reduce_flat) and 1 KiB (k_reduce_rows)."""
+    from distml_amd import DataDesc, encode_matrix_push
+    from distml_amd.group import HipOps
+    W = 2
+    fmt = DataDesc(1, 0, 1)
+    rng = np.random.default_rng(len(case) + cols)
+    expect = np.zeros((rows, cols), np.float32)
+    dev = []
+    for b in range(W):
+        keys = np.arange(rows)
+        if b == 1 and case == "swapped":
+            i, j = rows // 3, rows // 3 + 11
+            keys[i], keys[j] = keys[j], keys[i]
+        elif b == 1 and case == "rotated":
+            keys = np.roll(keys, 1)
+        v = rng.standard_normal((rows, cols), dtype=np.float32)
+        expect[keys] += v  # float32: one IEEE rounding per add, push order
+        dev.append(torch.frombuffer(bytearray(encode_matrix_push(keys, v, 0, 1)), dtype=torch.uint8).cuda())
+        del v
+    out = torch.full((rows * cols,), 7.0, dtype=torch.float32, device="cuda")
+    torch.cuda.synchronize()
+    ops = HipOps()
+    st = torch.cuda.current_stream().cuda_stream
+    h = ops.begin(fmt, 0, rows, cols, [d.data_ptr() for d in dev], [d.numel() for d in dev], st)
+    ops.piece(h, rows, rows, 0, rows, out.data_ptr(), st)
+    torch.cuda.synchronize()
+    ops.end(h)
+    assert out.cpu().numpy().reshape(rows, cols).tobytes() == expect.tobytes()
