@@ -1065,6 +1065,8 @@ __global__ __launch_bounds__(256) void k_ada_flat(float* __restrict__ shard, int
         const int nrow = (int)(rows - t0 < (int64_t)R ? rows - t0 : (int64_t)R);
         const int ss = slot_stride(nb);
         int32_t* const ls = s_slot[wid];
+        // identity pushes checked record by record before the launch (Batch::ident_ok)
+        const uint64_t ident = bt.ident_ok ? ctrl->ident : 0ull;
         // the wave's slot rows into LDS, handed back clean (-1) for the next batch;
         // rows a push repeats stay -1 here (the host replays them exactly)
         for (int e = lane; e < nrow * nb; e += 64) {
@@ -1072,8 +1074,12 @@ __global__ __launch_bounds__(256) void k_ada_flat(float* __restrict__ shard, int
             const int64_t r = t0 + rl;
             int32_t v = -1;
             if (!(rowflag && rowflag[r])) {
-                v = slot[r * ss + b];
-                slot[r * ss + b] = -1;
+                if ((ident >> b) & 1ull) {
+                    v = r < bt.nrec[b] ? (int32_t)r : -1;  // record = row; the index skipped it
+                } else {
+                    v = slot[r * ss + b];
+                    slot[r * ss + b] = -1;
+                }
             }
             ls[rl * kMaxW + b] = v;
         }

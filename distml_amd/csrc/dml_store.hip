@@ -420,6 +420,21 @@ int launch_chunk(dml_store* s, Chunk& c, Workspace& W, const Ctrl* prev) {
         if (!(clean || kept)) HIPCHK(hipMemsetAsync(W.rowflag, 0, (size_t)s->rows * sizeof(uint32_t), is));
         if (c.spec)
             HIPCHK(launch_ident_check(c.bt, c.nb, s->stride, s->K, s->first, s->rows, W.slot, W.ctrl, is));
+        // AdaGrad chunks of k_ada_flat (no speculation: the apply cannot be undone):
+        // full-range pushes whose records are rows in order skip the key index after a
+        // complete key check, when the slot table is beyond the caches (its atomics go
+        // to DRAM; see dml_prereduce_begin)
+        c.bt.ident_ok = 0;
+        if (s->adagrad && c.tail_cut == kNoPos &&
+            (int64_t)s->rows * slot_stride(c.nb) * 4 > ((int64_t)64 << 20) &&
+            use_flat(vtype_of(s->desc), reduce_mode(s), s->cols, c.bt, c.nb, s->rows)) {
+            bool full = c.nb > 0;
+            for (int j = 0; j < c.nb && full; ++j) full = c.bt.nrec[j] == s->rows;
+            if (full) {
+                HIPCHK(launch_ident_full(c.bt, c.nb, c.max_nrec, s->stride, s->K, s->first, s->rows, W.ctrl, is));
+                c.bt.ident_ok = 1;
+            }
+        }
         HIPCHK(launch_index(c.bt, c.nb, c.max_nrec, s->stride, s->K, s->first, s->rows, W.slot, W.rowflag, W.ctrl,
                             c.tail_cut, is));
     } else {

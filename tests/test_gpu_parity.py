@@ -1545,3 +1545,50 @@ def test_prereduce_verified_identity(case, rows, cols):
     torch.cuda.synchronize()
     ops.end(h)
     assert out.cpu().numpy().reshape(rows, cols).tobytes() == expect.tobytes()
+
+
+@pytest.mark.parametrize("case", ["ascending", "rotated", "out_of_shard"])
+def test_adagrad_identity_checked_large(oracle, case):
+    """AdaGrad chunks of k_ada_flat with a slot table beyond the caches (2.2 M rows):
+    full-range pushes whose records are rows in order skip the key index after a
+    complete key check (Batch::ident_ok); bit-exact data, alpha, delta, maxDelta and
+    error state against the oracle. `rotated`: push 1 rotated by one record (the check
+    sends it to the index); `out_of_shard`: push 1's record 1 000 000 holds a key
+    outside the shard (ArrayIndexOutOfBoundsException state)."""
+    from distml_amd import DataDesc, encode_matrix_push, ArrayIndexOutOfBoundsException
+    rows, cols, W = 2_200_000, 8, 2
+    fmt = DataDesc(1, 0, 1, False, True, True)
+    rng = np.random.default_rng(len(case))
+    s, _ = mk_store(fmt, 0, rows - 1, cols)
+    o = oracle_store(oracle, fmt, 0, rows - 1, cols)
+    s.setAlpha(0.025, 0.0001, 1.5)
+    o.set_alpha(0.025, 0.0001, 1.5)
+    init = rng.standard_normal((rows, cols)).astype(np.float32)
+    s.load_values(init)
+    o.data[:] = init
+    pushes = []
+    for b in range(W):
+        keys = np.arange(rows)
+        if b == 1 and case == "rotated":
+            keys = np.roll(keys, 1)
+        if b == 1 and case == "out_of_shard":
+            keys = keys.copy()
+            keys[1_000_000] = rows + 5
+        v = (rng.standard_normal((rows, cols)) * 0.8).astype(np.float32)  # delta passes 1 for some elements
+        pushes.append(encode_matrix_push(keys, v, 0, 1))
+    err = None
+    for p in pushes:
+        if o.push(p):
+            err = o.error()
+            break
+    if err is None:
+        s.handlePushBatch(fmt, pushes)
+    else:
+        with pytest.raises(ArrayIndexOutOfBoundsException):
+            s.handlePushBatch(fmt, pushes)
+        assert s.error_state() == (err[0], err[1], err[2])
+    assert kat.bits_equal(s.values(), o.data)
+    a, d = s.adagrad_state()
+    assert kat.bits_equal(a, o.alpha) and kat.bits_equal(d, o.delta)
+    assert s.maxDelta() == o.max_delta()
+    s.close()
