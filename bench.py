@@ -229,14 +229,14 @@ def _sparse_perm(b, dim):
 
 
 # ---------------------------------------------------------------- config 2
-def make_buckets(L, torch, fmt, n, rows_total):
+def make_buckets(L, torch, fmt, n, rows_total, value_seed: int = 1000):
     st = torch.cuda.current_stream().cuda_stream
     bufs = []
     for b in range(n):
         t = torch.empty(rows_total * REC, dtype=torch.uint8, device="cuda")
         pa, pc = perm_for(b)
         rc = L.dml_synth_dense_bucket(t.data_ptr(), C.byref(fmt.to_c()), 0, rows_total, rows_total, COLS,
-                                      1000 + b, pa % rows_total, pc % rows_total, C.c_void_p(st))
+                                      value_seed + b, pa % rows_total, pc % rows_total, C.c_void_p(st))
         assert rc == 0, rc
         bufs.append(t)
     torch.cuda.synchronize()
@@ -287,25 +287,31 @@ def headline(ctx: Ctx, L, args, out_line: dict):
     if not sharded:
         store = DataStore(fmt, KeyRange(0, ROWS - 1), COLS, device=ctx.local)
         store.synth_fill(7)
-        bufs = make_buckets(L, torch, fmt, W, ROWS)
-        batch = DeviceBatch([b.data_ptr() for b in bufs], [b.numel() for b in bufs])
+        # two bucket sets, stepped alternately: the same key order per push position
+        # (a worker pushing the same key set), different gradient values every step
+        bufs = make_buckets(L, torch, fmt, W, ROWS) + make_buckets(L, torch, fmt, W, ROWS, value_seed=5000)
+        batches = [DeviceBatch([b.data_ptr() for b in bs], [b.numel() for b in bs]) for bs in (bufs[:W], bufs[W:])]
+        k_step = [0]
 
         def step():
             # async: ack once captured; the store keeps <= 2 batches in flight and the
             # key index of batch k+1 overlaps the reduce of batch k
-            store.pushDevice(batch)
+            store.pushDevice(batches[k_step[0] & 1])
+            k_step[0] += 1
 
         finish = store.flush  # every pushed batch applied and error-checked
         timed_store = store
         algo_per_rank = W * BUCKET + 2 * SHARD
     else:
         group = ShardGroup(fmt, ROWS, COLS, rank, world, device=ctx.local, pieces=args.pieces)
-        bufs = make_buckets(L, torch, fmt, W, ROWS)
-        ptrs, lens = [b.data_ptr() for b in bufs], [b.numel() for b in bufs]
+        bufs = make_buckets(L, torch, fmt, W, ROWS) + make_buckets(L, torch, fmt, W, ROWS, value_seed=5000)
+        sets = [([b.data_ptr() for b in bs], [b.numel() for b in bs]) for bs in (bufs[:W], bufs[W:])]
         st = torch.cuda.current_stream().cuda_stream
+        k_step = [0]
 
         def step():
-            group.push_full_range(ptrs, lens, st)
+            group.push_full_range(*sets[k_step[0] & 1], st)
+            k_step[0] += 1
 
         finish = group.flush
         timed_store = group.store
@@ -337,6 +343,8 @@ def headline(ctx: Ctx, L, args, out_line: dict):
                                "([int32 key][1024 x f32] x 16384) -> 16384x1024 fp32 model per GPU",
                    "pushes_per_gpu": W, "push_bytes": BUCKET, "model_rows": ROWS, "cols": COLS,
                    "parallelism": ("single shard" if not sharded else f"linearSplit({world}) + RCCL reduce-scatter"),
+                   "pushes": "16 ascending + 16 permuted per step; two bucket sets stepped alternately "
+                             "(same key order per push position, different values)",
                    "algorithmic_bytes_per_step_per_gpu": algo_per_rank},
     })
     if not sharded and k_n > 0:
