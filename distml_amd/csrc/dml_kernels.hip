@@ -925,11 +925,12 @@ __global__ __launch_bounds__(256) void k_reduce_flat(T* __restrict__ shard, int6
         const int64_t mr = model_row(t0 + rl);
         int32_t v = -1;
         if (!(rm.block && mr >= rm.rows_total) && !(rowflag && rowflag[mr])) {
-            if ((ident >> b) & 1ull) {  // identity push: record = row (the index skipped it)
+            if (((ident >> b) & 1ull) && !((bt.reuse >> b) & 1ull)) {  // identity push: record = row
                 v = mr < bt.nrec[b] ? (int32_t)mr : -1;
             } else {
                 v = slot[mr * ss + b];
-                slot[mr * ss + b] = -1;
+                // a speculative chunk keeps its table (Batch::reuse, see k_reduce_rows)
+                if (!bt.spec) slot[mr * ss + b] = -1;
             }
         }
         ls[rl * kMaxW + b] = v;
@@ -998,8 +999,12 @@ __global__ __launch_bounds__(256) void k_reduce_flat(T* __restrict__ shard, int6
                 const int b = b0 + p < nb ? b0 + p : nb - 1;
                 const uint8_t* const bp = bt.base[b];
                 if constexpr (MODE == kAdd) {
-                    const bool kl = b0 + p < nb && ((ident >> b) & 1ull) && lane < nrow;
-                    kv[p] = kl ? ld_key(bp + (t0 + lane) * stride, K) : bt.first + t0 + lane;
+                    // verified pushes (identity, reused, or every push of a slot-keeping
+                    // chunk): lane l < nrow loads the key of row t0+l's record
+                    const bool kl = b0 + p < nb && (bt.keeps || ((ident >> b) & 1ull)) && lane < nrow;
+                    const int32_t kr = kl ? ls[lane * kMaxW + b] : 0;
+                    kv[p] = !kl ? bt.first + t0 + lane
+                                : kr >= 0 ? ld_key(bp + (int64_t)kr * stride, K) : bt.first - 1;  // no record: fails
                 }
 #pragma unroll
                 for (int j = 0; j < JMAX; ++j) {
@@ -1020,7 +1025,7 @@ __global__ __launch_bounds__(256) void k_reduce_flat(T* __restrict__ shard, int6
                     for (int e = 0; e < VEC; ++e) acc[j][e] = Elem<T>::add(acc[j][e], u[e]);
                 }
             if constexpr (MODE == kAdd)
-                if (ident)
+                if (ident || bt.keeps)
 #pragma unroll
                     for (int p = 0; p < PB; ++p)
                         bad |= lane < nrow && row_index(kv[p], bt.first, rows) != t0 + lane;

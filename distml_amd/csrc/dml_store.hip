@@ -809,7 +809,7 @@ int run_batch(dml_store* s, const uint8_t* const* dptr, const int64_t* lens, int
         // a push's slots from the column its workspace kept for the push at the same
         // position, when that push's sampled keys match it (k_ident_check)
         c.bt.reuse = 0;
-        c.keeps = c.spec && !use_flat(vtype_of(s->desc), reduce_mode(s), s->cols, c.bt, c.nb, s->rows);
+        c.keeps = c.spec;
         c.bt.keeps = c.keeps ? 1 : 0;
         if (c.keeps) {
             const Workspace& Wn = s->ws[s->next_ws];

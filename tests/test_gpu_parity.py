@@ -1435,7 +1435,7 @@ def test_adagrad_flat_exact(oracle, case, W, cols):
     s.close()
 
 
-@pytest.mark.parametrize("cols", [1024, 256])
+@pytest.mark.parametrize("cols", [1024, 256, 200])
 @pytest.mark.parametrize("case", ["same_order", "swapped_late", "duplicate_late", "out_of_shard_late", "order_change",
                                   "nb_change"])
 def test_slot_reuse_exact(oracle, case, cols):
@@ -1448,7 +1448,8 @@ def test_slot_reuse_exact(oracle, case, cols):
     (the first that can reuse) varies by case: the same orders; push 2 with two
     records swapped where the sample cannot see them; with a row listed twice; with
     an out-of-shard key there; all new orders (batch 6 then repeats batch 3's); nine
-    pushes (another slot-table stride, no reuse)."""
+    pushes (another slot-table stride, no reuse). Rows of whole KiB (k_reduce_rows)
+    and of 800 B (k_reduce_flat)."""
     from distml_amd import DataDesc, DataStore, KeyRange, encode_matrix_push, ArrayIndexOutOfBoundsException
     rows, W = 4000, 6
     fmt = DataDesc(1, 0, 1)
