@@ -51,7 +51,7 @@ struct Batch {
     const void* src;      // input shard (null: in place)
     int64_t first;        // key of row 0 (KeyRange first), for the verification
     int32_t spec;         // 1: speculative chunk
-    // Slot reuse (speculative chunks reduced by k_reduce_rows): bit b = push b's
+    // Slot reuse (speculative chunks): bit b = push b's
     // column of the workspace's slot table still holds the permutation the push at
     // position b of the workspace's previous chunk listed. A push whose sampled keys
     // match it skips the key index; the reduce reads its slots from the table and

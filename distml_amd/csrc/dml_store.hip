@@ -67,7 +67,7 @@ struct Chunk {
     SpPlan sp{};
     SpLayout spl{};
     bool spec = false;     // identity speculation (full-range plain-sum chunk, Batch::spec)
-    bool keeps = false;    // speculative chunk reduced by k_reduce_rows: its slot table is kept (Batch::reuse)
+    bool keeps = false;    // speculative chunk: its slot table is kept for the next chunk here (Batch::reuse)
     void* in = nullptr;    // matrix shard the chunk reads (the previous chunk's output)
     void* out = nullptr;   // and writes: == in, or the other buffer of a speculative chunk
 };
@@ -96,8 +96,7 @@ struct Workspace {
     SpStat* hsp = nullptr;            // pinned status of the single-pass sparse partition
     bool clears = false;              // the chunk's reduce leaves its slot table all -1
     bool clean = false;               // slot table all -1 and rowflags 0: only the Ctrl needs a reset
-    // Kept slot table (the last chunk here was a verified speculative chunk reduced by
-    // k_reduce_rows): rowflags 0, and column b of [rows][slot_stride(kept_nb)] is the
+    // Kept slot table (the last chunk here was a verified speculative chunk): rowflags 0, and column b of [rows][slot_stride(kept_nb)] is the
     // permutation push b listed when bit b of `perm` is set (indexed or reused, not
     // identity); other columns hold no meaning
     bool kept = false;
@@ -410,10 +409,10 @@ int launch_chunk(dml_store* s, Chunk& c, Workspace& W, const Ctrl* prev) {
     // with the running reduce).
     const bool clean = W.clean, kept = W.kept;
     W.clean = W.kept = false;
-    // A speculative k_reduce_rows chunk needs no -1 table either: its pushes are
-    // full-range, so the index rewrites every row of each column it builds (a push
-    // that is no permutation fails the chunk, and the re-run starts from a memset),
-    // and identity / reused columns are not rebuilt.
+    // A speculative chunk after a kept table needs no -1 table either: its pushes
+    // are full-range, so the index rewrites every row of each column it builds (a
+    // push that is no permutation fails the chunk's verification, and the re-run
+    // starts from a memset), and identity / reused columns are not rebuilt.
     const bool slots_ok = clean || (kept && c.keeps);
     HIPCHK(hipMemsetAsync(W.base, 0xFF, sizeof(Ctrl) + (slots_ok ? 0 : s->slot_bytes), is));
     if (s->is_matrix) {
