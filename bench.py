@@ -68,6 +68,7 @@ HBM_PEAK_GBS = 8000.0                    # MI355X_MICROARCH.md: HBM3E 8.0 TB/s (
 
 C4_ROWS, C4_COLS = 10_000_000, 200       # Word2Vec rows (BASELINE config 4)
 C5_ROWS, C5_COLS, C5_W, C5_NNZ = 1_000_000, 1000, 32, 65536  # LDA word-topic counts (config 5)
+SHUFFLE_ORDERS = 64                      # seeded push orders of the headline's arrival-order sub-line
 
 
 # ---------------------------------------------------------------- launcher
@@ -252,17 +253,48 @@ def _pre_time(L, every: int, reset: bool):
     return ms.value, n.value
 
 
-def load_traffic(key: str = "config2"):
+# Device-code sources: a profile's counted bytes stand for the kernels built from these
+DEVICE_SOURCES = ("dml_device.h", "dml_internal.h", "dml_kernels.hip", "dml_sparse.hip", "dml_split.hip")
+
+
+def device_src_hash() -> str:
+    """sha256 (16 hex digits) of the device-code sources; scripts/gpu_prof.sh records it
+    with every profile, and a stored traffic figure counts only while it still matches."""
+    import hashlib
+    h = hashlib.sha256()
+    for f in DEVICE_SOURCES:
+        h.update(f.encode())
+        with open(os.path.join(ROOT, "distml_amd", "csrc", f), "rb") as fh:
+            h.update(fh.read())
+    return h.hexdigest()[:16]
+
+
+def _kernel_sig(name: str) -> str:
+    """rocprof's kernel name without "void " and the parameter list."""
+    n = name[5:] if name.startswith("void ") else name
+    return n.split("(", 1)[0].strip()
+
+
+def traffic_for(key: str, kernel_ran: str) -> dict:
+    """roofline.traffic from profiles/pmc_traffic.json (PMC FETCH_SIZE / WRITE_SIZE per
+    dispatch), only when the stored entry profiled the same kernel instantiation that
+    ran here (dml_store_kernel_name) from the same device sources; otherwise
+    traffic = null and traffic_stale says why."""
     p = os.path.join(ROOT, "profiles", "pmc_traffic.json")
-    if not os.path.exists(p):
-        return None
     try:
-        d = json.load(open(p))
+        e = (json.load(open(p)).get("per_config") or {}).get(key)
     except Exception:
-        return None
-    if key == "config2":
-        return d.get("hbm_bytes_per_launch")
-    return (d.get("per_config") or {}).get(key, {}).get("hbm_bytes_per_launch")
+        e = None
+    if not e:
+        return {"traffic": None, "traffic_stale": f"no profile entry '{key}'"}
+    prof = _kernel_sig(e.get("kernel", ""))
+    if prof != kernel_ran:
+        return {"traffic": None, "traffic_stale": f"profiled {prof or '?'}, ran {kernel_ran or '?'}"}
+    if e.get("src_sha") != device_src_hash():
+        return {"traffic": None, "traffic_stale": f"device sources {device_src_hash()} differ from the profiled "
+                                                  f"{e.get('src_sha')}"}
+    return {"traffic": e["hbm_bytes_per_launch"],
+            "traffic_source": f"{e.get('source', '?')}; commit {e.get('commit', '?')}; src {e['src_sha']}"}
 
 
 def prereduce_roofline(L, ctx, pieces, pre_ms, pre_n, pre_bytes, label):
@@ -284,6 +316,7 @@ def headline(ctx: Ctx, L, args, out_line: dict):
     fmt = DataDesc(DataDesc.DATA_TYPE_MATRIX, DataDesc.KEY_TYPE_INT, DataDesc.ELEMENT_TYPE_FLOAT)
     sharded = world > 1 or args.group
     group = None
+    shuffled_batches = None
     if not sharded:
         store = DataStore(fmt, KeyRange(0, ROWS - 1), COLS, device=ctx.local)
         store.synth_fill(7)
@@ -291,12 +324,24 @@ def headline(ctx: Ctx, L, args, out_line: dict):
         # (a worker pushing the same key set), different gradient values every step
         bufs = make_buckets(L, torch, fmt, W, ROWS) + make_buckets(L, torch, fmt, W, ROWS, value_seed=5000)
         batches = [DeviceBatch([b.data_ptr() for b in bs], [b.numel() for b in bs]) for bs in (bufs[:W], bufs[W:])]
+        # the same steps with the 32 pushes in a new seeded order every step: the PS
+        # selector applies pushes in arrival order (PSAgent.java:166-186)
+        import random
+        rnd = random.Random(2024)
+        shuffled_batches = []
+        for k in range(SHUFFLE_ORDERS):
+            bs = bufs[:W] if k % 2 == 0 else bufs[W:]
+            order = list(range(W))
+            rnd.shuffle(order)
+            shuffled_batches.append(DeviceBatch([bs[j].data_ptr() for j in order], [bs[j].numel() for j in order]))
         k_step = [0]
+        cur = [batches]
 
         def step():
             # async: ack once captured; the store keeps <= 2 batches in flight and the
             # key index of batch k+1 overlaps the reduce of batch k
-            store.pushDevice(batches[k_step[0] & 1])
+            bl = cur[0]
+            store.pushDevice(bl[k_step[0] % len(bl)])
             k_step[0] += 1
 
         finish = store.flush  # every pushed batch applied and error-checked
@@ -326,14 +371,37 @@ def headline(ctx: Ctx, L, args, out_line: dict):
 
     def reset():
         timed_store.kernel_time(reset=True)
+        if not sharded:
+            timed_store.stats(reset=True)
         if sharded and timing:
             _pre_time(L, every=16, reset=True)
 
     el = timed_steps(ctx, step, finish, args.steps, 0, ramp_s=max(0.0, 0.3 - (time.perf_counter() - t0)),
                      reset=reset)
     k_ms, k_n = timed_store.kernel_time(reset=True)
-    timed_store.set_timing(False)
     pre_ms, pre_n = _pre_time(L, every=0, reset=True) if sharded else (0.0, 0)
+    shuffled = None
+    if not sharded:
+        counts = timed_store.stats(reset=True)
+        # the arrival-order case: every step's 32 pushes in a new order (SHUFFLE_ORDERS
+        # seeded orders, cycled), same store, warm
+        cur[0] = shuffled_batches
+        k_step[0] = 0
+        el_s = timed_steps(ctx, step, finish, args.steps, min(args.warmup, 50), reset=reset)
+        ks_ms, ks_n = timed_store.kernel_time(reset=True)
+        cs = timed_store.stats(reset=True)
+        shuffled = {"pushes": f"the same two bucket sets, each step's 32 pushes in a new seeded order "
+                              f"({SHUFFLE_ORDERS} orders cycled): slot reuse keyed by the pushes' content",
+                    "value": round(algo_per_rank * args.steps / el_s / 2**30, 2), "unit": "GiB/s",
+                    "ms_per_step": round(el_s / args.steps * 1e3, 4)}
+        if ks_n:
+            a_s = algo_per_rank / (ks_ms / ks_n / 1e3) / 1e9
+            shuffled.update({"avg_kernel_us": round(ks_ms / ks_n * 1e3, 2), "achieved": round(a_s, 1),
+                             "frac": round(a_s / HBM_PEAK_GBS, 4)})
+        shuffled["pushes_per_step"] = {k: round(cs[k] / max(cs["chunks"], 1), 2)
+                                       for k in ("identity_pushes", "reused_pushes", "indexed_pushes")}
+        shuffled["spec_reruns"] = cs["spec_reruns"]
+    timed_store.set_timing(False)
     value = algo_per_rank * world * args.steps / el / 2**30
     out_line.update({
         "metric": METRIC, "value": round(value, 2), "unit": "GiB/s", "n_gpus": world, "steps": args.steps,
@@ -351,14 +419,18 @@ def headline(ctx: Ctx, L, args, out_line: dict):
         avg_s = k_ms / k_n / 1e3
         achieved = algo_per_rank / avg_s / 1e9
         pk = stream_peaks(L, torch)
+        kn = timed_store.kernel_name()
         out_line["roofline"] = {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS,
                                 "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4),
-                                "traffic": load_traffic("config2"),
-                                "kernel": "k_reduce_rows<float,kAdd> (4 rows x 4 KiB per wave)",
+                                **traffic_for("config2", kn), "kernel": kn,
                                 "avg_kernel_us": round(avg_s * 1e6, 2), "launches": k_n,
                                 "measured_read_peak": round(pk["read"], 1),
                                 "frac_of_measured_read": round(achieved / pk["read"], 4),
                                 "measured_copy_peak": round(pk["copy"], 1)}
+        out_line["pushes_per_step"] = {k: round(counts[k] / max(counts["chunks"], 1), 2)
+                                                 for k in ("identity_pushes", "reused_pushes", "indexed_pushes")}
+        out_line["spec_reruns"] = counts["spec_reruns"]
+        out_line["shuffled"] = shuffled
     elif pre_n > 0:
         # the pre-reduce pieces (k_reduce_rows in pre-reduce mode) are the dominant
         # kernel; per call they read the W pushes and write the full-model partial
@@ -424,13 +496,21 @@ def sparse_leg(ctx: Ctx, L, steps: int, cpu: bool):
     store.kernel_time(reset=True)
     el = timed_steps(ctx, step, store.flush, steps, 0)
     k_ms, k_n = store.kernel_time(reset=True)
+    kn = store.kernel_name()
     algo = w * nnz * 12 + 2 * 4 * w * nnz
     out = {"workload": "config3: 1e9-dim fp32 array shard, 32 pushes x 1e6 unique int64 keys, ordered scatter-add",
            "value": round(steps * algo / el / 2**30, 2), "unit": "GiB/s (algorithmic)", "steps": steps,
-           "ms_per_step": round(el / steps * 1e3, 3), "algorithmic_bytes_per_step": algo,
-           "apply_kernel_us_avg": round(k_ms / max(k_n, 1) * 1e3, 2), "apply_launches": k_n,
-           # PMC HBM bytes per dispatch (profiles/pmc_traffic.json): leaf RMW and the two partition passes
-           "traffic": {k: load_traffic(k) for k in ("sparse", "sparse_l1", "sparse_l2")}}
+           "ms_per_step": round(el / steps * 1e3, 3), "algorithmic_bytes_per_step": algo}
+    if k_n:
+        # the leaf apply (ordered scatter-add) is the dominant kernel; the two partition
+        # passes of the next chunk run beside it on the index stream
+        k_s = k_ms / k_n / 1e3
+        out["roofline"] = {"bound": "hbm", "achieved": round(algo / k_s / 1e9, 1), "peak": HBM_PEAK_GBS,
+                           "unit": "GB/s", "frac": round(algo / k_s / 1e9 / HBM_PEAK_GBS, 4),
+                           **traffic_for("sparse", kn), "kernel": kn, "avg_kernel_us": round(k_s * 1e6, 2),
+                           "launches": k_n,
+                           "note": "random 4-B RMW into a 4 GB array: line-granular (64-B read / 32-B write "
+                                   "sectors), so counted traffic is ~3.9x the algorithmic bytes (DESIGN.md §4)"}
     store.close()
     del bufs
     torch.cuda.empty_cache()
@@ -525,10 +605,10 @@ def leg_config4(ctx: Ctx, L, args) -> dict:
            "algorithmic_bytes_per_step_per_gpu": algo}
     if not sharded and k_n:
         k_s = k_ms / k_n / 1e3
+        kn = store.kernel_name()
         out["roofline"] = {"bound": "hbm", "achieved": round(algo / k_s / 1e9, 1), "peak": HBM_PEAK_GBS,
                            "unit": "GB/s", "frac": round(algo / k_s / 1e9 / HBM_PEAK_GBS, 4),
-                           "traffic": load_traffic("leg4"),
-                           "kernel": "k_reduce_flat<float,kAdd> (200-col rows, identity-speculative: no key index)",
+                           **traffic_for("leg4", kn), "kernel": kn,
                            "avg_kernel_us": round(k_s * 1e6, 1), "launches": k_n}
     elif pre_n:
         out["roofline"] = prereduce_roofline(L, ctx, args.pieces, pre_ms, pre_n,
@@ -614,11 +694,11 @@ def leg_config4_ada(ctx: Ctx, L, args) -> dict:
     if k_n:
         k_s = k_ms / k_n / 1e3
         owner = world * w * S * rec + 4 * S * cols * 4  # one owner launch: every rank's slices + data/delta RMW
+        kn = store.kernel_name()
+        tr = traffic_for("leg4a", kn) if world == 1 else {"traffic": None, "traffic_stale": "profiled at N = 1 only"}
         out["roofline"] = {"bound": "hbm", "achieved": round(owner / k_s / 1e9, 1), "peak": HBM_PEAK_GBS,
                            "unit": "GB/s", "frac": round(owner / k_s / 1e9 / HBM_PEAK_GBS, 4),
-                           "traffic": load_traffic("leg4a") if world == 1 else None,
-                           "kernel": f"AdaGrad owner apply + maxDelta (k_ada_flat for <= 4 slices, else k_reduce; "
-                                     f"rank {rank})",
+                           **tr, "kernel": kn, "rank": rank,
                            "avg_kernel_us": round(k_s * 1e6, 1), "launches": k_n}
     group.close()
     del bufs, ptrs
@@ -693,10 +773,11 @@ def leg_config5(ctx: Ctx, L, args) -> dict:
            "algorithmic_bytes_per_step_per_gpu": algo, "algorithmic_bytes_per_step": int(algo_all)}
     if k_n:
         k_s = k_ms / k_n / 1e3
+        kn = store.kernel_name()
+        tr = traffic_for("leg5", kn) if world == 1 else {"traffic": None, "traffic_stale": "profiled at N = 1 only"}
         out["roofline"] = {"bound": "hbm", "achieved": round(algo / k_s / 1e9, 1), "peak": HBM_PEAK_GBS,
                            "unit": "GB/s", "frac": round(algo / k_s / 1e9 / HBM_PEAK_GBS, 4),
-                           "traffic": load_traffic("leg5") if world == 1 else None,
-                           "kernel": f"k_reduce_rows<int,kAddCheckI32> (rank {rank})",
+                           **tr, "kernel": kn, "rank": rank,
                            "avg_kernel_us": round(k_s * 1e6, 1), "launches": k_n}
     store.close()
     del pos, neg, sets
@@ -827,6 +908,7 @@ def run_shard_config(which: str, cpu_s: float, no_cpu: bool) -> dict:
     el = time.perf_counter() - t0
     k_ms, k_n = store.kernel_time(reset=True)
     store.set_timing(False)
+    kn = store.kernel_name()
     assert store.error_state()[0] == 0, store.error_state()
     store.close()
     del bufs, sets
@@ -840,7 +922,8 @@ def run_shard_config(which: str, cpu_s: float, no_cpu: bool) -> dict:
             "roofline": {"bound": "hbm", "achieved": round(algo / k_s / 1e9, 1) if k_n else None,
                          "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": round(algo / k_s / 1e9 / HBM_PEAK_GBS, 4) if k_n else None,
-                         "kernel_us_avg": round(k_s * 1e6, 1), "traffic": load_traffic("cfg" + which)}}
+                         "kernel_us_avg": round(k_s * 1e6, 1), "kernel": kn,
+                         **traffic_for("cfg" + which.replace("-", ""), kn)}}
     if not no_cpu:
         line["cpu_baseline"] = shard_cpu_baseline(c, cpu_s)
     return line

@@ -18,8 +18,9 @@ except Exception:  # pragma: no cover - torch is optional for the C-ABI itself
     torch = None
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-# DML_LIB_PATH: an alternative build of the same library (A/B runs of build-time variants)
-LIB_PATH = os.environ.get("DML_LIB_PATH") or os.path.join(_HERE, "libdistml_ps.so")
+# The one shipped build, next to this file: nothing in the environment selects
+# another (A/B runs of build-time variants load theirs through load(path) in scripts/).
+LIB_PATH = os.path.join(_HERE, "libdistml_ps.so")
 _lib = None
 
 
@@ -27,6 +28,12 @@ class dml_desc(C.Structure):
     """Mirror of DataDesc's six wire ints (DataDesc.java:62-69)."""
     _fields_ = [("data_type", C.c_int32), ("key_type", C.c_int32), ("value_type", C.c_int32),
                 ("dense_row", C.c_int32), ("dense_column", C.c_int32), ("ada_grad", C.c_int32)]
+
+
+class dml_store_counters(C.Structure):
+    """Mirror of dml_store_counters (dml_store_stats)."""
+    _fields_ = [("chunks", C.c_int64), ("spec_chunks", C.c_int64), ("spec_reruns", C.c_int64),
+                ("identity_pushes", C.c_int64), ("reused_pushes", C.c_int64), ("indexed_pushes", C.c_int64)]
 
 
 # Every symbol include/distml_ps.h declares, with its ctypes signature.
@@ -40,6 +47,9 @@ SIGNATURES = {
     "dml_store_push_batch": (C.c_int, [_vp, _P(_vp), _P(_i64), _i32]),
     "dml_store_push_batch_device": (C.c_int, [_vp, _P(_vp), _P(_i64), _i32]),
     "dml_store_flush": (C.c_int, [_vp]),
+    "dml_store_push_seq": (C.c_int, [_vp, _P(_u64)]),
+    "dml_store_retire": (C.c_int, [_vp, _u64]),
+    "dml_store_stats": (C.c_int, [_vp, _P(dml_store_counters), _i32]),
     "dml_store_error_state": (C.c_int, [_vp, _P(_i64), _P(_i32)]),
     "dml_store_clear_error": (None, [_vp]),
     "dml_store_shape": (C.c_int, [_vp, _P(_i64), _P(_i32)]),
@@ -61,6 +71,7 @@ SIGNATURES = {
     "dml_store_stream": (C.c_int, [_vp, _P(_vp)]),
     "dml_store_set_timing": (C.c_int, [_vp, _i32]),
     "dml_store_kernel_time": (C.c_int, [_vp, _P(C.c_double), _P(_i64), _i32]),
+    "dml_store_kernel_name": (C.c_int, [_vp, C.c_char_p, _i32]),
     "dml_store_apply_dense_device": (C.c_int, [_vp, _vp, _i64]),
     "dml_reduce_buckets_dense": (C.c_int, [_P(dml_desc), _i64, _i64, _i32, _P(_vp), _P(_i64), _i32, _vp, _vp]),
     "dml_prereduce_begin": (C.c_int, [_P(dml_desc), _i64, _i64, _i32, _P(_vp), _P(_i64), _i32, _vp, _P(_vp)]),
@@ -100,6 +111,7 @@ DML_E_CAPACITY = 20
 
 DML_FLAG_FLOAT_ARRAY_REF_STRIDE = 0x1
 DML_FLAG_ASYNC = 0x2
+DML_FLAG_NO_SPECULATION = 0x4
 
 
 class NativeLibraryMissing(RuntimeError):

@@ -71,7 +71,12 @@ struct dml_group {
     void* xrecv[2] = {nullptr, nullptr};
     int64_t xsend_cap[2] = {0, 0}, xrecv_cap[2] = {0, 0};
     hipEvent_t xsent[2] = {nullptr, nullptr};      // rstream: the set's all-to-all finished
-    hipEvent_t xconsumed[2] = {nullptr, nullptr};  // store stream: the store read the set's slices
+    hipEvent_t xconsumed[2] = {nullptr, nullptr};  // store stream: the store's reduce of the set's slices ran
+    // store push-call number of the set's slices (dml_store_push_seq): before the
+    // set's receive buffer is overwritten, the store retires that call
+    // (dml_store_retire), since a retiring chunk may read its pushes again (exact
+    // replay of repeated rows, int32 rollback, re-run of a failed speculation)
+    uint64_t xseq[2] = {0, 0};
     int64_t* xcnt = nullptr;  // device [2][world * kMaxW]: counts sent / received
     int xk = 0;
     // received slices of the last call, handed to the store by the next call or the flush
@@ -168,8 +173,10 @@ int hand_over(dml_group* g) {
     g->xheld = false;
     if (g->xptrs.empty()) return DML_OK;
     const int rc = dml_store_push_batch_device(g->store, g->xptrs.data(), g->xlens.data(), (int32_t)g->xptrs.size());
-    // the store's reads of the set are queued on its stream by now (index host-waited, reduce enqueued)
+    // the store's device reads of the set are queued on its stream by now (index
+    // host-waited, reduce enqueued); its host-side retire may read them once more
     GHIP(hipEventRecord(g->xconsumed[g->xheld_set], g->sstream));
+    GRC(dml_store_push_seq(g->store, &g->xseq[g->xheld_set]));
     return rc;
 }
 
@@ -343,7 +350,10 @@ int dml_group_push_exchange(dml_group* g, const void* const* dev_bufs, const int
         soff[(size_t)q + 1] = soff[(size_t)q] + sb;
         roff[(size_t)q + 1] = roff[(size_t)q] + rb;
     }
-    // xrecv[i] was last read by the store for the call two back
+    // xrecv[i] was last read by the store for the call two back: its chunks retire
+    // (host side) before the buffer is rewritten or freed, its reduce ran before
+    // this call's all-to-all writes it (device side)
+    GRC(dml_store_retire(g->store, g->xseq[i]));
     if (g->xrecv_cap[i] < roff[(size_t)W]) GHIP(hipEventSynchronize(g->xconsumed[i]));
     GRC(grow(&g->xrecv[i], &g->xrecv_cap[i], roff[(size_t)W]));
     GHIP(hipStreamWaitEvent(g->rstream, g->xconsumed[i], 0));

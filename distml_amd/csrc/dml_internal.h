@@ -33,8 +33,22 @@ struct Ctrl {
     unsigned long long ident;    // speculative chunk: bit b = push b verified in the reduce (identity: record r is row r; or slot reuse)
     unsigned int no_dup;         // 0xFFFFFFFF = no row repeated inside one push; 0 = repeat seen
     unsigned int spec_ok;        // speculative chunk: 0xFFFFFFFF = every identity record verified; 0 = not
+    // Slot-table column of push b (0xFF, the reset value: column b). k_index writes a
+    // push's records there and the reduce reads them from there. In a speculative
+    // chunk a push whose `ident` bit is set takes slot = row when its column is 0xFF
+    // (identity) and otherwise reads the kept column k_ident_check matched it to
+    // (slot reuse, whatever position the push arrived at).
+    unsigned char col[kMaxW];
 };
-static_assert(sizeof(Ctrl) == 32, "Ctrl layout");
+static_assert(sizeof(Ctrl) == 96, "Ctrl layout (a multiple of 32 B: the slot table after it stays aligned)");
+__host__ __device__ inline int ctrl_col(const Ctrl* c, int b) {
+    const unsigned v = c->col[b];
+    return v == 0xFFu ? b : (int)v;
+}
+// A speculative chunk's push b verified as identity (record r holds row r).
+__host__ __device__ inline bool ctrl_identity(const Ctrl* c, unsigned long long ident, int b) {
+    return ((ident >> b) & 1ull) && c->col[b] == 0xFFu;
+}
 
 // Bucket table passed by value as a kernel argument (scalar-loaded).
 struct Batch {
@@ -51,12 +65,12 @@ struct Batch {
     const void* src;      // input shard (null: in place)
     int64_t first;        // key of row 0 (KeyRange first), for the verification
     int32_t spec;         // 1: speculative chunk
-    // Slot reuse (speculative chunks): bit b = push b's
-    // column of the workspace's slot table still holds the permutation the push at
-    // position b of the workspace's previous chunk listed. A push whose sampled keys
-    // match it skips the key index; the reduce reads its slots from the table and
-    // verifies every record's key like an identity push's.
-    uint64_t reuse;
+    // Slot reuse (speculative chunks): bit c = column c of the workspace's slot table
+    // still holds the permutation a push of the workspace's previous chunk listed
+    // (verified there). A push whose sampled keys match one of these columns, at any
+    // position, skips the key index (k_ident_check sets Ctrl::col); the reduce reads
+    // its slots from that column and verifies every record's key.
+    uint64_t kept_cols;
     // 1: such a chunk (its table may hold kept columns, so a stale entry is no
     // repeat): the key index does not look for repeated rows, and the reduce
     // verifies the record of every row of every push instead (all pushes are
@@ -143,6 +157,10 @@ hipError_t launch_index(const Batch& bt, int nb, int64_t max_nrec, int64_t strid
 // every sampled record r of it has row_index(key) == r (Ctrl reset to all ones).
 hipError_t launch_ident_check(const Batch& bt, int nb, int64_t stride, int K, int64_t first, int64_t rows,
                               const int32_t* slot, Ctrl* ctrl, hipStream_t st);
+// After k_ident_check of a chunk offered kept columns: gives every push that is
+// neither identity nor matched a slot-table column no matched push reads
+// (Ctrl::col), so its key index does not overwrite a reused permutation.
+hipError_t launch_assign_cols(Ctrl* ctrl, int nb, hipStream_t st);
 // Complete identity check (Ctrl::ident reset to all ones, or as k_ident_check left
 // it): clears ctrl->ident bit b unless every record r of push b has row_index(key) == r.
 hipError_t launch_ident_full(const Batch& bt, int nb, int64_t max_nrec, int64_t stride, int K, int64_t first,
@@ -258,6 +276,28 @@ bool use_flat(int vtype, int mode, int32_t cols, const Batch& bt, int nb, int64_
 bool spec_shape(int vtype, int32_t cols);
 
 uint64_t splitmix64(uint64_t x);
+
+// Name of the dominant kernel (reduce / flat / AdaGrad / sparse leaf) the calling
+// thread launched last, in rocprof's form, e.g.
+// "dml::k_reduce_rows<float, 0, 4, 4, true, true, 1, 4, 0>": bench.py ties a profile's
+// counted HBM bytes to the instantiation that ran (dml_store_kernel_name).
+extern thread_local const char* g_kernel_name;
+inline std::string kname_arg(bool v) { return v ? "true" : "false"; }
+inline std::string kname_arg(int v) { return std::to_string(v); }
+inline std::string kname_arg(const char* v) { return v; }
+template <typename... A>
+std::string kname(const char* base, A... a) {
+    std::string s = std::string("dml::") + base + "<";
+    bool first = true;
+    ((s += (first ? "" : ", ") + kname_arg(a), first = false), ...);
+    return s + ">";
+}
+template <typename T>
+inline const char* type_name() {
+    if constexpr (sizeof(T) == 8) return "double";
+    else if constexpr (T(0.5) == T(0)) return "int";
+    else return "float";
+}
 
 // Records `msg` as the calling thread's dml_last_error() and returns `code`
 // (dml_store.hip; shared by the C-ABI translation units).

@@ -32,6 +32,7 @@ __host__ __device__ inline uint64_t splitmix64_dev(uint64_t x) {
     return z ^ (z >> 31);
 }
 uint64_t splitmix64(uint64_t x) { return splitmix64_dev(x); }
+thread_local const char* g_kernel_name = nullptr;
 
 template <typename T>
 __device__ inline void unpack(const u32x4& r, T* o) {
@@ -77,7 +78,7 @@ __global__ __launch_bounds__(256) void k_index(const Batch bt, int64_t stride, i
         atomicMin(&ctrl->cutoff, (unsigned long long)pos_of((uint64_t)bt.bidx[b], (uint64_t)off));
         return;
     }
-    const int32_t old = atomicExch(&slot[idx * slot_stride((int)gridDim.y) + b], (int32_t)r);
+    const int32_t old = atomicExch(&slot[idx * slot_stride((int)gridDim.y) + ctrl_col(ctrl, b)], (int32_t)r);
     if (old != -1 && !bt.keeps) {
         rowflag[idx] = 1u;
         ctrl->no_dup = 0u;  // benign race: every writer stores the same value
@@ -87,33 +88,86 @@ __global__ __launch_bounds__(256) void k_index(const Batch bt, int64_t stride, i
 // k_ident_check: one 64-lane block per push of a speculative chunk. Push b stays
 // an identity candidate if it is full-range (nrec == rows) and the records at 32
 // evenly spaced positions (first and last included) plus 32 hashed ones hold row
-// r at record r — or, for a slot-reuse candidate (Batch::reuse), the row the kept
-// slot column maps to record r. Cheap (64 key lines per push); the reduce
-// verifies every record.
+// r at record r. Otherwise, when the workspace kept verified permutations
+// (Batch::kept_cols), the push is matched by content to a kept column: the kept
+// columns whose entry for the row of record 0 is 0 are the candidates (one slot-row
+// load), its own position's column first, and the first candidate that maps every
+// sampled record's row to that record becomes Ctrl::col[b]. Arrival order does not
+// matter (PSAgent's selector applies pushes as they arrive, PSAgent.java:166-186).
+// Cheap (64 key lines and a few slot lines per push); the reduce verifies every record.
 __global__ __launch_bounds__(64) void k_ident_check(const Batch bt, int64_t stride, int K, int64_t first, int64_t rows,
                                                     const int32_t* __restrict__ slot, Ctrl* __restrict__ ctrl) {
     const int b = blockIdx.x, t = threadIdx.x;
-    bool ok = bt.nrec[b] == rows && rows > 0;
-    if (ok) {
-        const int64_t r = t < 32 ? (rows > 1 ? (int64_t)t * (rows - 1) / 31 : 0)
-                                 : (int64_t)(splitmix64_dev(((uint64_t)b << 32) + (uint64_t)t) % (uint64_t)rows);
-        const int64_t idx = row_index(ld_key(bt.base[b] + r * stride, K), first, rows);
-        if ((bt.reuse >> b) & 1ull)
-            ok = idx >= 0 && slot[idx * slot_stride((int)gridDim.x) + b] == (int32_t)r;
-        else
-            ok = idx == r;
+    const int ss = slot_stride((int)gridDim.x);
+    const bool full = bt.nrec[b] == rows && rows > 0;  // block-uniform
+    int64_t r = 0, idx = -1;
+    if (full) {
+        r = t < 32 ? (rows > 1 ? (int64_t)t * (rows - 1) / 31 : 0)
+                   : (int64_t)(splitmix64_dev(((uint64_t)b << 32) + (uint64_t)t) % (uint64_t)rows);
+        idx = row_index(ld_key(bt.base[b] + r * stride, K), first, rows);
     }
-    const bool all = __ballot(!ok) == 0ull;
+    const bool ident = full && __ballot(idx != r) == 0ull;
+    int col = -1;
+    if (full && !ident && bt.kept_cols) {
+        // sample t = 0 is record 0
+        const int32_t idx0 = __shfl((int32_t)idx, 0);
+        uint64_t cand = 0;
+        if (idx0 >= 0) {
+            const bool c = t < ss && ((bt.kept_cols >> t) & 1ull) && slot[(int64_t)idx0 * ss + t] == 0;
+            cand = __ballot(c);
+        }
+        // the column of the same position first (a worker arriving in its usual place)
+        if ((cand >> b) & 1ull) {
+            if (__ballot(!(idx >= 0 && slot[idx * ss + b] == (int32_t)r)) == 0ull) col = b;
+            cand &= ~(1ull << b);
+        }
+        while (col < 0 && cand) {
+            const int c = (int)__builtin_ctzll(cand);
+            cand &= cand - 1;
+            if (__ballot(!(idx >= 0 && slot[idx * ss + c] == (int32_t)r)) == 0ull) col = c;
+        }
+    }
     if (t == 0) {
-        unsigned long long clear = all ? 0ull : (1ull << b);
+        unsigned long long clear = (ident || col >= 0) ? 0ull : (1ull << b);
         if (b == 0 && gridDim.x < 64) clear |= ~((1ull << gridDim.x) - 1ull);  // no such push
         if (clear) atomicAnd(&ctrl->ident, ~clear);
+        if (col >= 0) ctrl->col[b] = (unsigned char)col;
     }
 }
 hipError_t launch_ident_check(const Batch& bt, int nb, int64_t stride, int K, int64_t first, int64_t rows,
                               const int32_t* slot, Ctrl* ctrl, hipStream_t st) {
     if (nb <= 0) return hipSuccess;
     hipLaunchKernelGGL(k_ident_check, dim3((unsigned)nb), dim3(64), 0, st, bt, stride, K, first, rows, slot, ctrl);
+    return hipGetLastError();
+}
+
+// k_assign_cols (one thread): the pushes k_ident_check neither verified as identity
+// nor matched to a kept column are indexed; each keeps its own column when no
+// matched push reads it, the others take the lowest free columns. A chunk of nb
+// pushes has slot_stride(nb) >= nb columns and at most nb of them are taken, so
+// every push gets one.
+__global__ __launch_bounds__(64) void k_assign_cols(Ctrl* __restrict__ ctrl, int nb) {
+    if (threadIdx.x != 0) return;
+    const unsigned long long id = ctrl->ident;
+    uint64_t used = 0, need = 0;
+    for (int b = 0; b < nb; ++b)
+        if (((id >> b) & 1ull) && ctrl->col[b] != 0xFFu) used |= 1ull << ctrl->col[b];
+    for (int b = 0; b < nb; ++b) {
+        if ((id >> b) & 1ull) continue;
+        if ((used >> b) & 1ull) need |= 1ull << b;
+        else used |= 1ull << b;  // column b (Ctrl::col stays 0xFF)
+    }
+    while (need) {
+        const int b = (int)__builtin_ctzll(need);
+        need &= need - 1;
+        const int c = (int)__builtin_ctzll(~used);
+        used |= 1ull << c;
+        ctrl->col[b] = (unsigned char)c;
+    }
+}
+hipError_t launch_assign_cols(Ctrl* ctrl, int nb, hipStream_t st) {
+    if (nb <= 0) return hipSuccess;
+    hipLaunchKernelGGL(k_assign_cols, dim3(1), dim3(64), 0, st, ctrl, nb);
     return hipGetLastError();
 }
 
@@ -624,24 +678,26 @@ __global__ __launch_bounds__(64 * WPB) void k_reduce_rows(T* __restrict__ shard,
     static_assert(kMaxW == 64, "one push per lane");
     int32_t vslot[RPW];
     // lanes >= nb read past the row's entries (another row's): masked to -1;
-    // an identity push (speculation) holds row r at record r when r < nrec
-    // a slot-reuse push (Batch::reuse) is verified like an identity push but takes
-    // its slots from the kept table
-    const bool lane_ident = lane < nb && ((ident >> lane) & 1ull) && !((bt.reuse >> lane) & 1ull);
+    // an identity push (speculation) holds row r at record r when r < nrec;
+    // every other push reads its column (Ctrl::col: its own, or the kept column a
+    // slot-reuse push was matched to, verified like an identity push)
+    const bool lane_ident = lane < nb && ctrl_identity(ctrl, ident, lane);
+    const int lcol = lane < nb ? ctrl_col(ctrl, lane) : lane;
 #pragma unroll
     for (int r = 0; r < RPW; ++r)
         vslot[r] = ((live >> r & 1u) && lane < nb)
-                       ? (lane_ident ? (row[r] < bt.nrec[lane] ? (int32_t)row[r] : -1) : slot[row[r] * slot_stride(nb) + lane])
+                       ? (lane_ident ? (row[r] < bt.nrec[lane] ? (int32_t)row[r] : -1) : slot[row[r] * slot_stride(nb) + lcol])
                        : -1;
-    if (!bt.spec) {
+    if (!bt.spec && ngroups == 1) {
         // Hand the slot rows back as the next batch's index expects them (-1 = no
         // record), so the host skips the slot-table memset (reduce_clears_slots); the
-        // int32 rollback (rare) rebuilds the table with a second index. A speculative
-        // chunk keeps its table: its full-range columns are permutations the next
-        // chunk in this workspace may reuse (Batch::reuse).
+        // int32 rollback (rare) rebuilds the table with a second index. Only when this
+        // wave is its rows' one reader (rows wider than CPW chunks have several). A
+        // speculative chunk keeps its table: its full-range columns are permutations
+        // the next chunk in this workspace may reuse (Batch::kept_cols).
 #pragma unroll
         for (int r = 0; r < RPW; ++r)
-            if ((live >> r & 1u) && lane < nb) slot[row[r] * slot_stride(nb) + lane] = -1;
+            if ((live >> r & 1u) && lane < nb) slot[row[r] * slot_stride(nb) + lcol] = -1;
     }
     const uint64_t vbase = lane < nb ? (uint64_t)bt.base[lane] : 0ull;
     // Speculative chunks verify identity records through lane 63 of the wave's last
@@ -925,12 +981,13 @@ __global__ __launch_bounds__(256) void k_reduce_flat(T* __restrict__ shard, int6
         const int64_t mr = model_row(t0 + rl);
         int32_t v = -1;
         if (!(rm.block && mr >= rm.rows_total) && !(rowflag && rowflag[mr])) {
-            if (((ident >> b) & 1ull) && !((bt.reuse >> b) & 1ull)) {  // identity push: record = row
+            if (ctrl_identity(ctrl, ident, b)) {  // identity push: record = row
                 v = mr < bt.nrec[b] ? (int32_t)mr : -1;
             } else {
-                v = slot[mr * ss + b];
-                // a speculative chunk keeps its table (Batch::reuse, see k_reduce_rows)
-                if (!bt.spec) slot[mr * ss + b] = -1;
+                const int cb = ctrl_col(ctrl, b);
+                v = slot[mr * ss + cb];
+                // a speculative chunk keeps its table (Batch::kept_cols, see k_reduce_rows)
+                if (!bt.spec) slot[mr * ss + cb] = -1;
             }
         }
         ls[rl * kMaxW + b] = v;
@@ -1259,6 +1316,9 @@ static hipError_t launch_reduce_t(void* shard, int64_t rows, int32_t cols, const
     const unsigned occ_lds = lds_for_blocks_per_cu(bpc);
     if constexpr (RPW > 1) {
         static_assert(MODE != kAdaGrad && MODE != kRollbackI32, "k_reduce_rows shapes");
+        static const std::string kn =
+            kname("k_reduce_rows", type_name<T>(), MODE, CPW, RPW, NT, FULL, G == 3 ? 3 : 1, WPB, SNT);
+        g_kernel_name = kn.c_str();
         if (ev.start || ev.stop)
             hipExtLaunchKernelGGL((k_reduce_rows<T, MODE, CPW, RPW, NT, FULL, G == 3 ? 3 : 1, WPB, SNT>), dim3((unsigned)nblocks),
                                   dim3(64 * WPB), occ_lds, st, ev.start, ev.stop, 0, (T*)shard, rows, cols, ngroups, bt, nb, stride,
@@ -1268,6 +1328,8 @@ static hipError_t launch_reduce_t(void* shard, int64_t rows, int32_t cols, const
                                dim3(64 * WPB), occ_lds, st, (T*)shard, rows, cols, ngroups, bt, nb, stride, K, const_cast<int32_t*>(slot), rowflag,
                                ctrl, tail_cut, rm);
     } else {
+        static const std::string kn = kname("k_reduce", type_name<T>(), MODE, G, NT, WPB, SNT != 0, CPW);
+        g_kernel_name = kn.c_str();
         if (ev.start || ev.stop)
             hipExtLaunchKernelGGL((k_reduce<T, MODE, G, NT, WPB, SNT, CPW>), dim3((unsigned)nblocks), dim3(64 * WPB),
                                   occ_lds, st, ev.start, ev.stop, 0, (T*)shard, rows, cols, ngroups, bt, nb, stride,
@@ -1358,6 +1420,8 @@ static hipError_t launch_flat_t(void* shard, int64_t rows, int32_t cols, const B
     const int64_t nblocks = ((rows + R - 1) / R + 3) / 4;
     if (nblocks_out) *nblocks_out = nblocks;
     if (nblocks <= 0) return hipSuccess;
+    static const std::string kn = kname("k_reduce_flat", type_name<T>(), MODE, JMAX, PB);
+    g_kernel_name = kn.c_str();
     if (ev.start || ev.stop)
         hipExtLaunchKernelGGL((k_reduce_flat<T, MODE, JMAX, PB>), dim3((unsigned)nblocks), dim3(256), 0, st, ev.start,
                               ev.stop, 0, (T*)shard, rows, cols, R, bt, nb, stride, K, const_cast<int32_t*>(slot),
@@ -1395,12 +1459,16 @@ bool use_flat(int vtype, int mode, int32_t cols, const Batch& bt, int nb, int64_
 }
 
 // Identity speculation pays where the double-buffered reduce streams as fast as
-// the in-place one (measured): rows of whole 1-KiB chunks
-// (k_reduce_rows FULL) and the flat kernel's rows under 4 KiB.
+// the in-place one (measured), and is only offered to the kernels
+// whose loops verify a slot-keeping chunk completely (every live row of every
+// push has a record, every record's key is checked): whole 4-KiB rows
+// (k_reduce_rows FULL, the DEPTH-1 loop) and the flat kernel's rows under 4 KiB.
+// Rows of >= 4 KiB that are not whole 4-KiB multiples run the pair-packed DEPTH-3
+// loop, which checks identity records only: no speculation there.
 bool spec_shape(int vtype, int32_t cols) {
     const int VEC = vtype == kF64 ? 2 : 4;
     const int64_t bytes = (int64_t)cols * (vtype == kF64 ? 8 : 4);
-    return bytes % 1024 == 0 || (cols % VEC == 0 && bytes < 4096);
+    return bytes % 4096 == 0 || (cols % VEC == 0 && bytes < 4096);
 }
 
 // k_ada_flat launch: R rows per wave (R = 5 at 200 columns).
@@ -1414,6 +1482,8 @@ static hipError_t launch_ada_flat_t(void* shard, int64_t rows, int32_t cols, con
     const int64_t nblocks = ((rows + R - 1) / R + 3) / 4;
     if (nblocks_out) *nblocks_out = nblocks;
     if (nblocks <= 0) return hipSuccess;
+    static const std::string kn = kname("k_ada_flat", JMAX, PB);
+    g_kernel_name = kn.c_str();
     if (ev.start || ev.stop)
         hipExtLaunchKernelGGL((k_ada_flat<JMAX, PB>), dim3((unsigned)nblocks), dim3(256), 0, st, ev.start, ev.stop, 0,
                               (float*)shard, rows, cols, R, bt, nb, stride, K, const_cast<int32_t*>(slot), rowflag,
@@ -1440,7 +1510,12 @@ bool reduce_clears_slots(int vtype, int mode, int32_t cols) {
     if (mode != kAdd && mode != kPreReduce && mode != kAddCheckI32) return false;
     const int VEC = vtype == kF64 ? 2 : 4;
     if (cols < VEC) return false;  // k_reduce's generic path
-    return true;
+    // k_reduce_rows clears only when one wave owns a row's every chunk (launch_auto's
+    // CPW: 4 for whole 4-KiB multiples and for >= 4 chunks, else 2 or 1); the flat
+    // kernel always does, but is chosen per chunk, so it is not counted on here
+    const int64_t nchunks = (cols + 64 * VEC - 1) / (64 * VEC);
+    const int64_t cpw = (nchunks >= 4 || cols % (64 * VEC * 4) == 0) ? 4 : nchunks >= 2 ? 2 : 1;
+    return nchunks <= cpw;
 }
 
 int64_t reduce_blocks(int vtype, int64_t rows, int32_t cols) {

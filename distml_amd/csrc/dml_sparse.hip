@@ -936,6 +936,9 @@ hipError_t launch_sparse_leaf(int vtype, void* shard, const SpPlan& pl, const Sp
     // line buckets: leaf rows >> bshift < kSpLines
     int bshift = 0;
     while ((((int64_t)1 << pl.SL) >> bshift) > kSpLines) ++bshift;
+    g_kernel_name = vtype == kF64 ? "dml::k_sp_leaf<double, false>"
+                    : pl.compact  ? "dml::k_sp_leaf<float, true>"
+                                  : "dml::k_sp_leaf<float, false>";
     if (vtype == kF32 && pl.compact)
         hipExtLaunchKernelGGL((k_sp_leaf<float, true>), grid, dim3(kSpLeafThreads), leaf_lds_pad<float, true>(), st,
                               ev.start, ev.stop, 0,

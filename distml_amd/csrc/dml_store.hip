@@ -67,7 +67,8 @@ struct Chunk {
     SpPlan sp{};
     SpLayout spl{};
     bool spec = false;     // identity speculation (full-range plain-sum chunk, Batch::spec)
-    bool keeps = false;    // speculative chunk: its slot table is kept for the next chunk here (Batch::reuse)
+    bool keeps = false;    // speculative chunk: its slot table is kept for the next chunk here (Batch::kept_cols)
+    uint64_t seq = 0;      // number of the push call the chunk belongs to (dml_store_push_seq)
     void* in = nullptr;    // matrix shard the chunk reads (the previous chunk's output)
     void* out = nullptr;   // and writes: == in, or the other buffer of a speculative chunk
 };
@@ -96,9 +97,10 @@ struct Workspace {
     SpStat* hsp = nullptr;            // pinned status of the single-pass sparse partition
     bool clears = false;              // the chunk's reduce leaves its slot table all -1
     bool clean = false;               // slot table all -1 and rowflags 0: only the Ctrl needs a reset
-    // Kept slot table (the last chunk here was a verified speculative chunk): rowflags 0, and column b of [rows][slot_stride(kept_nb)] is the
-    // permutation push b listed when bit b of `perm` is set (indexed or reused, not
-    // identity); other columns hold no meaning
+    // Kept slot table (the last chunk here was a verified speculative chunk): rowflags
+    // 0, and column c of [rows][slot_stride(kept_nb)] is the verified permutation of
+    // one of that chunk's pushes (indexed or reused, not identity) when bit c of
+    // `perm` is set; other columns hold no meaning
     bool kept = false;
     int kept_nb = 0;
     uint64_t perm = 0;
@@ -136,6 +138,9 @@ struct dml_store {
     Workspace ws[kRing];
     size_t slot_bytes = 0, ws_bytes = 0;
     int next_ws = 0;
+    uint64_t call_seq = 0;      // push calls accepted so far (dml_store_push_seq)
+    dml_store_counters st{};    // pipeline counters (dml_store_stats), counted at retire
+    bool no_spec = false;       // DML_FLAG_NO_SPECULATION, or no HBM headroom for data_alt
     std::deque<Pending> pend;   // launched, not yet retired (oldest first), at most kRing-1
     // staging for host-memory pushes
     uint8_t* hstage = nullptr;
@@ -157,6 +162,7 @@ struct dml_store {
     hipEvent_t neg_ev = nullptr;
     bool neg_pending = false;
     // timing of the dominant kernel
+    const char* kname = nullptr;  // its instantiation, as last launched (dml_store_kernel_name)
     bool timing = false;
     std::vector<std::pair<hipEvent_t, hipEvent_t>> ev_used, ev_free;
     double timed_ms = 0.0;
@@ -344,6 +350,13 @@ AdaArgs ada_args(dml_store* s) { return AdaArgs{s->alpha, s->delta, s->cand, s->
 // copy its Ctrl out and record `done`. `prev` = Ctrl of the chunk enqueued before.
 int launch_apply(dml_store* s, Chunk& c, Workspace& W, const Ctrl* prev) {
     c.bt.prev = prev;
+    g_kernel_name = nullptr;
+    struct NameOnExit {
+        dml_store* s;
+        ~NameOnExit() {
+            if (g_kernel_name) s->kname = g_kernel_name;
+        }
+    } name_on_exit{s};
     if (s->is_matrix) {
         // Boundary between consecutive reduces (measured): a plain dispatch
         // followed by one marker event ~7 µs; with timing, hipExtLaunchKernel's in-packet
@@ -417,8 +430,11 @@ int launch_chunk(dml_store* s, Chunk& c, Workspace& W, const Ctrl* prev) {
     HIPCHK(hipMemsetAsync(W.base, 0xFF, sizeof(Ctrl) + (slots_ok ? 0 : s->slot_bytes), is));
     if (s->is_matrix) {
         if (!(clean || kept)) HIPCHK(hipMemsetAsync(W.rowflag, 0, (size_t)s->rows * sizeof(uint32_t), is));
-        if (c.spec)
+        if (c.spec) {
             HIPCHK(launch_ident_check(c.bt, c.nb, s->stride, s->K, s->first, s->rows, W.slot, W.ctrl, is));
+            // pushes matched to kept columns: the indexed ones take columns nobody reads
+            if (c.bt.kept_cols) HIPCHK(launch_assign_cols(W.ctrl, c.nb, is));
+        }
         // AdaGrad chunks of k_ada_flat (no speculation: the apply cannot be undone):
         // full-range pushes whose records are rows in order skip the key index after a
         // complete key check, when the slot table is beyond the caches (its atomics go
@@ -632,7 +648,7 @@ int rerun_unspeculated(dml_store* s, Chunk& c, Workspace& W, Ctrl* ctl) {
     c.spec = false;
     c.bt.spec = 0;
     c.keeps = false;
-    c.bt.reuse = 0;
+    c.bt.kept_cols = 0;
     c.bt.keeps = 0;
     c.bt.prev = nullptr;
     set_buffers(s, c, s->data);
@@ -664,20 +680,42 @@ int retire_front(dml_store* s) {
     if (s->timing) ev_collect(s);
     const bool abnormal = ctrl_abnormal(&ctl);  // the chunk queued behind it ran as a no-op
     W.clean = s->is_matrix && !abnormal && W.clears;
+    s->st.chunks += 1;
     if (c.spec && ctl.spec_ok != 0u) {
         std::swap(s->data, s->data_alt);  // every identity record verified: the output is the shard
+        s->st.spec_chunks += 1;
+        uint64_t perm = 0;
+        for (int b = 0; b < c.nb; ++b) {
+            if (ctrl_identity(&ctl, ctl.ident, b)) {
+                s->st.identity_pushes += 1;
+                continue;
+            }
+            if ((ctl.ident >> b) & 1ull) s->st.reused_pushes += 1;
+            else s->st.indexed_pushes += 1;
+            perm |= 1ull << ctrl_col(&ctl, b);  // a verified permutation (indexed or reused)
+        }
         if (c.keeps) {  // the reduce left the slot table as built: the next chunk here may reuse it
             W.clean = false;
             W.kept = true;
             W.kept_nb = c.nb;
-            W.perm = (~ctl.ident | c.bt.reuse) & (c.nb >= 64 ? ~0ull : (1ull << c.nb) - 1ull);
+            W.perm = perm;
         }
     } else if (c.spec) {
         // An identity push was not (or the chunk met a cutoff / repeated row): the
         // output is discarded and the chunk re-runs exactly, in place on its input
         // (the shard as of the chunks before it), with the full key index.
+        s->st.spec_chunks += 1;
+        s->st.spec_reruns += 1;
+        s->st.indexed_pushes += c.nb;
         if (int r2 = rerun_unspeculated(s, c, W, &ctl)) return r2;
         W.clean = !ctrl_abnormal(&ctl) && W.clears;
+    } else if (s->is_matrix) {
+        // non-speculative: AdaGrad chunks may have skipped the index for pushes checked
+        // completely (Batch::ident_ok)
+        for (int b = 0; b < c.nb; ++b) {
+            if (c.bt.ident_ok && ((ctl.ident >> b) & 1ull)) s->st.identity_pushes += 1;
+            else s->st.indexed_pushes += 1;
+        }
     }
     int rc = DML_OK;
     if (s->is_matrix && ctl.no_dup == 0u) {
@@ -768,8 +806,10 @@ int collect_apply_check(dml_store* s, bool block);
 
 int run_batch(dml_store* s, const uint8_t* const* dptr, const int64_t* lens, int n) {
     if (int rc = collect_apply_check(s, false)) return rc;  // an int32 owner apply failed earlier
+    const uint64_t seq = ++s->call_seq;
     for (int c0 = 0; c0 < n; c0 += kMaxW) {
         Chunk c;
+        c.seq = seq;
         c.nb = std::min(kMaxW, n - c0);
         for (int j = 0; j < c.nb; ++j) {
             const int gb = c0 + j;
@@ -792,28 +832,35 @@ int run_batch(dml_store* s, const uint8_t* const* dptr, const int64_t* lens, int
         // Identity speculation: plain-sum matrices of the spec_shape
         // widths, when every push of the chunk is full-range (one record per row, no
         // ragged tail): no key index, the reduce verifies every record's key.
-        if (s->is_matrix && reduce_mode(s) == kAdd && spec_shape(vtype_of(s->desc), s->cols) &&
+        if (s->is_matrix && reduce_mode(s) == kAdd && !s->no_spec && spec_shape(vtype_of(s->desc), s->cols) &&
             c.tail_cut == kNoPos) {
             bool full = true;
             for (int j = 0; j < c.nb && full; ++j) full = c.bt.nrec[j] == s->rows && c.bt.len[j] == s->rows * s->stride;
-            if (full && !s->data_alt &&
-                hipMalloc(&s->data_alt, (size_t)s->rows * (size_t)s->cols * (size_t)s->V) != hipSuccess) {
-                (void)hipGetLastError();
-                s->data_alt = nullptr;  // no room for a second buffer: no speculation
+            if (full && !s->data_alt) {
+                // the second shard buffer, only with headroom left for the caller's
+                // buffers (exchange slices, partials): 1/8 of the device or 4 GiB
+                const size_t need = (size_t)s->rows * (size_t)s->cols * (size_t)s->V;
+                size_t free_b = 0, total_b = 0;
+                const bool room = hipMemGetInfo(&free_b, &total_b) == hipSuccess &&
+                                  free_b > need + std::max<size_t>(total_b / 8, (size_t)4 << 30);
+                if (!room || hipMalloc(&s->data_alt, need) != hipSuccess) {
+                    (void)hipGetLastError();
+                    s->data_alt = nullptr;
+                    s->no_spec = true;  // no room for a second buffer: no speculation
+                }
             }
             c.spec = full && s->data_alt;
         }
         c.bt.spec = c.spec ? 1 : 0;
-        // Slot reuse: a speculative chunk reduced by k_reduce_rows may take
-        // a push's slots from the column its workspace kept for the push at the same
-        // position, when that push's sampled keys match it (k_ident_check)
-        c.bt.reuse = 0;
+        // Slot reuse: a speculative chunk may take a push's slots from
+        // any column its workspace kept (a verified permutation of the workspace's
+        // previous chunk), when that push's sampled keys match it (k_ident_check)
+        c.bt.kept_cols = 0;
         c.keeps = c.spec;
         c.bt.keeps = c.keeps ? 1 : 0;
         if (c.keeps) {
             const Workspace& Wn = s->ws[s->next_ws];
-            if (Wn.kept && slot_stride(Wn.kept_nb) == slot_stride(c.nb))
-                c.bt.reuse = Wn.perm & (c.nb >= 64 ? ~0ull : (1ull << c.nb) - 1ull);
+            if (Wn.kept && slot_stride(Wn.kept_nb) == slot_stride(c.nb)) c.bt.kept_cols = Wn.perm;
         }
         c.bt.first = s->first;
         const Ctrl* prev = s->pend.empty() ? nullptr : s->ws[s->pend.back().w].ctrl;
@@ -904,6 +951,7 @@ int dml_store_create_range(const dml_desc* desc, int64_t first_key, int64_t last
     s->device = device;
     s->desc = d;
     s->flags = flags;
+    s->no_spec = (flags & DML_FLAG_NO_SPECULATION) != 0;
     s->is_matrix = d.data_type == 1;
     s->adagrad = s->is_matrix && d.value_type == DML_ELEMENT_TYPE_FLOAT && d.ada_grad;
     s->K = d.key_type == 0 ? 4 : 8;
@@ -1088,6 +1136,36 @@ int dml_store_flush(dml_store* s) {
     int rc = begin_call(s);
     if (rc) return rc;
     HIPCHK(hipStreamSynchronize(s->stream));
+    return DML_OK;
+}
+
+int dml_store_push_seq(dml_store* s, uint64_t* seq) {
+    if (int rc = check_store(s)) return rc;
+    if (!seq) return set_err(DML_E_INVALID_ARG, "null out");
+    std::lock_guard<std::mutex> lk(s->mu);
+    *seq = s->call_seq;
+    return DML_OK;
+}
+
+int dml_store_retire(dml_store* s, uint64_t seq) {
+    if (int rc = check_store(s)) return rc;
+    std::lock_guard<std::mutex> lk(s->mu);
+    DeviceGuard g(s->device);
+    while (!s->pend.empty() && s->pend.front().c.seq <= seq) {
+        if (int rc = retire_front(s)) {
+            s->pend.clear();
+            return rc;
+        }
+    }
+    return DML_OK;
+}
+
+int dml_store_stats(dml_store* s, dml_store_counters* out, int32_t reset) {
+    if (int rc = check_store(s)) return rc;
+    if (!out) return set_err(DML_E_INVALID_ARG, "null out");
+    std::lock_guard<std::mutex> lk(s->mu);
+    *out = s->st;
+    if (reset) s->st = dml_store_counters{};
     return DML_OK;
 }
 
@@ -1374,6 +1452,15 @@ int dml_store_set_timing(dml_store* s, int32_t enable) {
     return DML_OK;
 }
 
+int dml_store_kernel_name(dml_store* s, char* out, int32_t cap) {
+    if (int rc = check_store(s)) return rc;
+    if (!out || cap <= 0) return set_err(DML_E_INVALID_ARG, "bad name buffer");
+    std::lock_guard<std::mutex> lk(s->mu);
+    const char* n = s->kname ? s->kname : "";
+    std::snprintf(out, (size_t)cap, "%s", n);
+    return (int32_t)std::strlen(n) < cap ? DML_OK : set_err(DML_E_CAPACITY, "name buffer too small");
+}
+
 int dml_store_kernel_time(dml_store* s, double* total_ms, int64_t* launches, int32_t reset) {
     if (int rc = check_store(s)) return rc;
     std::lock_guard<std::mutex> lk(s->mu);
@@ -1393,7 +1480,12 @@ int dml_store_apply_dense_device(dml_store* s, const void* dev_src, int64_t elem
     if (int rc = check_store(s)) return rc;
     std::lock_guard<std::mutex> lk(s->mu);
     DeviceGuard g(s->device);
-    if (int rc = begin_call(s)) return rc;
+    // pushes before it are retired (an error there stops the store like the
+    // reference); the previous owner apply's check is read only if it has finished:
+    // blocking on it would serialize the sharded int32 pipeline
+    if (int rc = retire_all(s)) return rc;
+    if (int rc = collect_apply_check(s, false)) return rc;
+    if (s->err) return set_err(s->err, "store is in a failed state (see dml_store_error_state)");
     if (!dev_src || elems != s->rows * s->cols) return set_err(DML_E_INVALID_ARG, "apply size mismatch");
     std::pair<hipEvent_t, hipEvent_t> ev{};
     if (s->timing) {
@@ -1401,9 +1493,8 @@ int dml_store_apply_dense_device(dml_store* s, const void* dev_src, int64_t elem
         HIPCHK(hipEventRecord(ev.first, s->stream));
     }
     if (vtype_of(s->desc) == kI32) {
-        // IntMatrixStore: check the final counters (IntMatrixStore.java:174-176)
-        if (int rc = collect_apply_check(s, false)) return rc;
-        if (s->err) return set_err(s->err, "store is in a failed state (see dml_store_error_state)");
+        // IntMatrixStore: check the final counters (IntMatrixStore.java:174-176); the
+        // kernel skips itself once an earlier apply left a negative (sticky neg_dev)
         if (!s->neg_dev) {
             HIPCHK(hipMalloc((void**)&s->neg_dev, sizeof(unsigned long long)));
             HIPCHK(hipMemsetAsync(s->neg_dev, 0xFF, sizeof(unsigned long long), s->stream));

@@ -121,7 +121,7 @@ class ShardGroup:
         # 0.441 ms/step against 0.460 for P = 4 and 0.461 for P = 2)
         self.pieces = pieces
         self._pending: list = []  # pre-reduce handles whose errors are not yet collected
-        self._xbufs: list = []    # exchange receive buffers the store may still read: (event, recv, send)
+        self._xbufs: list = []    # exchange buffers the store may still read: (event, recv, send, push seq)
         self._xpool: list = []    # exchange buffers the store has passed: reused by the next calls
         self._held = None         # the last exchange call's slices, handed to the store next call / flush
         self._k = 0
@@ -325,34 +325,43 @@ class ShardGroup:
             return
         ev = self.torch.cuda.Event()
         ev.record(self._store_stream)
-        # keep the buffers until the store's stream has passed them; passed ones go back
-        # to the pool the next calls allocate from (no allocator churn on GB buffers)
+        seq = self.store.push_seq()
+        # keep the buffers until the store has passed them: its stream's reads (the
+        # event) and its host-side retire of those chunks, which may read the pushes
+        # again (exact replay, int32 rollback, re-run of a failed speculation);
+        # passed ones go back to the pool the next calls allocate from (no allocator
+        # churn on GB buffers)
         keep = []
         for x in self._xbufs:
             if x[0].query():
-                self._xrelease(x[1], x[2])
+                self._xpass(x)
             else:
                 keep.append(x)
-        keep.append((ev, recv, send))
+        keep.append((ev, recv, send, seq))
         while len(keep) > 3:  # bound the memory held for the asynchronous store
             x = keep.pop(0)
             x[0].synchronize()
-            self._xrelease(x[1], x[2])
+            self._xpass(x)
         self._xbufs = keep
+
+    def _xpass(self, x) -> None:
+        """Release an exchange buffer set once the store has retired the call that read it."""
+        self.store.retire(x[3])
+        self._xrelease(x[1], x[2])
 
     def _xalloc(self, n: int, dev):
         """An exchange buffer of at least n bytes: the smallest free pooled one, or new."""
         keep = []
         for x in self._xbufs:  # buffers the store has passed since the last hand-over
             if x[0].query():
-                self._xrelease(x[1], x[2])
+                self._xpass(x)
             else:
                 keep.append(x)
         self._xbufs = keep
         fit = [t for t in self._xpool if t.numel() >= n]
         if fit:
             t = min(fit, key=lambda x: x.numel())
-            self._xpool.remove(t)
+            self._xpool = [x for x in self._xpool if x is not t]  # by identity (tensor == is elementwise)
             return t
         return self.torch.empty(n, dtype=self.torch.uint8, device=dev)
 
@@ -361,7 +370,8 @@ class ShardGroup:
             if all(t is not u for u in self._xpool):
                 self._xpool.append(t)
         while len(self._xpool) > 2:  # keep the largest two (a send and a receive buffer)
-            self._xpool.remove(min(self._xpool, key=lambda x: x.numel()))
+            small = min(self._xpool, key=lambda x: x.numel())
+            self._xpool = [x for x in self._xpool if x is not small]
 
     def push_local(self, dev_ptrs: Sequence[int], lens: Sequence[int]) -> None:
         """Pushes already split to this shard: exact ordered apply, no exchange."""

@@ -193,6 +193,24 @@ class DataStore:
     def flush(self):
         check(_lib.load().dml_store_flush(self._h), self)
 
+    def push_seq(self) -> int:
+        """Number of the last accepted push call (dml_store_push_seq)."""
+        v = C.c_uint64()
+        check(_lib.load().dml_store_push_seq(self._h, C.byref(v)), self)
+        return v.value
+
+    def retire(self, seq: int):
+        """Finish the push calls up to `seq` on the host; their device buffers are
+        no longer read afterwards (dml_store_retire). Raises their deferred error."""
+        check(_lib.load().dml_store_retire(self._h, C.c_uint64(seq)), self)
+
+    def stats(self, reset: bool = False) -> dict:
+        """Pipeline counters (dml_store_stats): chunks, speculative chunks / re-runs,
+        identity / reused / indexed pushes, counted as chunks retire."""
+        c = _lib.dml_store_counters()
+        check(_lib.load().dml_store_stats(self._h, C.byref(c), int(reset)), self)
+        return {f: getattr(c, f) for f, _ in c._fields_}
+
     def handleFetch(self, format: DataDesc, rows: KeyCollection) -> bytes:
         """FloatMatrixStore.handleFetch dense-column layout (:113-174) and siblings."""
         self._check_format(format)
@@ -314,6 +332,12 @@ class DataStore:
 
     def set_timing(self, on: bool):
         check(_lib.load().dml_store_set_timing(self._h, int(on)), self)
+
+    def kernel_name(self) -> str:
+        """Instantiation of the dominant kernel last launched (dml_store_kernel_name)."""
+        buf = C.create_string_buffer(512)
+        check(_lib.load().dml_store_kernel_name(self._h, buf, 512), self)
+        return buf.value.decode()
 
     def kernel_time(self, reset=True):
         ms, n = C.c_double(), C.c_int64()

@@ -66,6 +66,11 @@ extern "C" {
  * synchronous: the call returns after the apply, like the reference's ack
  * (PSAgent.java:278-281). */
 #define DML_FLAG_ASYNC                   0x2
+/* No identity speculation / slot reuse. By default a plain-sum
+ * matrix store that receives full-range device pushes allocates a second shard
+ * buffer (rows*cols values) on first use, when the device has that plus
+ * max(1/8 of its memory, 4 GiB) free; this flag never allocates it. */
+#define DML_FLAG_NO_SPECULATION          0x4
 
 /* Mirrors the six big-endian int32s DataDesc puts on the wire, in wire order
  * (DataDesc.java:62-69). key/value sizes derive as in DataDesc.java:50-51. */
@@ -116,6 +121,32 @@ int dml_store_push_batch_device(dml_store* s, const void* const* dev_bufs, const
 
 /* Read barrier: every accepted push is applied; returns any deferred error. */
 int dml_store_flush(dml_store* s);
+
+/* Buffer release without a full flush (no reference counterpart: the JVM's
+ * byte[] is always copied). Every push call (dml_store_push, _push_batch,
+ * _push_batch_device) is numbered 1, 2, ...; dml_store_push_seq returns the
+ * number of the last accepted one. dml_store_retire(s, seq) finishes every chunk
+ * of the calls up to `seq` on the host (exact replays, int32 rollbacks, re-runs of
+ * failed speculation: the reads of a push that may follow its device apply); when
+ * it returns, those calls' device buffers are no longer read and may be reused or
+ * freed. Returns the first error those chunks met (sticky, as for flush). */
+int dml_store_push_seq(dml_store* s, uint64_t* seq);
+int dml_store_retire(dml_store* s, uint64_t seq);
+
+/* Pipeline counters since creation or the last reset (diagnostic): chunks
+ * retired, speculative chunks and how many of them re-ran without speculation,
+ * and per push how its records found their rows: identity (record r = row r,
+ * verified in the reduce), reused (a kept slot-table column, verified), indexed
+ * (the key index). Counted when a chunk retires: flush first. */
+typedef struct dml_store_counters {
+    int64_t chunks;
+    int64_t spec_chunks;
+    int64_t spec_reruns;
+    int64_t identity_pushes;
+    int64_t reused_pushes;
+    int64_t indexed_pushes;
+} dml_store_counters;
+int dml_store_stats(dml_store* s, dml_store_counters* out, int32_t reset);
 
 /* First error the store has seen (sticky until dml_store_clear_error):
  * status code, the key and column the reference would report, 0 if none. */
@@ -198,6 +229,11 @@ int dml_store_stream(dml_store* s, void** stream);
  * elapsed ms and the number of timed launches since the last reset. */
 int dml_store_set_timing(dml_store* s, int32_t enable);
 int dml_store_kernel_time(dml_store* s, double* total_ms, int64_t* launches, int32_t reset);
+/* The instantiation of that dominant kernel as last launched, in rocprof's
+ * spelling without "void " and the parameter list (e.g.
+ * "dml::k_reduce_rows<float, 0, 4, 4, true, true, 1, 4, 0>"); "" before any push.
+ * bench.py reports a profile's counted HBM bytes only for the kernel that ran. */
+int dml_store_kernel_name(dml_store* s, char* out, int32_t cap);
 
 /* Elementwise shard += src for a dense device buffer of rows*cols values in the
  * store's layout (owner-side apply after a reduce-scatter). */

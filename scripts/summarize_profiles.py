@@ -10,8 +10,9 @@ the algorithmic bytes of that streamed part (default: all reads streamed).
 
 - profiles/<round>_<tag>_kernel_stats.csv : the --kernel-trace --stats summary (verbatim)
 - profiles/<round>_<tag>_summary.md       : per-kernel table + HBM traffic per key
-- profiles/pmc_traffic.json               : per_config[<key>] (config2 also at the top level),
-                                            read by bench.py as roofline.traffic
+- profiles/pmc_traffic.json               : per_config[<key>], read by bench.py as roofline.traffic
+                                            only for the same kernel instantiation and device
+                                            sources (src_sha, written on the box by gpu_prof.sh)
 
 HBM bytes per dispatch follow MI355X_MICROARCH.md §HBM: FETCH_SIZE and WRITE_SIZE
 are KiB, collected in separate --pmc passes. On gfx950 FETCH_SIZE reports half
@@ -25,6 +26,7 @@ import csv
 import json
 import os
 import shutil
+import subprocess
 import sys
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
@@ -45,6 +47,15 @@ def main(rnd, tag, cmd, *specs):
     rows = list(csv.DictReader(open(stats)))
     pj = os.path.join(PROF, "pmc_traffic.json")
     d = json.load(open(pj)) if os.path.exists(pj) else {}
+    d = {"per_config": d.get("per_config", {})}
+    src_sha = open(os.path.join(OUT, f"prof_{tag}_src.txt")).read().strip()
+    try:
+        commit = subprocess.run(["git", "-C", ROOT, "rev-parse", "--short", "HEAD"], capture_output=True,
+                                text=True, check=True).stdout.strip()
+        if subprocess.run(["git", "-C", ROOT, "diff", "--quiet", "HEAD", "--", "distml_amd/csrc"]).returncode:
+            commit += "+uncommitted"
+    except Exception:
+        commit = "?"
     md = [f"# {rnd} {tag}: rocprofv3 summary (MI355X)\n",
           f"Command: `rocprofv3 --kernel-trace --stats -- python3 bench.py {cmd}`; counters: separate "
           "`--pmc FETCH_SIZE` and `--pmc WRITE_SIZE` passes of the same command (scripts/gpu_prof.sh).\n",
@@ -71,10 +82,9 @@ def main(rnd, tag, cmd, *specs):
                  "fetch_correction": corr, "fetch_bytes_raw": round(fetch_kib * 1024), "write_bytes": round(write_b),
                  "algorithmic_bytes_per_launch": algo, "traffic_over_algorithmic": round(traffic / algo, 4),
                  "rocprof_avg_ns": avg_ns, "achieved_algorithmic_GBps": round(algo / avg_ns, 1),
-                 "source": f"profiles/{rnd}_{tag}_kernel_stats.csv + FETCH_SIZE/WRITE_SIZE passes ({cmd})"}
-        d.setdefault("per_config", {})[key] = entry
-        if key == "config2":
-            d.update({k: v for k, v in entry.items()})
+                 "source": f"profiles/{rnd}_{tag}_kernel_stats.csv + FETCH_SIZE/WRITE_SIZE passes ({cmd})",
+                 "src_sha": src_sha, "commit": commit}
+        d["per_config"][key] = entry
         md += ["", f"## {key}: `{kpart}` ({nf}/{nw} dispatches sampled)", "",
                (f"- FETCH_SIZE {fetch_kib:.0f} KiB x 1024 x 2 = {read_b/1e9:.4f} GB read (gfx950 wide-read correction)"
                 if stream is None else

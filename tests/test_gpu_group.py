@@ -125,7 +125,10 @@ XR, XC, XW = 2000, 200, 4
 XADA = (0.025, 0.0001, 1.5)
 
 
-XCALLS = 2  # back-to-back exchange calls, no flush between them (the pipelined path)
+# back-to-back exchange calls, no flush between them (the pipelined path); the pooled
+# receive buffers are reused from the third call on, after the store retired the call
+# that read them (call 1 repeats a row: its chunk replays that row at retire)
+XCALLS = 4
 
 
 def _xbuckets(vt, rank, call=0):
@@ -134,6 +137,8 @@ def _xbuckets(vt, rank, call=0):
     for b in range(XW):
         rng = np.random.default_rng(500 * rank + 50 * call + b)
         keys = rng.permutation(XR)[: rng.integers(XR // 4, XR)]
+        if call == 1 and b == 0 and rank == 0:
+            keys[5] = keys[17]  # one row listed twice (the exact replay)
         vals = ((rng.standard_normal((len(keys), XC)) * 0.6).astype(np.float32) if vt == 1
                 else rng.integers(-2, 3, size=(len(keys), XC)).astype(np.int32))
         out.append(np.frombuffer(encode_matrix_push(keys, vals, 0, vt), np.uint8).copy())
@@ -157,12 +162,14 @@ def _xworker(rank, world, port, vt, out_dir):
     g.store.load_values(_init(vt, XR, XC)[sh.firstKey:sh.lastKey + 1])
     if vt == 1:
         g.store.setAlpha(*XADA)
+    keep = []  # push buffers stay allocated until flush() (the group's contract)
     for call in range(XCALLS):
         bufs = [torch.from_numpy(b).cuda() for b in _xbuckets(vt, rank, call)]
         torch.cuda.synchronize()
         g.push_exchange([b.data_ptr() for b in bufs], [b.numel() for b in bufs])
-        del bufs  # the split copied them
+        keep.append(bufs)
     g.flush()
+    del keep
     np.save(os.path.join(out_dir, f"data{rank}.npy"), g.store.values())
     if vt == 1:
         a, d = g.store.adagrad_state()
@@ -176,7 +183,7 @@ def _xworker(rank, world, port, vt, out_dir):
 @pytest.mark.parametrize("world,vt", [(2, 1), (3, 1), (2, 0)])
 def test_exchange_hip_multiprocess(tmp_path, oracle, world, vt):
     """push_exchange with the real dml_shard_split and HIP stores (ranks share cuda:0,
-    all-to-all over gloo through the host), two calls back to back without a flush:
+    all-to-all over gloo through the host), four calls back to back without a flush:
     bit-exact against one oracle store fed every call's pushes, rank-major per call; each shard's maxDelta against an oracle
     shard fed the same pushes restricted to its keys."""
     import torch.multiprocessing as mp

@@ -100,9 +100,15 @@ def rand_matrix_pushes(rng, first, rows, cols, key_type, value_type, n, row_frac
     (1, 0, 1024, 3, 1.0, False), (1, 0, 200, 9, 0.5, False), (1, 1, 37, 70, 0.3, False),
     (1, 0, 5, 4, 1.0, True), (3, 0, 10, 6, 0.7, False), (3, 1, 33, 3, 1.0, True),
     (0, 0, 1000, 5, 0.2, False), (0, 0, 7, 66, 0.5, False), (0, 1, 16, 3, 1.0, True),
+    # rows wider than one wave's 4 chunks (two waves per row: neither hands the slot rows back)
+    (1, 0, 1280, 4, 0.6, False), (1, 0, 2048, 3, 0.8, True), (3, 1, 640, 5, 0.5, False),
+    (0, 0, 1500, 4, 0.5, False), (1, 0, 700, 4, 0.6, False),
 ])
-@pytest.mark.parametrize("api", ["batch", "device"])
+@pytest.mark.parametrize("api", ["batch", "device", "device_calls"])
 def test_matrix_random_parity(oracle, value_type, key_type, cols, nb, frac, dup, api):
+    """Random pushes (key subsets, permuted, optionally repeated rows) for every value
+    type and many widths, bit-exact. `device_calls`: one device call per push, six
+    calls in flight over the three workspaces (slot tables handed back or memset)."""
     from distml_amd import DataDesc
     rng = np.random.default_rng(cols * 1000 + nb)
     first, rows = 1000, 300
@@ -123,7 +129,11 @@ def test_matrix_random_parity(oracle, value_type, key_type, cols, nb, frac, dup,
     else:
         bufs = [torch.frombuffer(bytearray(p), dtype=torch.uint8).cuda() for p in pushes]
         torch.cuda.synchronize()
-        s.pushDevice([b.data_ptr() for b in bufs], [b.numel() for b in bufs])
+        if api == "device":
+            s.pushDevice([b.data_ptr() for b in bufs], [b.numel() for b in bufs])
+        else:
+            for b in bufs:
+                s.pushDevice([b.data_ptr()], [b.numel()])
         s.flush()
     assert kat.bits_equal(s.values(), o.data)
     s.close()
@@ -493,6 +503,94 @@ def test_config2_dense_fp32_full_size_bit_exact(oracle):
     host = [oracle.synth_dense_bucket(0, 1, 0, rows, rows, cols, 1000 + b, *perms[b]) for b in range(W)]
     assert o.push_many(host, threads=8) == 0
     assert kat.bits_equal(s.values(), o.data)
+
+
+@pytest.mark.parametrize("order", ["position", "shuffled"])
+def test_config2_headline_steady_state_bit_exact(oracle, order):
+    """Exactly what bench.py's N=1 headline times, at full size: a 16 384 x 1 024 fp32
+    shard, two 32-push sets (16 ascending + 16 permuted, the bench's perm_for, value
+    seeds 1000+b and 5000+b) pushed alternately, six pushDevice calls without a flush.
+    Chunks 3..5 find their workspace's kept slot table (chunk j-3's), so their 16
+    permuted pushes reuse kept columns instead of the key index — asserted through
+    dml_store_stats — and the shard is bytes-equal to the oracle fed the same 192
+    pushes in order (FloatMatrixStore.java:200-222). `shuffled`: every call applies
+    its 32 pushes in a new seeded order (the selector's arrival order,
+    PSAgent.java:166-186); the content-keyed reuse still engages."""
+    from distml_amd import DataDesc, _lib
+    rows, cols, W, calls = 16384, 1024, 32, 6
+    fmt = DataDesc(1, 0, 1)
+    L = _lib.load()
+    s, _ = mk_store(fmt, 0, rows - 1, cols, async_push=True)
+    s.synth_fill(7)
+    perms = [config2_perm(b) for b in range(W)]
+    sets = [synth_device_buckets(L, fmt.to_c(), 0, rows, rows, cols, [seed0 + b for b in range(W)], perms)
+            for seed0 in (1000, 5000)]
+    rng = np.random.default_rng(2024)
+    orders = [rng.permutation(W) if order == "shuffled" else np.arange(W) for _ in range(calls)]
+    s.stats(reset=True)
+    for c in range(calls):
+        bs = [sets[c & 1][j] for j in orders[c]]
+        s.pushDevice([b.data_ptr() for b in bs], [b.numel() for b in bs])
+    s.flush()
+    st = s.stats()
+    assert st["chunks"] == calls and st["spec_chunks"] == calls and st["spec_reruns"] == 0, st
+    assert st["identity_pushes"] == 16 * calls, st
+    assert st["reused_pushes"] == 16 * (calls - 3) and st["indexed_pushes"] == 16 * 3, st
+    got = s.values()
+    s.close()
+    del sets
+    o = oracle_store(oracle, fmt, 0, rows - 1, cols)
+    o.synth_fill(7)
+    host = [[oracle.synth_dense_bucket(0, 1, 0, rows, rows, cols, seed0 + b, *perms[b]) for b in range(W)]
+            for seed0 in (1000, 5000)]
+    assert o.push_many([host[c & 1][j] for c in range(calls) for j in orders[c]], threads=16) == 0
+    assert kat.bits_equal(got, o.data)
+
+
+def test_config5_model_leg_bit_exact(oracle):
+    """bench.py's config-5 leg at N = 1, full size: the 1 000 000 x 1 000 int32
+    IntMatrixStore (4 GB) and its 32 pushes of 65 536 distinct rows (the leg's seeds
+    and permutations), then the 32 negated pushes (the leg's second step); bit-exact
+    against the oracle with the negativity check after each add
+    (IntMatrixStore.java:164-178), no error."""
+    from distml_amd import DataDesc, _lib
+    import math
+    rows, cols, W, nrec = 1_000_000, 1000, 32, 65536
+    fmt = DataDesc(1, 0, 0)
+    L = _lib.load()
+
+    def coprime(a, n):
+        while math.gcd(a, n) != 1:
+            a += 1
+        return a
+
+    perms = [(coprime(((4000 + b) * 2654435761) % rows | 1, rows), (b * 331) % rows) for b in range(W)]
+    s, _ = mk_store(fmt, 0, rows - 1, cols, async_push=True)
+    s.synth_fill(11)
+    pos = synth_device_buckets(L, fmt.to_c(), 0, rows, nrec, cols, [4000 + b for b in range(W)], perms)
+    neg = []
+    for t in pos:
+        n = t.clone().view(torch.int32).view(nrec, 1 + cols)
+        n[:, 1:] = -n[:, 1:]
+        neg.append(n.view(torch.uint8).view(-1))
+    torch.cuda.synchronize()
+    s.pushDevice([b.data_ptr() for b in pos], [b.numel() for b in pos])
+    s.pushDevice([b.data_ptr() for b in neg[:16]], [b.numel() for b in neg[:16]])
+    s.flush()
+    assert s.error_state()[0] == 0
+    got = s.values()
+    s.close()
+    del pos, neg
+    o = oracle_store(oracle, fmt, 0, rows - 1, cols)
+    o.synth_fill(11)
+    host = [oracle.synth_dense_bucket(0, 0, 0, rows, nrec, cols, 4000 + b, *perms[b]) for b in range(W)]
+    negh = []
+    for h in host[:16]:
+        t = h.view(np.int32).reshape(nrec, 1 + cols).copy()
+        t[:, 1:] = -t[:, 1:]
+        negh.append(t.view(np.uint8).reshape(-1))
+    assert o.push_many(host + negh, threads=16) == 0
+    assert kat.bits_equal(got, o.data)
 
 
 def test_config3_sparse_fp32_full_size_bit_exact(oracle):
@@ -878,6 +976,98 @@ def test_exchange_rccl_world1_adagrad(oracle, calls):
         assert g.store.maxDelta() == o.max_delta()
     finally:
         dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("binding", ["torch", "native"])
+@pytest.mark.parametrize("case", ["repeat_adagrad", "negative_int32"])
+def test_exchange_buffer_reuse_after_retire(oracle, binding, case):
+    """The exchange path's receive buffers are reused two calls later (native: two
+    alternating sets; torch: a pool). A store chunk may read its pushes again when it
+    retires on the host — the exact replay of a row a push repeats, the int32
+    rollback past a negative counter — so a set is rewritten only after the store
+    retired the call that read it (dml_store_retire). Six calls of two
+    pushes at world 1 over RCCL, each push with keys outside the matrix (the split
+    path, not the world-1 hand-through); call 1 repeats a row (AdaGrad: replayed) or
+    drives a counter negative (IllegalStateException at a later call or the flush).
+    Bit-exact against the oracle fed the client-split pushes in order, stopping where
+    it throws (IntMatrixStore.java:174-176)."""
+    import socket
+    import torch.distributed as dist
+    from distml_amd import DataDesc, DistMLException, encode_matrix_push
+    from distml_amd.group import NativeShardGroup, ShardGroup
+    rows, cols, calls, per = 1200, 64, 6, 2
+    ada = case == "repeat_adagrad"
+    fmt = DataDesc(1, 0, 1, False, True, True) if ada else DataDesc(1, 0, 0)
+    rng = np.random.default_rng(17 if ada else 19)
+    host = []
+    for i in range(calls * per):
+        keys = rng.permutation(rows + 40)[: rows // 2] - 20  # a few keys outside the matrix: dropped
+        if ada:
+            vals = (rng.standard_normal((len(keys), cols)) * 0.6).astype(np.float32)
+            if i == per:  # call 1, push 0 lists one row twice
+                inside = np.nonzero((keys >= 0) & (keys < rows))[0]
+                keys[inside[7]] = keys[inside[300]]
+        else:
+            vals = rng.integers(-2, 3, size=(len(keys), cols)).astype(np.int32)
+            if i == per:  # call 1, push 0: a counter goes negative
+                j = int(np.nonzero((keys >= 0) & (keys < rows))[0][250])
+                vals[j, 9] = -1000
+        host.append(encode_matrix_push(keys, vals, 0, fmt.valueType))
+    dev = [torch.frombuffer(bytearray(h), dtype=torch.uint8).cuda() for h in host]  # alive until the end
+    torch.cuda.synchronize()
+    o = oracle_store(oracle, fmt, 0, rows - 1, cols)
+    if ada:
+        o.set_alpha(0.025, 0.0001, 1.5)
+    else:
+        o.synth_fill(11)
+    err = None
+    for h in host:  # the client's split: out-of-matrix keys never reach the server
+        r = np.frombuffer(h, np.uint8).reshape(-1, 4 + 4 * cols)
+        k = r[:, :4].copy().view("<i4").ravel()
+        if o.push(r[(k >= 0) & (k < rows)].tobytes()):
+            err = o.error()
+            break
+    assert (err is None) == ada
+    port = None
+    if binding == "torch":
+        s = socket.socket()
+        s.bind(("127.0.0.1", 0))
+        port = s.getsockname()[1]
+        s.close()
+        dist.init_process_group("nccl", init_method=f"tcp://127.0.0.1:{port}", rank=0, world_size=1,
+                                device_id=torch.device("cuda", 0))
+        g = ShardGroup(fmt, rows, cols, 0, 1, device=0, exchange_only=True)
+    else:
+        g = NativeShardGroup(fmt, rows, cols, 0, 1, NativeShardGroup.unique_id(), device=0)
+    try:
+        if ada:
+            g.store.setAlpha(0.025, 0.0001, 1.5)
+        else:
+            g.store.synth_fill(11)
+        raised = None
+        try:
+            for c in range(calls):
+                sl = dev[c * per:(c + 1) * per]
+                g.push_exchange([d.data_ptr() for d in sl], [d.numel() for d in sl])
+            g.flush()
+        except DistMLException as e:
+            raised = e
+        if ada:
+            assert raised is None, raised
+            a, d = g.store.adagrad_state()
+            assert kat.bits_equal(a, o.alpha) and kat.bits_equal(d, o.delta)
+            assert g.store.maxDelta() == o.max_delta()
+        else:
+            assert raised is not None and (raised.code, raised.key, raised.col) == err
+        assert kat.bits_equal(g.store.values(), o.data)
+    finally:
+        try:
+            g.close()  # the torch group flushes first: the failed store raises again (it refuses pushes)
+        except DistMLException:
+            if ada:
+                raise
+        if port is not None:
+            dist.destroy_process_group()
 
 
 def test_native_group_exchange_world1(oracle):
@@ -1435,9 +1625,9 @@ def test_adagrad_flat_exact(oracle, case, W, cols):
     s.close()
 
 
-@pytest.mark.parametrize("cols", [1024, 256, 200])
+@pytest.mark.parametrize("cols", [1024, 256, 200, 2048, 1280])
 @pytest.mark.parametrize("case", ["same_order", "swapped_late", "duplicate_late", "out_of_shard_late", "order_change",
-                                  "nb_change"])
+                                  "nb_change", "order_shuffled"])
 def test_slot_reuse_exact(oracle, case, cols):
     """Slot reuse: a speculative k_reduce_rows chunk keeps its slot
     table, and the chunk three batches later in the same workspace takes a push's
@@ -1448,8 +1638,11 @@ def test_slot_reuse_exact(oracle, case, cols):
     (the first that can reuse) varies by case: the same orders; push 2 with two
     records swapped where the sample cannot see them; with a row listed twice; with
     an out-of-shard key there; all new orders (batch 6 then repeats batch 3's); nine
-    pushes (another slot-table stride, no reuse). Rows of whole KiB (k_reduce_rows)
-    and of 800 B (k_reduce_flat)."""
+    pushes (another slot-table stride, no reuse); from batch 3 on the six pushes in a
+    new order every batch (arrival order: reuse is keyed by content, not position).
+    Rows of whole 4 KiB (k_reduce_rows FULL; 8 KiB: two chunk groups per row), of 1
+    KiB and 800 B (k_reduce_flat), and of 5 KiB (1280 cols: the pair-packed loop,
+    which never speculates — ADVICE r2)."""
     from distml_amd import DataDesc, DataStore, KeyRange, encode_matrix_push, ArrayIndexOutOfBoundsException
     rows, W = 4000, 6
     fmt = DataDesc(1, 0, 1)
@@ -1466,9 +1659,10 @@ def test_slot_reuse_exact(oracle, case, cols):
     for bi in range(7):
         n = 9 if (case == "nb_change" and bi == 3) else W
         order = new_perms if (case == "order_change" and bi in (3, 6)) else perms
+        pos = rng.permutation(n) if (case == "order_shuffled" and bi >= 3) else np.arange(n)
         host = []
         for b in range(n):
-            keys = order[b].copy()
+            keys = order[pos[b]].copy()
             if bi == 3 and b == 2 and case.endswith("_late"):
                 free = sorted(set(range(rows)) - _sampled_rows(oracle, b, rows))
                 i, j = free[len(free) // 2], free[len(free) // 2 + 3]
@@ -1505,6 +1699,12 @@ def test_slot_reuse_exact(oracle, case, cols):
     got = st.values()
     bad_rows = np.nonzero((got.view(np.uint32) != o.data.view(np.uint32)).any(axis=1))[0]
     assert len(bad_rows) == 0, (len(bad_rows), bad_rows[:8])
+    stats = st.stats()
+    if cols == 1280:
+        assert stats["spec_chunks"] == 0, stats
+    elif case in ("same_order", "order_shuffled"):
+        # batches 3..6 take every push's slots from a kept column (chunk j-3's table)
+        assert stats["reused_pushes"] == 4 * W and stats["spec_reruns"] == 0, stats
     st.close()
 
 

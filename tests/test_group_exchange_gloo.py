@@ -117,11 +117,13 @@ def _worker(rank, world, port, vt, out_dir):
     g = G(fmt, ROWS, COLS, rank, world, device=None, ops=SplitOps(), store_factory=factory, exchange_only=True)
     with pytest.raises(RuntimeError):
         g.push_full_range([], [])  # an exchange-only group holds no partial buffers
+    keep = []  # push buffers stay allocated until flush() (the group's contract)
     for call in range(CALLS):
         bufs = [torch.from_numpy(b) for b in _buckets(vt, rank, call)]
         g.push_exchange([b.data_ptr() for b in bufs], [b.numel() for b in bufs])
-        del bufs  # the split copied them: the caller may reuse its buffers at once
+        keep.append(bufs)
     g.flush()
+    del keep
     o = g.store.o
     np.save(os.path.join(out_dir, f"data{rank}.npy"), o.data)
     if fmt.adaGrad:
