@@ -71,6 +71,40 @@ C5_ROWS, C5_COLS, C5_W, C5_NNZ = 1_000_000, 1000, 32, 65536  # LDA word-topic co
 SHUFFLE_ORDERS = 64                      # seeded push orders of the headline's arrival-order sub-line
 
 
+# ---------------------------------------------------------------- HBM footprint
+HBM_BYTES = 288e9                        # MI355X HBM3E per GPU
+WS_BYTES_PER_ROW = 64 * 4 + 4            # slot table row (kMaxW int32) + rowflag, per workspace
+
+
+def hbm_check(torch, leg: str, parts: dict) -> None:
+    """Fail fast (exit 3, with a message) when a leg's per-rank HBM footprint — the
+    sum of `parts`, bytes — would not fit the device, before anything is allocated."""
+    cap = HBM_BYTES
+    try:
+        cap = min(cap, float(torch.cuda.get_device_properties(torch.cuda.current_device()).total_memory))
+    except Exception:
+        pass
+    total = sum(parts.values())
+    if total > 0.97 * cap:
+        detail = ", ".join(f"{k} {v / 1e9:.1f} GB" for k, v in parts.items())
+        sys.stderr.write(f"bench.py: leg {leg} needs {total / 1e9:.1f} GB of HBM per rank ({detail}); "
+                         f"the device has {cap / 1e9:.1f} GB\n")
+        raise SystemExit(3)
+
+
+def store_bytes(rows: int, cols: int, vbytes: int, spec: bool = False, ada: bool = False) -> float:
+    """A dml_store: the shard (+ its second buffer under speculation, + AdaGrad's alpha
+    and delta) and the three-workspace ring."""
+    arrays = 1 + (1 if spec else 0) + (2 if ada else 0)
+    return arrays * rows * cols * vbytes + 3 * rows * WS_BYTES_PER_ROW
+
+
+def group_bytes(world: int, rows: int, cols: int, vbytes: int) -> float:
+    """ShardGroup's full-range path: two partial / receive sets and the pre-reduce context."""
+    step = (rows - 1 + world) // world
+    return 2 * world * step * cols * vbytes + 2 * step * cols * vbytes + 3 * rows * WS_BYTES_PER_ROW
+
+
 # ---------------------------------------------------------------- launcher
 def _free_port() -> int:
     s = socket.socket()
@@ -317,6 +351,10 @@ def headline(ctx: Ctx, L, args, out_line: dict):
     sharded = world > 1 or args.group
     group = None
     shuffled_batches = None
+    step_rows = (ROWS - 1 + world) // world
+    hbm_check(torch, "config2", {"pushes": 2 * W * BUCKET,
+                                 "store": store_bytes(step_rows if sharded else ROWS, COLS, 4, spec=True),
+                                 "group": group_bytes(world, ROWS, COLS, 4) if sharded else 0})
     if not sharded:
         store = DataStore(fmt, KeyRange(0, ROWS - 1), COLS, device=ctx.local)
         store.synth_fill(7)
@@ -373,6 +411,8 @@ def headline(ctx: Ctx, L, args, out_line: dict):
         timed_store.kernel_time(reset=True)
         if not sharded:
             timed_store.stats(reset=True)
+        else:
+            group.prereduce_stats(reset=True)
         if sharded and timing:
             _pre_time(L, every=16, reset=True)
 
@@ -436,6 +476,11 @@ def headline(ctx: Ctx, L, args, out_line: dict):
         # kernel; per call they read the W pushes and write the full-model partial
         out_line["roofline"] = prereduce_roofline(L, ctx, args.pieces, pre_ms, pre_n,
                                                   W * BUCKET + world * group.step_rows * COLS * 4, "config 2")
+    if sharded:
+        pst = group.prereduce_stats(reset=True)
+        out_line["pushes_per_step"] = {k: round(pst.get(k, 0) / max(pst.get("chunks", 0), 1), 2)
+                                       for k in ("identity_pushes", "reused_pushes", "indexed_pushes")}
+        out_line["spec_reruns"] = pst.get("spec_reruns", 0)
     if group is not None:
         group.close()
     else:
@@ -475,6 +520,8 @@ def sparse_leg(ctx: Ctx, L, steps: int, cpu: bool):
     from distml_amd.store import DeviceBatch
     dim, nnz, w = 10**9, 10**6, 32
     fmt = DataDesc(DataDesc.DATA_TYPE_ARRAY, DataDesc.KEY_TYPE_LONG, DataDesc.ELEMENT_TYPE_FLOAT)
+    # the shard, the pushes, and three partition workspaces (~40 B per record of a chunk)
+    hbm_check(torch, "sparse", {"shard": 4 * dim, "pushes": w * nnz * 12, "workspaces": 3 * 40 * w * nnz})
     store = DataStore(fmt, KeyRange(0, dim - 1), device=ctx.local)
     bufs = []
     st = torch.cuda.current_stream().cuda_stream
@@ -548,6 +595,10 @@ def leg_config4(ctx: Ctx, L, args) -> dict:
     rec = 4 + 4 * cols
     fmt = DataDesc(DataDesc.DATA_TYPE_MATRIX, DataDesc.KEY_TYPE_INT, DataDesc.ELEMENT_TYPE_FLOAT)
     st = torch.cuda.current_stream().cuda_stream
+    sharded = world > 1 or args.group
+    S4 = (rows - 1 + world) // world
+    hbm_check(torch, "config4", {"pushes": w * rows * rec, "store": store_bytes(S4 if sharded else rows, cols, 4, spec=True),
+                                 "group": group_bytes(world, rows, cols, 4) if sharded else 0})
     bufs = []
     asc = args.c4_order == "asc"
     for b in range(w):
@@ -560,7 +611,6 @@ def leg_config4(ctx: Ctx, L, args) -> dict:
     torch.cuda.synchronize()
     ptrs, lens = [b.data_ptr() for b in bufs], [b.numel() for b in bufs]
     group = None
-    sharded = world > 1 or args.group
     if not sharded:
         store = DataStore(fmt, KeyRange(0, rows - 1), cols, device=ctx.local)
         store.synth_fill(13)
@@ -650,6 +700,10 @@ def leg_config4_ada(ctx: Ctx, L, args) -> dict:
     rec = 4 + 4 * cols
     fmt = DataDesc(DataDesc.DATA_TYPE_MATRIX, DataDesc.KEY_TYPE_INT, DataDesc.ELEMENT_TYPE_FLOAT, False, True, True)
     st = torch.cuda.current_stream().cuda_stream
+    S4 = (rows - 1 + world) // world
+    # exchange buffers: a send and a receive set of up to all push bytes each, two in flight
+    hbm_check(torch, "config4_ada", {"pushes": w * rows * rec, "store": store_bytes(S4, cols, 4, ada=True),
+                                     "exchange": 0 if world == 1 else 4 * w * rows * rec})
     bufs = []
     for b in range(w):
         t = torch.empty(rows * rec, dtype=torch.uint8, device="cuda")
@@ -726,6 +780,7 @@ def leg_config5(ctx: Ctx, L, args) -> dict:
     nrec = int(round(C5_NNZ * S / C5_ROWS))
     rec = 4 + 4 * cols
     fmt = DataDesc(DataDesc.DATA_TYPE_MATRIX, DataDesc.KEY_TYPE_INT, DataDesc.ELEMENT_TYPE_INT)
+    hbm_check(torch, "config5", {"pushes": 2 * C5_W * nrec * rec, "store": store_bytes(S, cols, 4)})
     store = DataStore(fmt, shard, cols, device=ctx.local)
     store.synth_fill(11)
     st = torch.cuda.current_stream().cuda_stream
@@ -866,6 +921,9 @@ def run_shard_config(which: str, cpu_s: float, no_cpu: bool) -> dict:
     L = _lib.load()
     rows, cols, W_, nrec = c["rows"], c["cols"], c["W"], c["nrec"]
     fmt = DataDesc(1, 0, c["vt"], False, True, c["ada"] is not None)
+    hbm_check(torch, "config " + which, {"pushes": (2 if c["vt"] == 0 else 1) * W_ * nrec * (4 + 4 * cols),
+                                         "store": store_bytes(rows, cols, 4, spec=c["vt"] == 1 and not c["ada"],
+                                                              ada=c["ada"] is not None)})
     store = DataStore(fmt, KeyRange(0, rows - 1), cols)
     if c["ada"]:
         store.setAlpha(*c["ada"])

@@ -80,11 +80,17 @@ SIGNATURES = {
     "dml_prereduce_stream_wait": (C.c_int, [_vp, _vp]),
     "dml_prereduce_timing": (C.c_int, [_i32]),
     "dml_prereduce_kernel_time": (C.c_int, [_P(C.c_double), _P(_i64), _i32]),
+    "dml_prectx_create": (C.c_int, [_P(dml_desc), _i64, _i64, _i32, _i32, _P(_vp)]),
+    "dml_prectx_destroy": (None, [_vp]),
+    "dml_prectx_stats": (C.c_int, [_vp, _P(dml_store_counters), _i32]),
+    "dml_prereduce_begin_ctx": (C.c_int, [_vp, _P(_vp), _P(_i64), _i32, _vp, _P(_vp)]),
+    "dml_prereduce_verify": (C.c_int, [_vp, _P(_i32)]),
     "dml_shard_split": (C.c_int, [_P(dml_desc), _i32, _i64, _i32, _P(_vp), _P(_i64), _i32, _vp, _i64, _P(_i64), _vp]),
     "dml_group_unique_id": (C.c_int, [_vp, _i32]),
     "dml_group_push_exchange": (C.c_int, [_vp, _P(_vp), _P(_i64), _i32]),
     "dml_group_create": (C.c_int, [_vp, _i32, _i32, _i32, _P(dml_desc), _i64, _i32, _i32, _P(_vp)]),
     "dml_group_store": (C.c_int, [_vp, _P(_vp)]),
+    "dml_group_prereduce_stats": (C.c_int, [_vp, _P(dml_store_counters), _i32]),
     "dml_group_push_full_range": (C.c_int, [_vp, _P(_vp), _P(_i64), _i32]),
     "dml_group_flush": (C.c_int, [_vp]),
     "dml_group_destroy": (None, [_vp]),

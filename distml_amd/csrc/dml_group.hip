@@ -7,8 +7,12 @@
 //   1. ordered pre-reduce of the rank's pushes into a partial of the whole
 //      matrix (dml_prereduce_*, k_reduce_rows in pre-reduce mode), in P row
 //      slices laid out [rank][row];
-//   2. ncclReduceScatter(sum) of each slice on a communication stream as soon
-//      as the slice is written (xGMI under the next slice's pre-reduce);
+//   2. ncclReduceScatter(sum) of the slices on a communication stream, once the
+//      call's speculation is verified: full-range pushes whose records are rows in
+//      order, or the permutations a call three before listed, skip the key index
+//      and the pieces verify every record (dml_prectx); the next call reads the
+//      verdict (a failure re-runs the pieces exactly) and then launches this
+//      call's reduce-scatter, so it runs on xGMI under the next call's pre-reduce;
 //   3. owner apply shard += received on the store's stream.
 // Calls are asynchronous and overlap exactly as in group.py: the next call's key
 // index runs on a high-priority side stream, two partial / receive buffer sets
@@ -61,7 +65,14 @@ struct dml_group {
     void* recv[2] = {nullptr, nullptr};
     hipEvent_t rs_done[2] = {nullptr, nullptr};
     hipEvent_t applied[2] = {nullptr, nullptr};
-    std::deque<dml_prereduce*> pending;
+    dml_prectx* pctx = nullptr;  // speculative pre-reduce (workspace ring with kept slot tables)
+    // calls whose pieces are enqueued but whose partial is not yet reduce-scattered:
+    // the reduce-scatter waits for the call's verdict (dml_prereduce_verify)
+    struct Call {
+        dml_prereduce* h;
+        int set;  // partial / recv buffer set
+    };
+    std::deque<Call> pending;
     int k = 0;
     bool plain = true;  // plain-sum dense matrix: the full-range pre-reduce path applies
     // exchange path (dml_group_push_exchange), two buffer sets alternating by call:
@@ -88,12 +99,36 @@ struct dml_group {
 
 namespace {
 
+// The oldest pending call: read its verdict (a failed speculation re-runs its
+// pieces exactly), then reduce-scatter its partial on the communication stream
+// and apply the received rows on the store's stream; its errors are returned.
+int finish_front(dml_group* g) {
+    dml_group::Call c = g->pending.front();
+    g->pending.pop_front();
+    int rc = dml_prereduce_verify(c.h, nullptr);
+    if (rc == DML_OK) rc = dml_prereduce_stream_wait(c.h, g->rstream);
+    const int64_t S = g->step_rows, P = g->pieces, blk = S / P, W = g->world, C = g->cols;
+    uint8_t* part = (uint8_t*)g->partial[c.set];
+    uint8_t* rcv = (uint8_t*)g->recv[c.set];
+    for (int64_t j = 0; j < P && rc == DML_OK; ++j) {
+        const ncclResult_t r = ncclReduceScatter(part + (size_t)(j * W * blk * C) * g->vbytes,
+                                                 rcv + (size_t)(j * blk * C) * g->vbytes, (size_t)(blk * C), g->dtype,
+                                                 ncclSum, g->comm, g->rstream);
+        if (r != ncclSuccess) rc = set_error(DML_E_HIP, std::string("ncclReduceScatter: ") + ncclGetErrorString(r));
+    }
+    if (rc == DML_OK && hipEventRecord(g->rs_done[c.set], g->rstream) != hipSuccess) rc = set_error(DML_E_HIP, "event");
+    if (rc == DML_OK && hipStreamWaitEvent(g->sstream, g->rs_done[c.set], 0) != hipSuccess)
+        rc = set_error(DML_E_HIP, "stream wait");
+    if (rc == DML_OK) rc = dml_store_apply_dense_device(g->store, rcv, g->shard_rows * C);
+    if (rc == DML_OK && hipEventRecord(g->applied[c.set], g->sstream) != hipSuccess) rc = set_error(DML_E_HIP, "event");
+    const int r2 = dml_prereduce_end(c.h);  // the call's key / repeated-row errors
+    return rc != DML_OK ? rc : r2;
+}
+
 int end_pending(dml_group* g, size_t keep) {
     int rc = DML_OK;
     while (g->pending.size() > keep) {
-        dml_prereduce* p = g->pending.front();
-        g->pending.pop_front();
-        const int r = dml_prereduce_end(p);
+        const int r = finish_front(g);
         if (rc == DML_OK) rc = r;
     }
     return rc;
@@ -103,6 +138,7 @@ void group_free(dml_group* g) {
     if (!g) return;
     (void)hipSetDevice(g->device);
     (void)end_pending(g, 0);
+    if (g->pctx) dml_prectx_destroy(g->pctx);
     if (g->xcnt) (void)hipFree(g->xcnt);
     for (int i = 0; i < 2; ++i) {
         if (g->xsend[i]) (void)hipFree(g->xsend[i]);
@@ -163,6 +199,7 @@ int ensure_partials(dml_group* g) {
         GHIP(hipMalloc(&g->partial[i], part));
         GHIP(hipMalloc(&g->recv[i], rcv));
     }
+    GRC(dml_prectx_create(&g->desc, 0, g->total_rows, g->cols, g->device, &g->pctx));
     return DML_OK;
 }
 
@@ -235,6 +272,15 @@ int dml_group_create(const uint8_t* unique_id, int32_t world, int32_t rank, int3
     return DML_OK;
 }
 
+int dml_group_prereduce_stats(dml_group* g, dml_store_counters* out, int32_t reset) {
+    if (!g || !out) return set_error(DML_E_INVALID_ARG, "null argument");
+    if (!g->pctx) {
+        *out = dml_store_counters{};
+        return DML_OK;
+    }
+    return dml_prectx_stats(g->pctx, out, reset);
+}
+
 int dml_group_store(dml_group* g, dml_store** store) {
     if (!g || !store) return set_error(DML_E_INVALID_ARG, "null group");
     *store = g->store;
@@ -258,37 +304,29 @@ int dml_group_push_full_range(dml_group* g, const void* const* dev_bufs, const i
     const int k = g->k;
     g->k ^= 1;
     dml_prereduce* h = nullptr;
-    GRC(dml_prereduce_begin(&g->desc, 0, g->total_rows, g->cols, dev_bufs, lens, n, g->istream, &h));
+    GRC(dml_prereduce_begin_ctx(g->pctx, dev_bufs, lens, n, g->istream, &h));
     // buffer set k was used two calls ago: its apply (behind its reduce-scatter) is done
     int rc = hipEventSynchronize(g->applied[k]) == hipSuccess ? DML_OK : set_error(DML_E_HIP, "applied wait");
     uint8_t* part = (uint8_t*)g->partial[k];
-    uint8_t* rcv = (uint8_t*)g->recv[k];
-    for (int64_t j = 0; j < P && rc == DML_OK; ++j) {
-        uint8_t* piece = part + (size_t)(j * W * blk * C) * g->vbytes;
-        rc = dml_prereduce_piece(h, blk, S, j * blk, W * blk, piece, g->cstream);
-        if (rc == DML_OK) rc = dml_prereduce_stream_wait(h, g->rstream);
-        if (rc == DML_OK) {
-            const ncclResult_t r = ncclReduceScatter(piece, rcv + (size_t)(j * blk * C) * g->vbytes,
-                                                     (size_t)(blk * C), g->dtype, ncclSum, g->comm, g->rstream);
-            if (r != ncclSuccess) rc = set_error(DML_E_HIP, std::string("ncclReduceScatter: ") + ncclGetErrorString(r));
-        }
-    }
+    for (int64_t j = 0; j < P && rc == DML_OK; ++j)
+        rc = dml_prereduce_piece(h, blk, S, j * blk, W * blk, part + (size_t)(j * W * blk * C) * g->vbytes,
+                                 g->cstream);
     if (rc != DML_OK) {
         (void)dml_prereduce_end(h);
         return rc;
     }
-    GHIP(hipEventRecord(g->rs_done[k], g->rstream));
-    GHIP(hipStreamWaitEvent(g->sstream, g->rs_done[k], 0));
-    GRC(dml_store_apply_dense_device(g->store, rcv, g->shard_rows * C));
-    GHIP(hipEventRecord(g->applied[k], g->sstream));
-    g->pending.push_back(h);
-    return end_pending(g, 1);  // the previous call's errors
+    g->pending.push_back({h, k});
+    // the previous call: verdict, reduce-scatter (under this call's pieces), apply, errors
+    return end_pending(g, 1);
 }
 
 int dml_group_push_exchange(dml_group* g, const void* const* dev_bufs, const int64_t* lens, int32_t n) {
     if (!g || n < 0 || n > kMaxW || (n > 0 && (!dev_bufs || !lens)))
         return set_error(DML_E_INVALID_ARG, "bad push arguments (n must be <= 64)");
     GHIP(hipSetDevice(g->device));
+    // full-range calls still waiting for their reduce-scatter come first: the store
+    // applies calls in order
+    GRC(end_pending(g, 0));
     const int W = g->world;
     const int64_t K = g->desc.key_type == 0 ? 4 : 8;
     const int64_t stride = g->desc.data_type == DML_DATA_TYPE_MATRIX ? K + (int64_t)g->vbytes * g->cols

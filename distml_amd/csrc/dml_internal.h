@@ -123,6 +123,12 @@ struct RowMap {
     int64_t block = 0, stride = 0, off = 0;
     int64_t rows_total = 0;
     void* out = nullptr;
+    // model row of task row t (rows <= INT32_MAX, a Java array: 32-bit division)
+    __host__ __device__ inline int64_t row(int64_t t) const {
+        if (!block) return t;
+        const uint32_t q = (uint32_t)t / (uint32_t)block;
+        return (int64_t)q * stride + off + (int64_t)((uint32_t)t - q * (uint32_t)block);
+    }
 };
 
 struct AdaArgs {

@@ -263,7 +263,7 @@ __global__ __launch_bounds__(64 * WPB) void k_reduce(T* __restrict__ shard, int6
         if (bt.prev && ctrl_abnormal(bt.prev)) break;  // predecessor needs the host first
         const int64_t trow = task / ngroups;
         const int cg = (int)(task - trow * ngroups);
-        const int64_t row = rm.block ? (trow / rm.block) * rm.stride + rm.off + trow % rm.block : trow;
+        const int64_t row = rm.row(trow);
         T* const rowp = rm.out ? (T*)rm.out + trow * (int64_t)cols : shard + row * (int64_t)cols;
         if (rm.block && row >= rm.rows_total) {  // padding row of a short last shard
 #pragma unroll
@@ -582,7 +582,7 @@ __global__ __launch_bounds__(64 * WPB) void k_reduce_rows(T* __restrict__ shard,
     for (int r = 0; r < RPW; ++r) {
         const int64_t trow = tb * RPW + r;
         const int64_t tr = trow < rows ? trow : tb * RPW;
-        row[r] = rm.block ? (tr / rm.block) * rm.stride + rm.off + tr % rm.block : tr;
+        row[r] = rm.row(tr);
         rowp[r] = rm.out ? (T*)rm.out + tr * (int64_t)cols : shard + row[r] * (int64_t)cols;
         if (trow >= rows) continue;
         if (rm.block && row[r] >= rm.rows_total) {  // padding row of a short last shard: zeros
@@ -607,7 +607,10 @@ __global__ __launch_bounds__(64 * WPB) void k_reduce_rows(T* __restrict__ shard,
     // repeated row turns into a no-op the host re-runs without speculation.
     uint64_t ident = 0;
     bool bad = false;
-    if constexpr (MODE == kAdd) {
+    // (the sharded pre-reduce speculates the same way: a failed verification re-runs
+    // the call's pieces before its partial is reduce-scattered, dml_prereduce_verify)
+    constexpr bool kSpecMode = MODE == kAdd || MODE == kPreReduce;
+    if constexpr (kSpecMode) {
         if (bt.spec) {
             if (cut != kNoPos || ctrl->no_dup == 0u) {
                 if (lane == 0) ctrl->spec_ok = 0u;
@@ -836,7 +839,7 @@ __global__ __launch_bounds__(64 * WPB) void k_reduce_rows(T* __restrict__ shard,
             has |= (rr[r] >= 0 ? 1u : 0u) << r;
         }
         // a slot-keeping chunk: every live row of every (full-range) push has a record
-        if (MODE == kAdd && bt.keeps && (has & live) != live) bad = true;
+        if (kSpecMode && bt.keeps && (has & live) != live) bad = true;
         if (!has) continue;
         touched |= has;
         const uint8_t* bp = (const uint8_t*)(((uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)vbase, b)) |
@@ -845,10 +848,12 @@ __global__ __launch_bounds__(64 * WPB) void k_reduce_rows(T* __restrict__ shard,
         int64_t kv[RPW];
 #pragma unroll
         for (int r = 0; r < RPW; ++r) {
-            if constexpr (MODE == kAdd) {
-                // identity push: verify the key of every record taken as row r
-                kv[r] = (bt.keeps || ((ident >> b) & 1ull)) && rr[r] >= 0 ? ld_key(bp + (int64_t)rr[r] * stride, K)
-                                                                         : bt.first + row[r];
+            if constexpr (kSpecMode) {
+                // identity / reused push (every push of a keeping chunk): verify the key
+                // of every record taken as row r
+                kv[r] = bt.spec && (bt.keeps || ((ident >> b) & 1ull)) && rr[r] >= 0
+                            ? ld_key(bp + (int64_t)rr[r] * stride, K)
+                            : bt.first + row[r];
             }
             if constexpr (FULL) {
                 // one address per row; the chunks are immediate offsets of the loads
@@ -867,9 +872,9 @@ __global__ __launch_bounds__(64 * WPB) void k_reduce_rows(T* __restrict__ shard,
                 }
             }
         }
-        if constexpr (MODE == kAdd) {
+        if constexpr (kSpecMode) {
 #pragma unroll
-            for (int r = 0; r < RPW; ++r) bad |= row_index(kv[r], bt.first, rows) != row[r];
+            for (int r = 0; r < RPW; ++r) bad |= row_index(kv[r], bt.first, rm.block ? rm.rows_total : rows) != row[r];
         }
 #pragma unroll
         for (int r = 0; r < RPW; ++r) {
@@ -920,7 +925,7 @@ __global__ __launch_bounds__(64 * WPB) void k_reduce_rows(T* __restrict__ shard,
         }
     }
     if (MODE == kAddCheckI32 && negpos != kNoPos) atomicMin(&ctrl->neg_pos, (unsigned long long)negpos);
-    if (MODE == kAdd && bad) ctrl->spec_ok = 0u;  // an identity push is not: the host re-runs the chunk
+    if (kSpecMode && bad) ctrl->spec_ok = 0u;  // an identity push is not: the host re-runs the chunk
 }
 
 // ---------------------------------------------------------------------------
@@ -954,7 +959,7 @@ __global__ __launch_bounds__(256) void k_reduce_flat(T* __restrict__ shard, int6
     uint64_t cut = ctrl->cutoff;
     if (tail_cut < cut) cut = tail_cut;
     uint64_t ident = 0;  // identity speculation (Batch::spec), see k_reduce_rows
-    if constexpr (MODE == kAdd) {
+    {
         if (bt.spec) {
             if (cut != kNoPos || ctrl->no_dup == 0u) {
                 if (lane == 0) ctrl->spec_ok = 0u;
@@ -969,11 +974,16 @@ __global__ __launch_bounds__(256) void k_reduce_flat(T* __restrict__ shard, int6
     const int nrow = (int)(rows - t0 < (int64_t)R ? rows - t0 : (int64_t)R);
     const int ss = slot_stride(nb);
     int32_t* const ls = s_slot[wid];
-    auto model_row = [&](int64_t t) { return rm.block ? (t / rm.block) * rm.stride + rm.off + t % rm.block : t; };
+    auto model_row = [&](int64_t t) { return rm.row(t); };
     auto out_ptr = [&](int rlj, int cvj) {
         const int64_t t = t0 + rlj;
         return (rm.out ? (T*)rm.out + t * (int64_t)cols : shard + model_row(t) * (int64_t)cols) + cvj * VEC;
     };
+    // speculative verification: lane l < nrow checks the record of task row t0 + l,
+    // model row lrow (its row map evaluated once, not per push round)
+    const int64_t lrow = model_row(t0 + lane);
+    const bool lchk = lane < nrow && !(rm.block && lrow >= rm.rows_total);  // padding rows have no record
+    const int64_t vrows = rm.block ? rm.rows_total : rows;
     // the wave's slot rows into LDS (rows a push repeats, and padding rows, stay -1;
     // the table is handed back clean for the next batch's index)
     for (int e = lane; e < nrow * nb; e += 64) {
@@ -1055,12 +1065,12 @@ __global__ __launch_bounds__(256) void k_reduce_flat(T* __restrict__ shard, int6
             for (int p = 0; p < PB; ++p) {
                 const int b = b0 + p < nb ? b0 + p : nb - 1;
                 const uint8_t* const bp = bt.base[b];
-                if constexpr (MODE == kAdd) {
+                {
                     // verified pushes (identity, reused, or every push of a slot-keeping
                     // chunk): lane l < nrow loads the key of row t0+l's record
-                    const bool kl = b0 + p < nb && (bt.keeps || ((ident >> b) & 1ull)) && lane < nrow;
+                    const bool kl = bt.spec && b0 + p < nb && (bt.keeps || ((ident >> b) & 1ull)) && lane < nrow;
                     const int32_t kr = kl ? ls[lane * kMaxW + b] : 0;
-                    kv[p] = !kl ? bt.first + t0 + lane
+                    kv[p] = !kl ? bt.first + lrow
                                 : kr >= 0 ? ld_key(bp + (int64_t)kr * stride, K) : bt.first - 1;  // no record: fails
                 }
 #pragma unroll
@@ -1081,11 +1091,10 @@ __global__ __launch_bounds__(256) void k_reduce_flat(T* __restrict__ shard, int6
 #pragma unroll
                     for (int e = 0; e < VEC; ++e) acc[j][e] = Elem<T>::add(acc[j][e], u[e]);
                 }
-            if constexpr (MODE == kAdd)
-                if (ident || bt.keeps)
+            if (bt.spec && (ident || bt.keeps)) {
 #pragma unroll
-                    for (int p = 0; p < PB; ++p)
-                        bad |= lane < nrow && row_index(kv[p], bt.first, rows) != t0 + lane;
+                for (int p = 0; p < PB; ++p) bad |= lchk && row_index(kv[p], bt.first, vrows) != lrow;
+            }
         }
     }
 #pragma unroll
@@ -1095,7 +1104,7 @@ __global__ __launch_bounds__(256) void k_reduce_flat(T* __restrict__ shard, int6
             if (MODE == kPreReduce) stg16(op, pack<T>(acc[j]));
             else stg16_nt(op, pack<T>(acc[j]));
         }
-    if (MODE == kAdd && bad) ctrl->spec_ok = 0u;  // an identity push is not: the host re-runs the chunk
+    if (bad) ctrl->spec_ok = 0u;  // an identity push is not: the host re-runs the chunk
 }
 
 // k_ada_flat: FloatMatrixStoreAdaGrad's push (FloatMatrixStoreAdaGrad.java:262-277)

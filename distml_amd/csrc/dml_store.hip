@@ -1643,6 +1643,50 @@ struct dml_prereduce {
     bool timed = false;
     hipEvent_t done_ev = nullptr;  // completion of the last piece: last_ev, or its timing stop event
     std::vector<std::pair<hipEvent_t, hipEvent_t>> tev;  // per-piece start/stop of a timed call
+    // speculative calls of a pre-reduce context (dml_prereduce_begin_ctx)
+    dml_prectx* ctx = nullptr;
+    int wi = -1;            // the context's workspace
+    bool spec = false;      // identity / kept-column speculation, verified by the pieces
+    bool verified = false;  // dml_prereduce_verify ran (the partial is exact)
+    int64_t max_nrec = 0;
+    struct PieceRec {
+        int64_t block, stride, off, ntask;
+        void* out;
+    };
+    std::vector<PieceRec> prec;  // the pieces as launched (a failed verification re-runs them)
+    hipEvent_t rerun_ev = nullptr;
+};
+
+// Pre-reduce context (dml_prectx_*): the sharded path's pre-reduce with the
+// store's speculation. Three workspaces in a ring, like a store's;
+// a verified call keeps its slot table, whose permutations the call three later
+// may reuse. The partial is reduce-scattered only after dml_prereduce_verify has
+// read the pieces' verdict (and re-run them exactly if it failed).
+struct PreWs {
+    uint8_t* base = nullptr;
+    Ctrl* ctrl = nullptr;
+    int32_t* slot = nullptr;
+    uint32_t* rowflag = nullptr;
+    Ctrl* hctrl = nullptr;          // pinned Ctrl, copied after the pieces (or their re-run)
+    hipEvent_t ctrl_ev = nullptr;   // that copy done
+    hipEvent_t free_ev = nullptr;   // the workspace's last call ended (pieces / re-run done)
+    bool used = false, clean = false, kept = false;
+    int kept_nb = 0;
+    uint64_t perm = 0;              // kept columns holding verified permutations (see Workspace)
+};
+struct dml_prectx {
+    std::mutex mu;
+    dml_desc desc{};
+    int64_t first = 0, rows = 0;
+    int32_t cols = 0;
+    int K = 4, V = 4;
+    int64_t stride = 0;
+    int device = 0;
+    size_t slot_bytes = 0;
+    PreWs ws[kRing];
+    int next = 0;
+    hipStream_t xstream = nullptr;  // Ctrl read-back and re-runs
+    dml_store_counters st{};
 };
 
 // Pre-reduce kernel timing (dml_prereduce_timing(every)): one call in `every`
@@ -1661,7 +1705,84 @@ static std::vector<std::pair<hipEvent_t, hipEvent_t>> g_pre_pool;
 static void prereduce_free(dml_prereduce* p) {
     if (p->idx_ev) (void)hipEventDestroy(p->idx_ev);
     if (p->last_ev) (void)hipEventDestroy(p->last_ev);
+    if (p->rerun_ev) (void)hipEventDestroy(p->rerun_ev);
     delete p;
+}
+
+// Read a context call's verdict once its pieces are done; if speculation failed,
+// re-run the call exactly on the context's stream: a fresh slot table, the full
+// key index (repeated rows detected), every recorded piece without speculation.
+static int prereduce_verify(dml_prereduce* p, int32_t* rerun) {
+    if (rerun) *rerun = 0;
+    if (!p->ctx || p->verified) return DML_OK;
+    dml_prectx* x = p->ctx;
+    PreWs& W = x->ws[p->wi];
+    HIPCHK(hipStreamWaitEvent(x->xstream, p->done_ev ? p->done_ev : p->idx_ev, 0));
+    HIPCHK(hipMemcpyAsync(W.hctrl, W.ctrl, sizeof(Ctrl), hipMemcpyDeviceToHost, x->xstream));
+    HIPCHK(hipEventRecord(W.ctrl_ev, x->xstream));
+    HIPCHK(hipEventSynchronize(W.ctrl_ev));
+    const Ctrl h = *W.hctrl;
+    x->st.chunks += 1;
+    if (p->spec && h.spec_ok != 0u) {
+        x->st.spec_chunks += 1;
+        uint64_t perm = 0;
+        for (int b = 0; b < p->nb; ++b) {
+            if (ctrl_identity(&h, h.ident, b)) {
+                x->st.identity_pushes += 1;
+                continue;
+            }
+            if ((h.ident >> b) & 1ull) x->st.reused_pushes += 1;
+            else x->st.indexed_pushes += 1;
+            perm |= 1ull << ctrl_col(&h, b);
+        }
+        // every row verified: the table's columns are the pushes' permutations
+        if (p->rows_done == p->rows) {
+            W.kept = true;
+            W.kept_nb = p->nb;
+            W.perm = perm;
+        }
+    } else if (p->spec) {
+        x->st.spec_chunks += 1;
+        x->st.spec_reruns += 1;
+        x->st.indexed_pushes += p->nb;
+        Batch bt = p->bt;
+        bt.spec = 0;
+        bt.keeps = 0;
+        bt.kept_cols = 0;
+        bt.ident_ok = 0;
+        bt.prev = nullptr;
+        hipStream_t xs = x->xstream;
+        HIPCHK(hipMemsetAsync(W.base, 0xFF, sizeof(Ctrl) + x->slot_bytes, xs));
+        HIPCHK(hipMemsetAsync(W.rowflag, 0, (size_t)x->rows * sizeof(uint32_t), xs));
+        HIPCHK(launch_index(bt, p->nb, p->max_nrec, p->stride, p->K, p->first, p->rows, W.slot, W.rowflag, W.ctrl,
+                            kNoPos, xs));
+        AdaArgs none{};
+        for (const auto& pr : p->prec) {
+            RowMap rm;
+            rm.block = pr.block;
+            rm.stride = pr.stride;
+            rm.off = pr.off;
+            rm.rows_total = p->rows;
+            rm.out = pr.out;
+            HIPCHK(launch_reduce(p->desc.value_type, kPreReduce, pr.out, pr.ntask, p->cols, bt, p->nb, p->stride,
+                                 p->K, W.slot, nullptr, W.ctrl, kNoPos, none, xs, nullptr, LaunchEv{}, rm));
+        }
+        if (!p->rerun_ev) HIPCHK(hipEventCreateWithFlags(&p->rerun_ev, hipEventDisableTiming));
+        HIPCHK(hipEventRecord(p->rerun_ev, xs));
+        p->done_ev = p->rerun_ev;  // consumers of the partial (dml_prereduce_stream_wait) wait for the re-run
+        HIPCHK(hipMemcpyAsync(W.hctrl, W.ctrl, sizeof(Ctrl), hipMemcpyDeviceToHost, xs));
+        HIPCHK(hipEventRecord(W.ctrl_ev, xs));
+        p->bt = bt;
+        p->spec = false;
+        if (rerun) *rerun = 1;
+    } else {
+        for (int b = 0; b < p->nb; ++b) {
+            if (p->bt.ident_ok && ((h.ident >> b) & 1ull)) x->st.identity_pushes += 1;
+            else x->st.indexed_pushes += 1;
+        }
+    }
+    p->verified = true;
+    return DML_OK;
 }
 
 extern "C" {
@@ -1791,6 +1912,7 @@ int dml_prereduce_piece(dml_prereduce* p, int64_t row_block, int64_t row_stride,
     HIPCHK(launch_reduce(p->desc.value_type, kPreReduce, dev_out, ntask_rows, p->cols, p->bt, p->nb, p->stride, p->K,
                          p->slot, nullptr, p->ctrl, kNoPos, none, st, nullptr, ev, rm));
     p->done_ev = ev.stop;
+    p->prec.push_back({row_block, row_stride, row_off, ntask_rows, dev_out});
     // model rows this piece covered: blocks of row_block task rows at row_off + q*row_stride
     for (int64_t t0 = 0; t0 < ntask_rows; t0 += row_block) {
         const int64_t lo = (t0 / row_block) * row_stride + row_off;
@@ -1825,8 +1947,51 @@ int dml_prereduce_stream_wait(dml_prereduce* p, void* stream) {
     return DML_OK;
 }
 
+int dml_prereduce_verify(dml_prereduce* p, int32_t* rerun) {
+    if (!p) return set_err(DML_E_INVALID_ARG, "null pre-reduce");
+    if (!p->ctx) {  // a call without a context does not speculate
+        if (rerun) *rerun = 0;
+        return DML_OK;
+    }
+    std::lock_guard<std::mutex> lk(p->ctx->mu);
+    return prereduce_verify(p, rerun);
+}
+
 int dml_prereduce_end(dml_prereduce* p) {
     if (!p) return set_err(DML_E_INVALID_ARG, "null pre-reduce");
+    if (p->ctx) {
+        dml_prectx* x = p->ctx;
+        std::lock_guard<std::mutex> lk(x->mu);
+        PreWs& W = x->ws[p->wi];
+        int rc = prereduce_verify(p, nullptr);
+        hipError_t e = rc == DML_OK ? hipEventSynchronize(W.ctrl_ev) : hipErrorUnknown;  // pieces / re-run done
+        const Ctrl h = *W.hctrl;
+        if (!p->tev.empty()) {
+            double ms = 0.0;
+            for (auto& t : p->tev) {
+                float v = 0.f;
+                if (e == hipSuccess && hipEventElapsedTime(&v, t.first, t.second) == hipSuccess) ms += v;
+            }
+            std::lock_guard<std::mutex> lk2(g_pre_mu);
+            if (e == hipSuccess) {
+                g_pre_ms += ms;
+                g_pre_launches += (int64_t)p->tev.size();
+            }
+            g_pre_pool.insert(g_pre_pool.end(), p->tev.begin(), p->tev.end());
+            p->tev.clear();
+        }
+        if (rc == DML_OK && e != hipSuccess) rc = set_err(DML_E_HIP, hipGetErrorString(e));
+        else if (rc == DML_OK && h.cutoff != kNoPos) rc = set_err(DML_E_KEY_OUT_OF_SHARD, "pre-reduce: key outside the matrix");
+        else if (rc == DML_OK && h.no_dup == 0u) rc = set_err(DML_E_UNSUPPORTED, "pre-reduce: a push repeats a row");
+        // a kept table stays (not clean); a non-speculative call whose pieces covered every
+        // row through the clearing kernel left it clean; anything else is memset next time
+        W.clean = !W.kept && !p->spec && rc == DML_OK && p->rows_done == p->rows &&
+                  reduce_clears_slots(p->desc.value_type, kPreReduce, p->cols);
+        if (rc != DML_OK) W.kept = false;
+        (void)hipEventRecord(W.free_ev, x->xstream);
+        prereduce_free(p);
+        return rc;
+    }
     hipError_t e = hipEventSynchronize(p->idx_ev);  // index done, Ctrl copied out
     const Ctrl h = *p->hctrl;
     // the workspace is free once the last piece ran
@@ -1856,6 +2021,155 @@ int dml_prereduce_end(dml_prereduce* p) {
     if (e == hipSuccess) ws_release(p->device, WsLease{p->ws, p->ws_bytes, clean, p->hctrl});
     prereduce_free(p);
     return rc;
+}
+
+int dml_prectx_create(const dml_desc* desc, int64_t first_key, int64_t rows, int32_t cols, int32_t device,
+                      dml_prectx** out) {
+    if (!desc || !out || rows <= 0 || cols <= 0) return set_err(DML_E_INVALID_ARG, "bad pre-reduce context arguments");
+    *out = nullptr;
+    if (desc->data_type != 1 || !desc->dense_column || desc->ada_grad)
+        return set_err(DML_E_UNSUPPORTED, "pre-reduce supports dense-column plain matrices");
+    if (desc->value_type != 0 && desc->value_type != 1 && desc->value_type != 3)
+        return set_err(DML_E_BAD_DESC, "bad value type");
+    if (rows > INT32_MAX) return set_err(DML_E_INVALID_ARG, "matrix larger than a Java array");
+    DeviceGuard g(device);
+    auto* x = new (std::nothrow) dml_prectx();
+    if (!x) return set_err(DML_E_NOMEM, "out of host memory");
+    x->desc = *desc;
+    x->first = first_key;
+    x->rows = rows;
+    x->cols = cols;
+    x->K = desc->key_type == 0 ? 4 : 8;
+    x->V = desc->value_type == 3 ? 8 : 4;
+    x->stride = x->K + (int64_t)x->V * cols;
+    x->device = device;
+    x->slot_bytes = (size_t)rows * kMaxW * sizeof(int32_t);
+    auto fail = [&](hipError_t e) {
+        dml_prectx_destroy(x);
+        return set_err(DML_E_HIP, std::string("pre-reduce context: ") + hipGetErrorString(e));
+    };
+    hipError_t e;
+    if ((e = hipStreamCreateWithFlags(&x->xstream, hipStreamNonBlocking)) != hipSuccess) return fail(e);
+    for (PreWs& W : x->ws) {
+        if ((e = hipMalloc((void**)&W.base, sizeof(Ctrl) + x->slot_bytes + (size_t)rows * sizeof(uint32_t))) !=
+            hipSuccess)
+            return fail(e);
+        W.ctrl = (Ctrl*)W.base;
+        W.slot = (int32_t*)(W.base + sizeof(Ctrl));
+        W.rowflag = (uint32_t*)(W.base + sizeof(Ctrl) + x->slot_bytes);
+        if ((e = hipHostMalloc((void**)&W.hctrl, sizeof(Ctrl), hipHostMallocDefault)) != hipSuccess) return fail(e);
+        if ((e = hipEventCreateWithFlags(&W.ctrl_ev, hipEventDisableTiming)) != hipSuccess) return fail(e);
+        if ((e = hipEventCreateWithFlags(&W.free_ev, hipEventDisableTiming)) != hipSuccess) return fail(e);
+    }
+    *out = x;
+    return DML_OK;
+}
+
+void dml_prectx_destroy(dml_prectx* x) {
+    if (!x) return;
+    {
+        std::lock_guard<std::mutex> lk(x->mu);
+        DeviceGuard g(x->device);
+        if (x->xstream) (void)hipStreamSynchronize(x->xstream);
+        for (PreWs& W : x->ws) {
+            if (W.free_ev) (void)hipEventSynchronize(W.free_ev);
+            (void)hipFree(W.base);
+            if (W.hctrl) (void)hipHostFree(W.hctrl);
+            if (W.ctrl_ev) (void)hipEventDestroy(W.ctrl_ev);
+            if (W.free_ev) (void)hipEventDestroy(W.free_ev);
+        }
+        if (x->xstream) (void)hipStreamDestroy(x->xstream);
+    }
+    delete x;
+}
+
+int dml_prectx_stats(dml_prectx* x, dml_store_counters* out, int32_t reset) {
+    if (!x || !out) return set_err(DML_E_INVALID_ARG, "null argument");
+    std::lock_guard<std::mutex> lk(x->mu);
+    *out = x->st;
+    if (reset) x->st = dml_store_counters{};
+    return DML_OK;
+}
+
+int dml_prereduce_begin_ctx(dml_prectx* x, const void* const* dev_bufs, const int64_t* lens, int32_t n, void* stream,
+                            dml_prereduce** out) {
+    if (!x || !out || n < 0 || n > kMaxW || (n > 0 && (!dev_bufs || !lens)))
+        return set_err(DML_E_INVALID_ARG, "bad pre-reduce arguments (n must be <= 64)");
+    std::lock_guard<std::mutex> lk(x->mu);
+    DeviceGuard g(x->device);
+    auto* p = new (std::nothrow) dml_prereduce();
+    if (!p) return set_err(DML_E_NOMEM, "out of host memory");
+    p->desc = x->desc;
+    p->first = x->first;
+    p->rows = x->rows;
+    p->cols = x->cols;
+    p->K = x->K;
+    p->V = x->V;
+    p->stride = x->stride;
+    p->stream = (hipStream_t)stream;
+    p->device = x->device;
+    for (int j = 0; j < n; ++j) {
+        if (lens[j] % p->stride) {
+            delete p;
+            return set_err(DML_E_TRUNCATED, "ragged full-range push");
+        }
+        p->bt.base[j] = (const uint8_t*)dev_bufs[j];
+        p->bt.len[j] = lens[j];
+        p->bt.nrec[j] = lens[j] / p->stride;
+        p->bt.bidx[j] = j;
+        p->max_nrec = std::max(p->max_nrec, p->bt.nrec[j]);
+    }
+    p->nb = n;
+    p->bt.first = x->first;
+    const int wi = x->next;
+    x->next = (x->next + 1) % kRing;
+    PreWs& W = x->ws[wi];
+    p->ctx = x;
+    p->wi = wi;
+    p->ws = W.base;
+    p->ctrl = W.ctrl;
+    p->slot = W.slot;
+    p->rowflag = W.rowflag;
+    p->hctrl = W.hctrl;
+    const int vt = x->desc.value_type;
+    bool full = n > 0;
+    for (int j = 0; j < n && full; ++j) full = p->bt.nrec[j] == x->rows;
+    // full-range pushes of the speculation shapes: identity / kept-column pushes skip
+    // the key index and the pieces verify every record (a failure re-runs the call)
+    p->spec = full && spec_shape(vt, x->cols);
+    p->bt.spec = p->bt.keeps = p->spec ? 1 : 0;
+    p->bt.kept_cols = (p->spec && W.kept && slot_stride(W.kept_nb) == slot_stride(n)) ? W.perm : 0;
+    hipStream_t st = p->stream;
+    hipError_t e = hipSuccess;
+    if (W.used) e = hipStreamWaitEvent(st, W.free_ev, 0);  // its last call's pieces / re-run
+    const bool slots_ok = W.clean || (W.kept && p->spec);
+    if (e == hipSuccess) e = hipMemsetAsync(W.base, 0xFF, sizeof(Ctrl) + (slots_ok ? 0 : x->slot_bytes), st);
+    if (e == hipSuccess && !(W.clean || W.kept)) e = hipMemsetAsync(W.rowflag, 0, (size_t)x->rows * sizeof(uint32_t), st);
+    W.clean = W.kept = false;
+    W.used = true;
+    if (e == hipSuccess && p->spec) {
+        e = launch_ident_check(p->bt, n, p->stride, p->K, x->first, x->rows, W.slot, W.ctrl, st);
+        if (e == hipSuccess && p->bt.kept_cols) e = launch_assign_cols(W.ctrl, n, st);
+    } else if (e == hipSuccess && full && (int64_t)x->rows * slot_stride(n) * 4 > ((int64_t)64 << 20)) {
+        // other shapes: the complete identity check of dml_prereduce_begin
+        e = launch_ident_full(p->bt, n, p->max_nrec, p->stride, p->K, x->first, x->rows, W.ctrl, st);
+        p->bt.ident_ok = 1;
+    }
+    if (e == hipSuccess)
+        e = launch_index(p->bt, n, p->max_nrec, p->stride, p->K, x->first, x->rows, W.slot, W.rowflag, W.ctrl, kNoPos,
+                         st);
+    if (e == hipSuccess) e = hipEventCreateWithFlags(&p->idx_ev, hipEventDisableTiming);
+    if (e == hipSuccess) e = hipEventRecord(p->idx_ev, st);
+    if (e != hipSuccess) {
+        (void)hipStreamSynchronize(st);
+        (void)hipEventRecord(W.free_ev, st);
+        prereduce_free(p);
+        return set_err(DML_E_HIP, hipGetErrorString(e));
+    }
+    const int32_t every = g_pre_timing.load(std::memory_order_relaxed);
+    p->timed = every > 0 && g_pre_calls.fetch_add(1, std::memory_order_relaxed) % every == 0;
+    *out = p;
+    return DML_OK;
 }
 
 // ---- synthetic data --------------------------------------------------------

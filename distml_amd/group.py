@@ -72,6 +72,34 @@ class HipOps:
     def end(self, h) -> None:
         check(_lib.load().dml_prereduce_end(C.c_void_p(h)))
 
+    # speculative pre-reduce within a context (dml_prectx_*)
+    def ctx_create(self, fmt: DataDesc, first: int, rows: int, cols: int, device: int):
+        h = C.c_void_p()
+        check(_lib.load().dml_prectx_create(C.byref(fmt.to_c()), first, rows, cols, device, C.byref(h)))
+        return h.value
+
+    def ctx_destroy(self, ctx) -> None:
+        _lib.load().dml_prectx_destroy(C.c_void_p(ctx))
+
+    def ctx_stats(self, ctx, reset: bool = False) -> dict:
+        c = _lib.dml_store_counters()
+        check(_lib.load().dml_prectx_stats(C.c_void_p(ctx), C.byref(c), int(reset)))
+        return {f: getattr(c, f) for f, _ in c._fields_}
+
+    def begin_ctx(self, ctx, dev_ptrs, lens, stream: int):
+        n = len(dev_ptrs)
+        ptrs = (C.c_void_p * max(n, 1))(*dev_ptrs)
+        ls = (C.c_int64 * max(n, 1))(*lens)
+        h = C.c_void_p()
+        check(_lib.load().dml_prereduce_begin_ctx(C.c_void_p(ctx), ptrs, ls, n, C.c_void_p(stream), C.byref(h)))
+        return h.value
+
+    def verify(self, h) -> bool:
+        """The call's verdict; True when a failed speculation re-ran its pieces."""
+        r = C.c_int32()
+        check(_lib.load().dml_prereduce_verify(C.c_void_p(h), C.byref(r)))
+        return bool(r.value)
+
     def stream_wait(self, h, stream: int) -> None:
         check(_lib.load().dml_prereduce_stream_wait(C.c_void_p(h), C.c_void_p(stream)))
 
@@ -120,7 +148,8 @@ class ShardGroup:
         # pre-reduce, and one launch per call has no per-piece tails (world 1, config 2:
         # 0.441 ms/step against 0.460 for P = 4 and 0.461 for P = 2)
         self.pieces = pieces
-        self._pending: list = []  # pre-reduce handles whose errors are not yet collected
+        self._pending: list = []  # (pre-reduce handle, buffer set) not yet reduce-scattered / checked
+        self._pctx = None         # speculative pre-reduce context (dml_prectx), created on first use
         self._xbufs: list = []    # exchange buffers the store may still read: (event, recv, send, push seq)
         self._xpool: list = []    # exchange buffers the store has passed: reused by the next calls
         self._held = None         # the last exchange call's slices, handed to the store next call / flush
@@ -160,7 +189,7 @@ class ShardGroup:
             if self.partial.is_cuda:
                 torch.cuda.current_stream(self.partial.device).synchronize()
             self._hand_over()
-        if (self.partial.is_cuda and hasattr(self.ops, "begin") and len(dev_ptrs) <= 64
+        if (self.partial.is_cuda and hasattr(self.ops, "begin_ctx") and len(dev_ptrs) <= 64
                 and self.step_rows % self.pieces == 0):
             return self._push_pipelined(dev_ptrs, lens)
         if self.partial.is_cuda:
@@ -177,13 +206,16 @@ class ShardGroup:
 
     def _push_pipelined(self, dev_ptrs, lens) -> None:
         """Pre-reduce in `pieces` row slices; slice j holds rows [q*S + j*S/P, q*S + (j+1)*S/P)
-        of every rank q, laid out [rank][row], so its reduce-scatter (comm stream) runs
-        while slice j+1 is pre-reduced (compute stream).
+        of every rank q, laid out [rank][row].
 
-        Asynchronous across calls: the key index runs on a side stream (overlapping
-        the previous call's pre-reduce), the owner apply is queued on the store's
-        stream behind the reduce-scatter, and the call's key / repeated-row errors are
-        raised by the next call or flush() (like DML_FLAG_ASYNC)."""
+        Speculative and asynchronous across calls (dml_prectx):
+        full-range pushes whose records are rows in order, or the permutations a
+        call three before listed, skip the key index (side stream) and the pieces
+        verify every record. The NEXT call (or flush()) reads this call's verdict —
+        a failure re-runs its pieces exactly — and only then reduce-scatters its
+        partial on the communication stream, under that next call's pieces; the
+        owner apply is queued on the store's stream behind it. Key / repeated-row
+        errors are raised by the next call or flush() (like DML_FLAG_ASYNC)."""
         torch = self.torch
         S, P, cols, world = self.step_rows, self.pieces, self.cols, self.world
         blk = S // P
@@ -196,8 +228,10 @@ class ShardGroup:
         # the key index reads the push keys too: it orders after the producers as well
         self.istream.wait_event(self._ready)
         st = self.cstream.cuda_stream
-        partial, recv = self._partials[k], self._recvs[k]
-        h = self.ops.begin(self.fmt, 0, self.total_rows, cols, dev_ptrs, lens, self.istream.cuda_stream)
+        partial = self._partials[k]
+        if self._pctx is None:
+            self._pctx = self.ops.ctx_create(self.fmt, 0, self.total_rows, cols, self.device)
+        h = self.ops.begin_ctx(self._pctx, dev_ptrs, lens, self.istream.cuda_stream)
         # buffer set k was last used two calls ago: its apply (queued behind its
         # reduce-scatter) has finished with recv[k], and so has the scatter with partial[k]
         self._applied[k].synchronize()
@@ -205,26 +239,44 @@ class ShardGroup:
             for j in range(P):
                 piece = partial[j * world * blk * cols:(j + 1) * world * blk * cols]
                 self.ops.piece(h, blk, S, j * blk, world * blk, piece.data_ptr(), st)
-                self.ops.stream_wait(h, self.comm.cuda_stream)  # in-packet completion event of the piece
-                with torch.cuda.stream(self.comm):
-                    self._rs(recv[j * blk * cols:(j + 1) * blk * cols], piece)
         except BaseException:
             self.ops.end(h)
             raise
-        self._rs_done[k].record(self.comm)
-        if self._store_stream is not None:
-            self._store_stream.wait_event(self._rs_done[k])
-        else:
-            self.comm.synchronize()
-        self.ops.apply(self.store, recv.data_ptr(), self.shard.size() * cols)
-        if self._store_stream is not None:
-            self._applied[k].record(self._store_stream)
-        self._pending.append(h)
-        self._end_pending(keep=1)  # the previous call's pieces are done by now or soon
+        self._pending.append((h, k))
+        self._end_pending(keep=1)  # the previous call: verdict, reduce-scatter, apply, errors
+
+    def _finish(self, h, k) -> None:
+        """A pending call: verdict (exact re-run if the speculation failed), its slices'
+        reduce-scatter on the communication stream, the owner apply, its errors."""
+        torch = self.torch
+        S, P, cols, world = self.step_rows, self.pieces, self.cols, self.world
+        blk = S // P
+        try:
+            self.ops.verify(h)
+            self.ops.stream_wait(h, self.comm.cuda_stream)  # the pieces (or their re-run)
+            partial, recv = self._partials[k], self._recvs[k]
+            with torch.cuda.stream(self.comm):
+                for j in range(P):
+                    self._rs(recv[j * blk * cols:(j + 1) * blk * cols],
+                             partial[j * world * blk * cols:(j + 1) * world * blk * cols])
+            self._rs_done[k].record(self.comm)
+            if self._store_stream is not None:
+                self._store_stream.wait_event(self._rs_done[k])
+            else:
+                self.comm.synchronize()
+            self.ops.apply(self.store, recv.data_ptr(), self.shard.size() * cols)
+            if self._store_stream is not None:
+                self._applied[k].record(self._store_stream)
+        finally:
+            self.ops.end(h)
 
     def _end_pending(self, keep: int = 0) -> None:
         while len(self._pending) > keep:
-            self.ops.end(self._pending.pop(0))
+            self._finish(*self._pending.pop(0))
+
+    def prereduce_stats(self, reset: bool = False) -> dict:
+        """dml_prectx_stats of the speculative pre-reduce (identity / reused / indexed pushes)."""
+        return self.ops.ctx_stats(self._pctx, reset) if self._pctx is not None else {}
 
     def record_stride(self) -> int:
         f = self.fmt
@@ -251,6 +303,7 @@ class ShardGroup:
         torch, dist = self.torch, self.dist
         n, world = len(dev_ptrs), self.world
         stride = self.record_stride()
+        self._end_pending(0)  # full-range calls still waiting for their reduce-scatter come first
         dev = self.partial.device
         if world == 1 and n and self.partial.is_cuda and self._whole_shard(dev_ptrs, lens, stride):
             # one owner and every key inside the matrix: the split would copy each push
@@ -407,6 +460,9 @@ class ShardGroup:
         try:
             self.flush()
         finally:
+            if self._pctx is not None:
+                self.ops.ctx_destroy(self._pctx)
+                self._pctx = None
             self.store.close()
             self._partials = self._recvs = []
             self.partial = self.recv = None
@@ -457,6 +513,11 @@ class NativeShardGroup:
 
     def flush(self) -> None:
         check(self._L.dml_group_flush(C.c_void_p(self._h)), self.store)
+
+    def prereduce_stats(self, reset: bool = False) -> dict:
+        c = _lib.dml_store_counters()
+        check(self._L.dml_group_prereduce_stats(C.c_void_p(self._h), C.byref(c), int(reset)))
+        return {f: getattr(c, f) for f, _ in c._fields_}
 
     def close(self) -> None:
         if self._h:

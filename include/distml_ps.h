@@ -273,6 +273,27 @@ int dml_prereduce_stream_wait(dml_prereduce* p, void* stream);
 int dml_prereduce_timing(int32_t every);
 int dml_prereduce_kernel_time(double* ms, int64_t* launches, int32_t reset);
 
+/* Speculative pre-reduce (the sharded path's per-call cost). A
+ * context holds a ring of three workspaces for one matrix (rows*cols, the
+ * whole model) on `device`. _begin_ctx is _begin within the context: full-range
+ * pushes whose sampled records say "record r holds row r", or that match a
+ * permutation a call three before listed (kept slot-table columns, any
+ * position), skip the key index, and the pieces verify every record's key.
+ * dml_prereduce_verify waits for the pieces and reads their verdict; if a
+ * record was not what the sample said, it re-runs the call exactly (fresh
+ * table, full key index, every piece as launched) on the context's stream and
+ * sets *rerun. Consume the partial (reduce-scatter) only after verify, behind
+ * dml_prereduce_stream_wait; _end then reports the call's errors as before.
+ * dml_prectx_stats counts calls as dml_store_stats counts chunks. */
+typedef struct dml_prectx dml_prectx;
+int dml_prectx_create(const dml_desc* desc, int64_t first_key, int64_t rows, int32_t cols, int32_t device,
+                      dml_prectx** out);
+void dml_prectx_destroy(dml_prectx* ctx);
+int dml_prectx_stats(dml_prectx* ctx, dml_store_counters* out, int32_t reset);
+int dml_prereduce_begin_ctx(dml_prectx* ctx, const void* const* dev_bufs, const int64_t* lens, int32_t n,
+                            void* stream, dml_prereduce** out);
+int dml_prereduce_verify(dml_prereduce* p, int32_t* rerun);
+
 /* --- per-shard split of device-resident pushes (multi-GPU exchange path) -- */
 
 /* The client-side split of SparseMatrix.push / SparseArray.push
@@ -307,6 +328,9 @@ int dml_group_create(const uint8_t* unique_id, int32_t world, int32_t rank, int3
                      int64_t total_rows, int32_t cols, int32_t pieces, dml_group** out);
 /* The rank's shard store (fetch / checkpoint / read), owned by the group. */
 int dml_group_store(dml_group* g, dml_store** store);
+/* dml_prectx_stats of the group's speculative pre-reduce (zeros before the first
+ * full-range call). */
+int dml_group_prereduce_stats(dml_group* g, dml_store_counters* out, int32_t reset);
 int dml_group_push_full_range(dml_group* g, const void* const* dev_bufs, const int64_t* lens, int32_t n);
 /* The exact path (AdaGrad, int32-checked, arrays, key-subset pushes): each of the
  * rank's n device-resident pushes is split by owner shard (dml_shard_split), the

@@ -19,7 +19,7 @@ def _run(n):
                           env=env, capture_output=True, text=True, timeout=240)
 
 
-@pytest.mark.parametrize("n", [2, 3])
+@pytest.mark.parametrize("n", [2, 3, 4, 8])
 def test_bench_self_launch_ranks(n):
     r = _run(n)
     assert r.returncode == 0, r.stderr[-2000:]
@@ -37,3 +37,24 @@ def test_bench_launcher_propagates_failure():
     r = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "2", "--config", "4"],
                        env=env, capture_output=True, text=True, timeout=240)
     assert r.returncode != 0
+
+
+def test_hbm_footprint_check():
+    """bench.py refuses (exit 3, with a message) a leg whose per-rank HBM footprint
+    exceeds the device before it allocates anything (VERDICT r2 #7)."""
+    sys.path.insert(0, ROOT)
+    import bench
+
+    class NoGpu:  # get_device_properties fails without a GPU: the 288 GB spec applies
+        class cuda:
+            @staticmethod
+            def current_device():
+                raise RuntimeError("no GPU")
+
+    bench.hbm_check(NoGpu, "fits", {"pushes": 128.6e9, "store": bench.store_bytes(10_000_000, 200, 4, spec=True)})
+    with pytest.raises(SystemExit) as ei:
+        bench.hbm_check(NoGpu, "too big", {"pushes": 40 * 8.04e9})
+    assert ei.value.code == 3
+    # the config-4 leg at N = 8: 16 pushes of the full model per rank + the sharded path's buffers
+    s4 = bench.store_bytes(1_250_000, 200, 4, spec=True) + bench.group_bytes(8, 10_000_000, 200, 4)
+    assert 16 * 10_000_000 * 804 + s4 < 0.97 * bench.HBM_BYTES

@@ -23,10 +23,20 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 pytestmark = pytest.mark.gpu
 
 
-def _buckets(pyoracle, vt, rank, W, rows, cols):
+def _buckets(pyoracle, vt, rank, W, rows, cols, call=0):
     # multipliers coprime with 1000: every push lists each row once, in a permuted order
-    return [pyoracle.synth_dense_bucket(0, vt, 0, rows, rows, cols, 100 * rank + b, (1, 3, 7, 9, 11)[b % 5], 13 * b)
-            for b in range(W)]
+    # (push 0 ascending); call 2: rank 0's push 0 has two records swapped where the
+    # speculative pre-reduce's sample cannot see them (its pieces fail verification and
+    # the call re-runs with the key index; the sums are unchanged)
+    out = [pyoracle.synth_dense_bucket(0, vt, 0, rows, rows, cols, 1000 * call + 100 * rank + b,
+                                       (1, 3, 7, 9, 11)[b % 5], 13 * b) for b in range(W)]
+    if call == 2 and rank == 0:
+        sampled = {t * (rows - 1) // 31 for t in range(32)} | {pyoracle.splitmix64(t) % rows for t in range(32, 64)}
+        free = sorted(set(range(rows)) - sampled)
+        rec = out[0].reshape(rows, -1)
+        i, j = free[len(free) // 2], free[len(free) // 2 + 1]
+        rec[[i, j]] = rec[[j, i]]
+    return out
 
 
 def _init(vt, rows, cols):
@@ -51,13 +61,18 @@ def _worker(rank, world, port, vt, rows, cols, W, pieces, out_dir):
     g = ShardGroup(fmt, rows, cols, rank, world, device=0, pieces=pieces)
     sh = g.shard
     g.store.load_values(_init(vt, rows, cols)[sh.firstKey:sh.lastKey + 1])
-    bufs = [torch.from_numpy(b).cuda() for b in _buckets(pyoracle, vt, rank, W, rows, cols)]
-    torch.cuda.synchronize()
+    keep = []
     pipelined = g.step_rows % pieces == 0
-    for _ in range(2):  # twice: the second step reuses the pooled pre-reduce workspace
+    for call in range(CALLS):  # back to back: workspaces and kept slot tables are reused
+        bufs = [torch.from_numpy(b).cuda() for b in _buckets(pyoracle, vt, rank, W, rows, cols, call)]
+        keep.append(bufs)
+        torch.cuda.synchronize()
         g.push_full_range([b.data_ptr() for b in bufs], [b.numel() for b in bufs],
                           torch.cuda.current_stream().cuda_stream)
     g.flush()
+    if pipelined and cols % 4 == 0:
+        st = g.prereduce_stats()
+        assert st["spec_chunks"] == CALLS and st["spec_reruns"] == (1 if rank == 0 else 0), st
     np.save(os.path.join(out_dir, f"shard{rank}.npy"), g.store.values())
     with open(os.path.join(out_dir, f"path{rank}.txt"), "w") as f:
         f.write("pipelined" if pipelined else "plain")
@@ -73,16 +88,24 @@ def _free_port():
     return p
 
 
+CALLS = 4
+
+
 # (world, vt, rows, pieces): step_rows = ceil-ish linearSplit step
 #   2, 1000 rows -> step 500, pieces 4: pipelined, no padding
 #   3, 1000 rows -> step 334, pieces 2: pipelined, last shard 332 rows (2 padding rows)
 #   3, 1000 rows -> step 334, pieces 4: 334 % 4 != 0 -> one-shot pre-reduce path
 #   2, 1000 rows int32, pieces 4: exact
-@pytest.mark.parametrize("world,vt,rows,pieces,path", [(2, 1, 1000, 4, "pipelined"), (3, 1, 1000, 2, "pipelined"),
-                                                       (3, 1, 1000, 4, "plain"), (2, 0, 1000, 4, "pipelined")])
-def test_shard_group_hip_multiprocess(tmp_path, oracle, world, vt, rows, pieces, path):
+#   cols 64: the speculative pre-reduce (whole vectors); 67: ragged rows, key index
+@pytest.mark.parametrize("world,vt,rows,pieces,path,cols", [
+    (2, 1, 1000, 4, "pipelined", 67), (3, 1, 1000, 2, "pipelined", 67), (3, 1, 1000, 4, "plain", 67),
+    (2, 0, 1000, 4, "pipelined", 67), (2, 1, 1000, 1, "pipelined", 64), (3, 0, 1000, 2, "pipelined", 64)])
+def test_shard_group_hip_multiprocess(tmp_path, oracle, world, vt, rows, pieces, path, cols):
+    """ShardGroup.push_full_range with the HIP kernels at world 2-3 (ranks share cuda:0,
+    gloo reduce-scatter): four calls back to back; call 2 has rank 0 fail the
+    speculative pre-reduce's verification (re-run exactly)."""
     import torch.multiprocessing as mp
-    cols, W = 67, 5
+    W = 5
     mp.spawn(_worker, args=(world, _free_port(), vt, rows, cols, W, pieces, str(tmp_path)), nprocs=world, join=True)
     for r in range(world):
         assert (tmp_path / f"path{r}.txt").read_text() == path
@@ -90,7 +113,7 @@ def test_shard_group_hip_multiprocess(tmp_path, oracle, world, vt, rows, pieces,
     init = _init(vt, rows, cols)
     o = oracle.OracleStore(1, 0, vt, 0, rows - 1, cols)
     o.data[:] = init
-    all_b = [b for _ in range(2) for r in range(world) for b in _buckets(oracle, vt, r, W, rows, cols)]
+    all_b = [b for c in range(CALLS) for r in range(world) for b in _buckets(oracle, vt, r, W, rows, cols, c)]
     for b in all_b:
         assert o.push(b.tobytes()) == 0
     if vt == 0:

@@ -709,6 +709,82 @@ def test_shard_group_rccl_world1(oracle):
         dist.destroy_process_group()
 
 
+@pytest.mark.parametrize("binding", ["torch", "native"])
+@pytest.mark.parametrize("vt", [1, 0])
+def test_sharded_speculation_world1(oracle, binding, vt):
+    """The sharded path's speculative pre-reduce (dml_prectx) at world 1
+    over RCCL: six calls of four full-range pushes (ascending, two fixed permutations,
+    ascending), no flush between them. Calls 3 and 5 reuse the permutations their
+    workspace kept three calls before; call 4's first push has two records swapped
+    where k_ident_check's sample cannot see them, so its pieces fail verification and
+    the call re-runs exactly with the key index before its reduce-scatter. int32 is
+    exact; fp32 within the summation-order bound of tests/test_group_gloo.py."""
+    import socket
+    import torch.distributed as dist
+    from distml_amd import DataDesc, encode_matrix_push
+    from distml_amd.group import NativeShardGroup, ShardGroup
+    rows, cols, calls, W = 1000, 256, 6, 4
+    fmt = DataDesc(1, 0, vt)
+    rng = np.random.default_rng(33 + vt)
+    pa, pb = rng.permutation(rows), rng.permutation(rows)
+    free = sorted(set(range(rows)) - _sampled_rows(oracle, 0, rows))
+    host = []
+    for c in range(calls):
+        for b, keys in enumerate((np.arange(rows), pa, pb, np.arange(rows))):
+            keys = keys.copy()
+            if c == 4 and b == 0:
+                i, j = free[len(free) // 2], free[len(free) // 2 + 1]
+                keys[i], keys[j] = keys[j], keys[i]
+            v = (rng.integers(-3, 4, size=(rows, cols)).astype(np.int32) if vt == 0
+                 else (rng.standard_normal((rows, cols)) * 1e-3).astype(np.float32))
+            host.append(encode_matrix_push(keys, v, 0, vt))
+    dev = [torch.frombuffer(bytearray(h), dtype=torch.uint8).cuda() for h in host]
+    torch.cuda.synchronize()
+    port = None
+    if binding == "torch":
+        s = socket.socket()
+        s.bind(("127.0.0.1", 0))
+        port = s.getsockname()[1]
+        s.close()
+        dist.init_process_group("nccl", init_method=f"tcp://127.0.0.1:{port}", rank=0, world_size=1,
+                                device_id=torch.device("cuda", 0))
+        g = ShardGroup(fmt, rows, cols, 0, 1, device=0)
+    else:
+        g = NativeShardGroup(fmt, rows, cols, 0, 1, NativeShardGroup.unique_id(), device=0)
+    try:
+        g.store.synth_fill(3)
+        for c in range(calls):
+            sl = dev[c * W:(c + 1) * W]
+            if binding == "torch":
+                g.push_full_range([d.data_ptr() for d in sl], [d.numel() for d in sl],
+                                  torch.cuda.current_stream().cuda_stream)
+            else:
+                g.push_full_range([d.data_ptr() for d in sl], [d.numel() for d in sl])
+        g.flush()
+        st = g.prereduce_stats()
+        assert st["chunks"] == calls and st["spec_chunks"] == calls and st["spec_reruns"] == 1, st
+        assert st["reused_pushes"] == 4 and st["identity_pushes"] == 2 * (calls - 1), st
+        got = g.store.values()
+        o = oracle_store(oracle, fmt, 0, rows - 1, cols)
+        o.synth_fill(3)
+        init = o.data.copy()
+        for h in host:
+            assert o.push(h) == 0
+        if vt == 0:
+            assert np.array_equal(got, o.data)
+            return
+        terms = np.abs(init.astype(np.float64))
+        for h in host:
+            rec = np.frombuffer(h, np.uint8).reshape(rows, 4 + 4 * cols)
+            terms[rec[:, :4].copy().view("<i4").ravel()] += np.abs(rec[:, 4:].copy().view("<f4"))
+        diff = np.abs(got.astype(np.float64) - o.data.astype(np.float64))
+        assert np.all(diff <= 2 * len(host) * 2.0 ** -24 * terms)
+    finally:
+        g.close()
+        if port is not None:
+            dist.destroy_process_group()
+
+
 def test_prereduce_pieces_row_map(oracle):
     """dml_prereduce_{begin,piece,end}: slices laid out [rank][row] for a 3-way
     linearSplit of 1000 rows (step 334, last shard 332 rows + 2 padding rows),

@@ -1,5 +1,5 @@
 """CPU, multi-process (gloo): the exact exchange path of distml_amd.group
-(ShardGroup.push_exchange) at world_size 2 and 3.
+(ShardGroup.push_exchange) at world_size 2, 3, 4 and 8.
 
 Each rank pushes key-subset buckets; ShardGroup splits them by owner shard,
 exchanges the slices all-to-all over torch.distributed, and each owner applies
@@ -140,7 +140,9 @@ def _free_port():
     return p
 
 
-@pytest.mark.parametrize("world,vt", [(2, 1), (3, 1), (2, 0), (3, 0)])
+# world 4 and 8 (the driver's node sizes): linearSplit(8) of 97 rows is 7 shards of 13
+# and a short last shard of 6
+@pytest.mark.parametrize("world,vt", [(2, 1), (3, 1), (2, 0), (3, 0), (4, 1), (8, 1), (8, 0)])
 def test_exchange_push_gloo_bit_exact(tmp_path, oracle, world, vt):
     import torch.multiprocessing as mp
     mp.spawn(_worker, args=(world, _free_port(), vt, str(tmp_path)), nprocs=world, join=True)

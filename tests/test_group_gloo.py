@@ -2,7 +2,7 @@
 
 ShardGroup's orchestration (linearSplit shard plan, ordered local pre-reduce,
 reduce-scatter of the partials, owner apply) runs for real over torch.distributed
-with world_size 2 and 3; only the two device ops are replaced by oracle-backed
+with world_size 2, 3, 4 and 8; only the two device ops are replaced by oracle-backed
 CPU stand-ins injected by this test (the product ops are the HIP kernels).
 
 Tolerance: the sharded path sums each element as p0 + (P_0 + P_1 + ...) where
@@ -114,7 +114,9 @@ def _free_port():
     return p
 
 
-@pytest.mark.parametrize("world,vt", [(2, 1), (2, 0), (3, 1)])
+# world 4 and 8 (the driver's node sizes): linearSplit(8) of 101 rows is 7 shards of 13
+# and a short last shard of 10 (padded in the reduce-scatter)
+@pytest.mark.parametrize("world,vt", [(2, 1), (2, 0), (3, 1), (4, 1), (8, 1), (8, 0)])
 def test_sharded_full_range_push_gloo(tmp_path, oracle, world, vt):
     import torch.multiprocessing as mp
     mp.spawn(_worker, args=(world, _free_port(), vt, str(tmp_path)), nprocs=world, join=True)
