@@ -73,10 +73,12 @@ SIGNATURES = {
     "dml_store_kernel_time": (C.c_int, [_vp, _P(C.c_double), _P(_i64), _i32]),
     "dml_store_kernel_name": (C.c_int, [_vp, C.c_char_p, _i32]),
     "dml_store_apply_dense_device": (C.c_int, [_vp, _vp, _i64]),
+    "dml_store_apply_adagrad_moments_device": (C.c_int, [_vp, _vp, _i64]),
     "dml_reduce_buckets_dense": (C.c_int, [_P(dml_desc), _i64, _i64, _i32, _P(_vp), _P(_i64), _i32, _vp, _vp]),
     "dml_prereduce_begin": (C.c_int, [_P(dml_desc), _i64, _i64, _i32, _P(_vp), _P(_i64), _i32, _vp, _P(_vp)]),
     "dml_prereduce_piece": (C.c_int, [_vp, _i64, _i64, _i64, _i64, _vp, _vp]),
     "dml_prereduce_end": (C.c_int, [_vp]),
+    "dml_prereduce_moments_piece": (C.c_int, [_vp, _i64, _i64, _i64, _i64, _vp, _vp]),
     "dml_prereduce_stream_wait": (C.c_int, [_vp, _vp]),
     "dml_prereduce_timing": (C.c_int, [_i32]),
     "dml_prereduce_kernel_time": (C.c_int, [_P(C.c_double), _P(_i64), _i32]),
@@ -88,6 +90,7 @@ SIGNATURES = {
     "dml_shard_split": (C.c_int, [_P(dml_desc), _i32, _i64, _i32, _P(_vp), _P(_i64), _i32, _vp, _i64, _P(_i64), _vp]),
     "dml_group_unique_id": (C.c_int, [_vp, _i32]),
     "dml_group_push_exchange": (C.c_int, [_vp, _P(_vp), _P(_i64), _i32]),
+    "dml_group_push_moments": (C.c_int, [_vp, _P(_vp), _P(_i64), _i32]),
     "dml_group_create": (C.c_int, [_vp, _i32, _i32, _i32, _P(dml_desc), _i64, _i32, _i32, _P(_vp)]),
     "dml_group_store": (C.c_int, [_vp, _P(_vp)]),
     "dml_group_prereduce_stats": (C.c_int, [_vp, _P(dml_store_counters), _i32]),

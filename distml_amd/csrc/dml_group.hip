@@ -95,6 +95,14 @@ struct dml_group {
     int xheld_set = 0;
     std::vector<const void*> xptrs;
     std::vector<int64_t> xlens;
+    // two-moment AdaGrad path (dml_group_push_moments), two buffer sets by call:
+    // [rank][row][Σu | Σu²] partials and the shard's received moments
+    void* mpart[2] = {nullptr, nullptr};
+    void* mrecv[2] = {nullptr, nullptr};
+    hipEvent_t mrs_done[2] = {nullptr, nullptr};
+    hipEvent_t mapplied[2] = {nullptr, nullptr};
+    std::deque<dml_prereduce*> mpending;  // calls whose index errors are not yet collected
+    int mk = 0;
 };
 
 namespace {
@@ -134,11 +142,29 @@ int end_pending(dml_group* g, size_t keep) {
     return rc;
 }
 
+int end_moments(dml_group* g, size_t keep) {
+    int rc = DML_OK;
+    while (g->mpending.size() > keep) {
+        dml_prereduce* p = g->mpending.front();
+        g->mpending.pop_front();
+        const int r = dml_prereduce_end(p);
+        if (rc == DML_OK) rc = r;
+    }
+    return rc;
+}
+
 void group_free(dml_group* g) {
     if (!g) return;
     (void)hipSetDevice(g->device);
     (void)end_pending(g, 0);
+    (void)end_moments(g, 0);
     if (g->pctx) dml_prectx_destroy(g->pctx);
+    for (int i = 0; i < 2; ++i) {
+        if (g->mpart[i]) (void)hipFree(g->mpart[i]);
+        if (g->mrecv[i]) (void)hipFree(g->mrecv[i]);
+        if (g->mrs_done[i]) (void)hipEventDestroy(g->mrs_done[i]);
+        if (g->mapplied[i]) (void)hipEventDestroy(g->mapplied[i]);
+    }
     if (g->xcnt) (void)hipFree(g->xcnt);
     for (int i = 0; i < 2; ++i) {
         if (g->xsend[i]) (void)hipFree(g->xsend[i]);
@@ -424,6 +450,51 @@ int dml_group_push_exchange(dml_group* g, const void* const* dev_bufs, const int
     return DML_OK;
 }
 
+int dml_group_push_moments(dml_group* g, const void* const* dev_bufs, const int64_t* lens, int32_t n) {
+    if (!g || n < 0 || n > kMaxW || (n > 0 && (!dev_bufs || !lens)))
+        return set_error(DML_E_INVALID_ARG, "bad push arguments (n must be <= 64)");
+    if (!g->desc.ada_grad || g->desc.value_type != DML_ELEMENT_TYPE_FLOAT)
+        return set_error(DML_E_UNSUPPORTED, "the two-moment path is for AdaGrad (float) matrices");
+    GHIP(hipSetDevice(g->device));
+    if (g->xheld) {  // earlier calls' slices first: the store applies calls in order
+        GHIP(hipStreamSynchronize(g->rstream));
+        GRC(hand_over(g));
+    }
+    GRC(end_pending(g, 0));
+    const int64_t S = g->step_rows, W = g->world, C = g->cols;
+    if (!g->mpart[0]) {
+        for (int i = 0; i < 2; ++i) {
+            GHIP(hipMalloc(&g->mpart[i], (size_t)(W * S * 2 * C) * sizeof(float)));
+            GHIP(hipMalloc(&g->mrecv[i], (size_t)(S * 2 * C) * sizeof(float)));
+            GHIP(hipEventCreateWithFlags(&g->mrs_done[i], hipEventDisableTiming));
+            GHIP(hipEventCreateWithFlags(&g->mapplied[i], hipEventDisableTiming));
+        }
+    }
+    const int k = g->mk;
+    g->mk ^= 1;
+    dml_prereduce* h = nullptr;
+    GRC(dml_prereduce_begin(&g->desc, 0, g->total_rows, g->cols, dev_bufs, lens, n, g->istream, &h));
+    // buffer set k was used two calls ago: its apply (behind its reduce-scatter) is done
+    int rc = hipEventSynchronize(g->mapplied[k]) == hipSuccess ? DML_OK : set_error(DML_E_HIP, "applied wait");
+    if (rc == DML_OK) rc = dml_prereduce_moments_piece(h, S, S, 0, W * S, g->mpart[k], g->cstream);
+    if (rc == DML_OK) rc = dml_prereduce_stream_wait(h, g->rstream);
+    if (rc == DML_OK) {
+        const ncclResult_t r = ncclReduceScatter(g->mpart[k], g->mrecv[k], (size_t)(S * 2 * C), ncclFloat32, ncclSum,
+                                                 g->comm, g->rstream);
+        if (r != ncclSuccess) rc = set_error(DML_E_HIP, std::string("ncclReduceScatter: ") + ncclGetErrorString(r));
+    }
+    if (rc != DML_OK) {
+        (void)dml_prereduce_end(h);
+        return rc;
+    }
+    GHIP(hipEventRecord(g->mrs_done[k], g->rstream));
+    GHIP(hipStreamWaitEvent(g->sstream, g->mrs_done[k], 0));
+    GRC(dml_store_apply_adagrad_moments_device(g->store, g->mrecv[k], g->shard_rows));
+    GHIP(hipEventRecord(g->mapplied[k], g->sstream));
+    g->mpending.push_back(h);
+    return end_moments(g, 1);  // the previous call's errors
+}
+
 int dml_group_flush(dml_group* g) {
     if (!g) return set_error(DML_E_INVALID_ARG, "null group");
     GHIP(hipSetDevice(g->device));
@@ -434,6 +505,8 @@ int dml_group_flush(dml_group* g) {
     }
     const int r1 = end_pending(g, 0);
     if (rc == DML_OK) rc = r1;
+    const int rm = end_moments(g, 0);
+    if (rc == DML_OK) rc = rm;
     for (hipStream_t s : {g->cstream, g->rstream})
         if (hipStreamSynchronize(s) != hipSuccess && rc == DML_OK) rc = set_error(DML_E_HIP, "group stream sync");
     for (hipEvent_t e : g->applied)

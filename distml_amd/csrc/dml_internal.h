@@ -267,6 +267,16 @@ hipError_t sparse_replay(int vtype, void* shard, const SpPlan& pl, const SpLayou
                          int64_t stride, int K, int64_t first, int64_t rows, Ctrl* ctrl, uint64_t tail_cut,
                          hipStream_t st);
 
+// Two-moment AdaGrad (sharded path): per-rank [row][Σu | Σu²]
+// pre-reduce pieces (flat shapes: cols % 4 == 0, rows under 4 KiB), and the owner
+// apply of the reduce-scattered moments (+ maxDelta finalize; ada.cand holds
+// kMomentBlocks entries).
+constexpr int kMomentBlocks = 2048;
+hipError_t launch_moments(int64_t ntask, int32_t cols, const Batch& bt, int nb, int64_t stride, int K, int32_t* slot,
+                          const Ctrl* ctrl, RowMap rm, hipStream_t st, LaunchEv ev);
+hipError_t launch_ada_moments(float* shard, const float* src, int64_t rows, int32_t cols, const AdaArgs& ada,
+                              MaxDelta* md, int64_t first, hipStream_t st, LaunchEv ev);
+
 hipError_t launch_stream(bool copy, void* dst, const void* src, int64_t n16, hipStream_t st, LaunchEv ev);
 hipError_t launch_rand(int vtype, void* p, int64_t rows, int32_t cols, uint64_t s0, hipStream_t st);
 hipError_t launch_synth_fill(int vtype, void* p, int64_t n, uint64_t s0, hipStream_t st);

@@ -593,7 +593,9 @@ __global__ __launch_bounds__(64 * WPB) void k_reduce_rows(T* __restrict__ shard,
                     if (e < nv[c]) rowp[r][c0[c] + e] = T(0);
             continue;
         }
-        if (rowflag && rowflag[row[r]]) continue;  // a push repeats this row: the host replays it exactly
+        // a push repeats this row: the host replays it exactly (a keeping chunk's index
+        // flags nothing: no dependent flag load ahead of the row loads)
+        if (rowflag && !bt.keeps && rowflag[row[r]]) continue;
         live |= 1u << r;
         if (!fb) fb = (const uint8_t*)rowp[r];
     }
@@ -984,13 +986,18 @@ __global__ __launch_bounds__(256) void k_reduce_flat(T* __restrict__ shard, int6
     const int64_t lrow = model_row(t0 + lane);
     const bool lchk = lane < nrow && !(rm.block && lrow >= rm.rows_total);  // padding rows have no record
     const int64_t vrows = rm.block ? rm.rows_total : rows;
+    // bit rl of padm / flg: task row t0 + rl is padding of a short last shard / a row a
+    // push repeats (one flag load per row; a keeping chunk's index flags nothing)
+    const uint32_t padm = (uint32_t)__ballot(lane < nrow && rm.block && lrow >= rm.rows_total);
+    const uint32_t flg =
+        (rowflag && !bt.keeps) ? (uint32_t)__ballot(lane < nrow && !((padm >> lane) & 1u) && rowflag[lrow] != 0u) : 0u;
     // the wave's slot rows into LDS (rows a push repeats, and padding rows, stay -1;
     // the table is handed back clean for the next batch's index)
     for (int e = lane; e < nrow * nb; e += 64) {
         const int rl = e / nb, b = e - rl * nb;
         const int64_t mr = model_row(t0 + rl);
         int32_t v = -1;
-        if (!(rm.block && mr >= rm.rows_total) && !(rowflag && rowflag[mr])) {
+        if (!(((padm | flg) >> rl) & 1u)) {
             if (ctrl_identity(ctrl, ident, b)) {  // identity push: record = row
                 v = mr < bt.nrec[b] ? (int32_t)mr : -1;
             } else {
@@ -1019,8 +1026,8 @@ __global__ __launch_bounds__(256) void k_reduce_flat(T* __restrict__ shard, int6
         const int cvj = v < nvec ? v - rlj * NV : 0;
         rc[j] = (rlj << 16) | cvj;
         const int64_t mr = model_row(t0 + rlj);
-        const bool pad = rm.block && mr >= rm.rows_total;
-        const bool flagged = !pad && rowflag && rowflag[mr];
+        const bool pad = (padm >> rlj) & 1u;
+        const bool flagged = (flg >> rlj) & 1u;
         const bool o = v < nvec && !pad && !flagged;
         on |= (o ? 1u : 0u) << j;
         wr |= ((v < nvec && (MODE == kPreReduce ? !flagged : o)) ? 1u : 0u) << j;
@@ -1138,25 +1145,37 @@ __global__ __launch_bounds__(256) void k_ada_flat(float* __restrict__ shard, int
         int32_t* const ls = s_slot[wid];
         // identity pushes checked record by record before the launch (Batch::ident_ok)
         const uint64_t ident = bt.ident_ok ? ctrl->ident : 0ull;
-        // the wave's slot rows into LDS, handed back clean (-1) for the next batch;
-        // rows a push repeats stay -1 here (the host replays them exactly)
-        for (int e = lane; e < nrow * nb; e += 64) {
-            const int rl = e / nb, b = e - rl * nb;
-            const int64_t r = t0 + rl;
-            int32_t v = -1;
-            if (!(rowflag && rowflag[r])) {
-                if ((ident >> b) & 1ull) {
-                    v = r < bt.nrec[b] ? (int32_t)r : -1;  // record = row; the index skipped it
-                } else {
-                    v = slot[r * ss + b];
-                    slot[r * ss + b] = -1;
+        const uint64_t nbm = nb >= 64 ? ~0ull : (1ull << nb) - 1ull;
+        // Every push identity (the 4a leg's ascending full-range pushes): the key index
+        // ran for none of them, so no row is flagged and record r holds row r. No slot
+        // rows, no flag reads: the data, delta and record loads issue at once instead
+        // of behind two dependent DRAM round trips.
+        const bool all_id = (ident & nbm) == nbm;  // wave-uniform
+        uint32_t flg = 0;                          // bit rl: row t0 + rl is flagged (the host replays it)
+        if (!all_id) {
+            // the rows' flags, one load per row, and the wave's slot rows into LDS,
+            // handed back clean (-1) for the next batch; flagged rows stay -1 there
+            if (rowflag) flg = (uint32_t)__ballot(lane < nrow && rowflag[t0 + lane] != 0u);
+            for (int e = lane; e < nrow * nb; e += 64) {
+                const int rl = e / nb, b = e - rl * nb;
+                const int64_t r = t0 + rl;
+                int32_t v = -1;
+                if (!((flg >> rl) & 1u)) {
+                    if ((ident >> b) & 1ull) {
+                        v = r < bt.nrec[b] ? (int32_t)r : -1;  // record = row; the index skipped it
+                    } else {
+                        v = slot[r * ss + b];
+                        slot[r * ss + b] = -1;
+                    }
                 }
+                ls[rl * kMaxW + b] = v;
             }
-            ls[rl * kMaxW + b] = v;
+            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+            __builtin_amdgcn_wave_barrier();
+            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
         }
-        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-        __builtin_amdgcn_wave_barrier();
-        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+        // record of push b for the row of this lane's vector j
+        auto rec_of = [&](int rl, int b) -> int32_t { return all_id ? (int32_t)(t0 + rl) : ls[rl * kMaxW + b]; };
 
         int rc[JMAX];  // (row << 16 | vector within the row)
         uint32_t on = 0, tch = 0;
@@ -1170,7 +1189,7 @@ __global__ __launch_bounds__(256) void k_ada_flat(float* __restrict__ shard, int
             const int cvj = v < nvec ? v - rlj * NV : 0;
             rc[j] = (rlj << 16) | cvj;
             const int64_t ei = (t0 + rlj) * (int64_t)cols + cvj * VEC;
-            const bool o = v < nvec && !(rowflag && rowflag[t0 + rlj]);
+            const bool o = v < nvec && !((flg >> rlj) & 1u);
             on |= (o ? 1u : 0u) << j;
             if (o) {
                 unpack<float>(ldg16_nt((const uint8_t*)(shard + ei)), acc[j]);
@@ -1208,7 +1227,7 @@ __global__ __launch_bounds__(256) void k_ada_flat(float* __restrict__ shard, int
                 for (int b = 0; b < nb; ++b) {
                     const int gb = bt.bidx[b];
                     if (gb > cut_b) break;
-                    const int32_t rr = ls[(rc[j] >> 16) * kMaxW + b];
+                    const int32_t rr = rec_of(rc[j] >> 16, b);
                     if (rr < 0) continue;
 #pragma unroll
                     for (int e = 0; e < VEC; ++e) {
@@ -1233,7 +1252,7 @@ __global__ __launch_bounds__(256) void k_ada_flat(float* __restrict__ shard, int
                     const uint8_t* const bp = bt.base[b];
 #pragma unroll
                     for (int j = 0; j < JMAX; ++j) {
-                        rr[q][j] = (b0 + q < nb && (on >> j & 1u)) ? ls[(rc[j] >> 16) * kMaxW + b] : -1;
+                        rr[q][j] = (b0 + q < nb && (on >> j & 1u)) ? rec_of(rc[j] >> 16, b) : -1;
                         const uint8_t* src =
                             bp + (int64_t)(rr[q][j] >= 0 ? rr[q][j] : 0) * stride + K + (int64_t)(rc[j] & 0xFFFF) * 16;
                         raw[q][j] = rr[q][j] >= 0 ? ldg16_nt(src) : u32x4{0u, 0u, 0u, 0u};
@@ -1280,7 +1299,7 @@ __global__ __launch_bounds__(256) void k_ada_flat(float* __restrict__ shard, int
                 if (!all_a && lg[j][e] > 1.0f) ada.alpha[ei + e] = na[e];
                 if (rb[j][e] >= 0) {
                     const int b = rb[j][e];
-                    const int32_t rr = ls[rl * kMaxW + b];
+                    const int32_t rr = rec_of(rl, b);
                     const uint64_t p = pos_of((uint64_t)bt.bidx[b],
                                               (uint64_t)((int64_t)rr * stride + K + (int64_t)(cv * VEC + e) * 4));
                     if (!cand_ok || rv[j][e] > cand_v || (rv[j][e] == cand_v && p < cand_p)) {
@@ -2125,6 +2144,219 @@ hipError_t launch_key_rows(const uint8_t* base, int64_t nrec, int64_t stride, in
                            int32_t* out, hipStream_t st) {
     if (nrec <= 0) return hipSuccess;
     hipLaunchKernelGGL(k_key_rows, dim3(grid_for(nrec)), dim3(256), 0, st, base, nrec, stride, K, first, rows, out);
+    return hipGetLastError();
+}
+
+// ---------------------------------------------------------------------------
+// Two-moment AdaGrad reduce-scatter: the sharded
+// AdaGrad path whose xGMI bytes do not grow with the pushes per rank. Each rank
+// pre-reduces its full-range pushes into Σu and Σu·u per element (fp32, push
+// order; u·u rounded, then added, like the reference's delta update,
+// FloatMatrixStoreAdaGrad.java:265-267), written as one [row][2 x cols] run so a
+// rank's share of both is one contiguous reduce-scatter chunk; the owner applies
+// row += Σu, delta += Σu², and alpha = f(final delta) where it ends above 1
+// (:268-272: delta never falls, so the last push that sets alpha sees the final
+// delta). The summation order is not the reference's: within 1e-6, not bit-exact.
+//
+// k_moments_flat: k_reduce_flat's layout (R rows per wave as one flat run of
+// 16-B vectors), slot rows in LDS unless every push is identity (Batch::ident_ok).
+// A call whose index met a key outside the matrix or a repeated row writes zeros
+// (dml_prereduce_end reports the error; nothing of it is applied).
+template <int JMAX>
+__global__ __launch_bounds__(256) void k_moments_flat(int64_t ntask, int32_t cols, int32_t R, const Batch bt, int nb,
+                                                      int64_t stride, int K, int32_t* __restrict__ slot,
+                                                      const Ctrl* __restrict__ ctrl, RowMap rm) {
+    constexpr int VEC = 4;
+    constexpr int RMAX = 16;
+    __shared__ int32_t s_slot[4][RMAX * kMaxW];
+    const int lane = threadIdx.x & 63;
+    const int wid = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    const int64_t t0 = ((int64_t)blockIdx.x * 4 + wid) * R;  // first task row of the wave
+    if (t0 >= ntask) return;
+    const int NV = cols / VEC;
+    const int nrow = (int)(ntask - t0 < (int64_t)R ? ntask - t0 : (int64_t)R);
+    const int ss = slot_stride(nb);
+    int32_t* const ls = s_slot[wid];
+    const uint64_t ident = bt.ident_ok ? ctrl->ident : 0ull;
+    const uint64_t nbm = nb >= 64 ? ~0ull : (1ull << nb) - 1ull;
+    const bool all_id = (ident & nbm) == nbm;
+    const bool err = ctrl->cutoff != kNoPos || ctrl->no_dup == 0u;
+    const int64_t lrow = rm.row(t0 + lane);
+    const uint32_t padm = (uint32_t)__ballot(lane < nrow && lrow >= rm.rows_total);
+    if (!all_id) {
+        // slot rows into LDS, handed back clean (-1) like k_reduce_flat's
+        for (int e = lane; e < nrow * nb; e += 64) {
+            const int rl = e / nb, b = e - rl * nb;
+            const int64_t mr = rm.row(t0 + rl);
+            int32_t v = -1;
+            if (!((padm >> rl) & 1u)) {
+                if ((ident >> b) & 1ull) {
+                    v = mr < bt.nrec[b] ? (int32_t)mr : -1;
+                } else {
+                    v = slot[mr * ss + b];
+                    slot[mr * ss + b] = -1;
+                }
+            }
+            ls[rl * kMaxW + b] = v;
+        }
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+        __builtin_amdgcn_wave_barrier();
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    }
+    int rc[JMAX];
+    uint32_t on = 0;
+    float acc[JMAX][VEC], sq[JMAX][VEC];
+    const int nvec = nrow * NV;
+#pragma unroll
+    for (int j = 0; j < JMAX; ++j) {
+        const int v = j * 64 + lane;
+        const int rlj = v < nvec ? v / NV : 0;
+        const int cvj = v < nvec ? v - rlj * NV : 0;
+        rc[j] = (rlj << 16) | cvj;
+        on |= ((v < nvec && !((padm >> rlj) & 1u) && !err) ? 1u : 0u) << j;
+#pragma unroll
+        for (int e = 0; e < VEC; ++e) acc[j][e] = sq[j][e] = 0.f;
+    }
+#pragma unroll 1
+    for (int b = 0; b < nb; ++b) {
+        const uint8_t* const bp = bt.base[b];
+        int32_t rr[JMAX];
+        u32x4 raw[JMAX];
+#pragma unroll
+        for (int j = 0; j < JMAX; ++j) {
+            const int rl = rc[j] >> 16;
+            rr[j] = (on >> j & 1u) ? (all_id ? (int32_t)rm.row(t0 + rl) : ls[rl * kMaxW + b]) : -1;
+            raw[j] = rr[j] >= 0 ? ldg16_nt(bp + (int64_t)rr[j] * stride + K + (int64_t)(rc[j] & 0xFFFF) * 16)
+                                : u32x4{0u, 0u, 0u, 0u};
+        }
+#pragma unroll
+        for (int j = 0; j < JMAX; ++j) {
+            if (rr[j] < 0) continue;
+            float u[VEC];
+            unpack<float>(raw[j], u);
+#pragma unroll
+            for (int e = 0; e < VEC; ++e) {
+                acc[j][e] = __fadd_rn(acc[j][e], u[e]);
+                sq[j][e] = __fadd_rn(sq[j][e], __fmul_rn(u[e], u[e]));
+            }
+        }
+    }
+    float* const out = (float*)rm.out;
+#pragma unroll
+    for (int j = 0; j < JMAX; ++j) {
+        if (j * 64 + lane >= nvec) continue;
+        float* const op = out + (t0 + (rc[j] >> 16)) * (int64_t)(2 * cols) + (rc[j] & 0xFFFF) * VEC;
+        stg16(op, pack<float>(acc[j]));
+        stg16(op + cols, pack<float>(sq[j]));
+    }
+}
+
+hipError_t launch_moments(int64_t ntask, int32_t cols, const Batch& bt, int nb, int64_t stride, int K, int32_t* slot,
+                          const Ctrl* ctrl, RowMap rm, hipStream_t st, LaunchEv ev) {
+    constexpr int JMAX = 8;
+    if (cols % 4 || cols * 4 >= 4096 || !rm.out) return hipErrorInvalidValue;  // the flat shapes
+    const int NV = cols / 4;
+    const int R = std::max(1, std::min(16, JMAX * 64 / NV));
+    const int64_t nblocks = ((ntask + R - 1) / R + 3) / 4;
+    if (nblocks <= 0) return hipSuccess;
+    g_kernel_name = "dml::k_moments_flat<8>";
+    if (ev.start || ev.stop)
+        hipExtLaunchKernelGGL((k_moments_flat<JMAX>), dim3((unsigned)nblocks), dim3(256), 0, st, ev.start, ev.stop, 0,
+                              ntask, cols, R, bt, nb, stride, K, slot, ctrl, rm);
+    else
+        hipLaunchKernelGGL((k_moments_flat<JMAX>), dim3((unsigned)nblocks), dim3(256), 0, st, ntask, cols, R, bt, nb,
+                           stride, K, slot, ctrl, rm);
+    return hipGetLastError();
+}
+
+// Owner apply of the reduce-scattered moments ([row][Σu | Σu²], rows x 2 cols):
+// data += Σu, delta += Σu², alpha = f(delta) where delta ends above 1, each
+// element's strict rise of delta its maxDelta candidate (ties: first in row-major
+// order). One candidate per block into ada.cand.
+__global__ __launch_bounds__(256) void k_ada_moments(float* __restrict__ shard, const float* __restrict__ src,
+                                                     int64_t rows, int32_t cols, AdaArgs ada) {
+    const int NV = cols / 4;
+    const int64_t nvec = rows * NV;
+    float cand_v = 0.f;
+    uint64_t cand_p = kNoPos;
+    bool cand_ok = false;
+    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < nvec; i += (int64_t)gridDim.x * blockDim.x) {
+        const int64_t r = i / NV;
+        const int cv = (int)(i - r * NV);
+        const int64_t ei = r * cols + cv * 4;
+        const float* sp = src + r * (int64_t)(2 * cols) + cv * 4;
+        float a[4], d[4], su[4], s2[4];
+        unpack<float>(ldg16_nt((const uint8_t*)(shard + ei)), a);
+        unpack<float>(ldg16_nt((const uint8_t*)(ada.delta + ei)), d);
+        unpack<float>(ldg16((const uint8_t*)sp), su);
+        unpack<float>(ldg16((const uint8_t*)(sp + cols)), s2);
+        float na[4];
+        bool all_a = true;
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+            a[e] = __fadd_rn(a[e], su[e]);
+            const float nd = __fadd_rn(d[e], s2[e]);
+            if (nd > d[e] && (!cand_ok || nd > cand_v)) {  // elements visited in row-major order per thread
+                cand_ok = true;
+                cand_v = nd;
+                cand_p = (uint64_t)(ei + e);
+            }
+            d[e] = nd;
+            na[e] = 0.f;
+            if (nd > 1.0f) {
+                na[e] = (float)((double)ada.initial_alpha / ((double)ada.factor * sqrt((double)nd)));
+                if (na[e] < ada.min_alpha) na[e] = ada.min_alpha;
+            } else {
+                all_a = false;
+            }
+        }
+        stg16_nt(shard + ei, pack<float>(a));
+        stg16_nt(ada.delta + ei, pack<float>(d));
+        if (all_a) {
+            stg16_nt(ada.alpha + ei, pack<float>(na));
+        } else {
+#pragma unroll
+            for (int e = 0; e < 4; ++e)
+                if (d[e] > 1.0f) ada.alpha[ei + e] = na[e];
+        }
+    }
+    cand_block_best<4>(cand_ok, cand_v, cand_p);
+    if (threadIdx.x == 0) {
+        DeltaCand c;
+        c.value = cand_v;
+        c.valid = cand_ok;
+        c.pos = cand_p;
+        ada.cand[blockIdx.x] = c;
+    }
+}
+
+// maxDelta finalize for element-index candidates (k_ada_moments): the reference's
+// strict `>` against the running maximum; row = the element's key (first + row).
+__global__ __launch_bounds__(256) void k_maxdelta_elems(const DeltaCand* __restrict__ cand, int64_t n,
+                                                        MaxDelta* __restrict__ md, int64_t first, int32_t cols) {
+    bool ok = false;
+    float v = 0.f;
+    uint64_t p = kNoPos;
+    cand_scan(cand, threadIdx.x, n, 256, ok, v, p);
+    cand_block_best<4>(ok, v, p);
+    if (threadIdx.x != 0) return;
+    if (ok && v > md->value) {
+        md->value = v;
+        md->row = (int32_t)(first + (int64_t)(p / (uint64_t)cols));
+        md->col = (int32_t)(p % (uint64_t)cols);
+    }
+}
+
+hipError_t launch_ada_moments(float* shard, const float* src, int64_t rows, int32_t cols, const AdaArgs& ada,
+                              MaxDelta* md, int64_t first, hipStream_t st, LaunchEv ev) {
+    if (cols % 4 || rows <= 0) return hipErrorInvalidValue;
+    g_kernel_name = "dml::k_ada_moments";
+    if (ev.start || ev.stop)
+        hipExtLaunchKernelGGL(k_ada_moments, dim3(kMomentBlocks), dim3(256), 0, st, ev.start, ev.stop, 0, shard, src,
+                              rows, cols, ada);
+    else
+        hipLaunchKernelGGL(k_ada_moments, dim3(kMomentBlocks), dim3(256), 0, st, shard, src, rows, cols, ada);
+    hipLaunchKernelGGL(k_maxdelta_elems, dim3(1), dim3(256), 0, st, ada.cand, (int64_t)kMomentBlocks, md, first, cols);
     return hipGetLastError();
 }
 

@@ -1515,6 +1515,31 @@ int dml_store_apply_dense_device(dml_store* s, const void* dev_src, int64_t elem
     return DML_OK;
 }
 
+int dml_store_apply_adagrad_moments_device(dml_store* s, const void* dev_src, int64_t rows) {
+    if (int rc = check_store(s)) return rc;
+    std::lock_guard<std::mutex> lk(s->mu);
+    DeviceGuard g(s->device);
+    if (!s->adagrad) return set_err(DML_E_UNSUPPORTED, "not an AdaGrad store");
+    if (!dev_src || rows != s->rows) return set_err(DML_E_INVALID_ARG, "moments size mismatch");
+    if (s->cols % 4) return set_err(DML_E_UNSUPPORTED, "two-moment apply: rows of whole 16-B vectors");
+    if (int rc = retire_all(s)) return rc;
+    if (s->err) return set_err(s->err, "store is in a failed state (see dml_store_error_state)");
+    if (s->cand_n < kMomentBlocks) {  // one candidate per apply block
+        HIPCHK(hipStreamSynchronize(s->stream));
+        HIPCHK(hipFree(s->cand));
+        s->cand = nullptr;
+        HIPCHK(hipMalloc((void**)&s->cand, sizeof(DeltaCand) * (size_t)(kMomentBlocks + kMdParts)));
+        s->cand_n = kMomentBlocks;
+    }
+    std::pair<hipEvent_t, hipEvent_t> ev{};
+    if (s->timing) ev = ev_pair(s);
+    HIPCHK(launch_ada_moments((float*)s->data, (const float*)dev_src, s->rows, s->cols, ada_args(s), s->md, s->first,
+                              s->stream, LaunchEv{ev.first, ev.second}));
+    if (s->timing) s->ev_used.push_back(ev);
+    s->kname = g_kernel_name;
+    return DML_OK;
+}
+
 }  // extern "C"
 
 // Per-device pool of pre-reduce workspaces (Ctrl + slot table + rowflags).
@@ -1791,8 +1816,9 @@ int dml_prereduce_begin(const dml_desc* desc, int64_t first_key, int64_t rows, i
                         const int64_t* lens, int32_t n, void* stream, dml_prereduce** out) {
     if (!desc || !out || rows <= 0 || cols <= 0 || n < 0 || n > kMaxW || (n > 0 && (!dev_bufs || !lens)))
         return set_err(DML_E_INVALID_ARG, "bad pre-reduce arguments (n must be <= 64)");
-    if (desc->data_type != 1 || !desc->dense_column || desc->ada_grad)
-        return set_err(DML_E_UNSUPPORTED, "pre-reduce supports dense-column plain matrices");
+    // AdaGrad matrices: only the two-moment pieces (dml_prereduce_moments_piece)
+    if (desc->data_type != 1 || !desc->dense_column || (desc->ada_grad && desc->value_type != DML_ELEMENT_TYPE_FLOAT))
+        return set_err(DML_E_UNSUPPORTED, "pre-reduce supports dense-column matrices");
     if (desc->value_type != 0 && desc->value_type != 1 && desc->value_type != 3)
         return set_err(DML_E_BAD_DESC, "bad value type");
     auto* p = new (std::nothrow) dml_prereduce();
@@ -1872,9 +1898,39 @@ int dml_prereduce_begin(const dml_desc* desc, int64_t first_key, int64_t rows, i
     return DML_OK;
 }
 
+int dml_prereduce_moments_piece(dml_prereduce* p, int64_t row_block, int64_t row_stride, int64_t row_off,
+                                int64_t ntask_rows, void* dev_out, void* stream) {
+    if (!p || !dev_out || row_block <= 0 || ntask_rows < 0) return set_err(DML_E_INVALID_ARG, "bad piece arguments");
+    if (p->ctx || p->desc.value_type != DML_ELEMENT_TYPE_FLOAT || p->cols % 4 || p->cols * 4 >= 4096)
+        return set_err(DML_E_UNSUPPORTED, "two-moment pieces: f32 rows of whole 16-B vectors under 4 KiB");
+    hipStream_t st = (hipStream_t)stream;
+    if (st != p->stream && !p->idx_waited) {
+        HIPCHK(hipEventSynchronize(p->idx_ev));
+        p->idx_waited = true;
+    }
+    RowMap rm;
+    rm.block = row_block;
+    rm.stride = row_stride;
+    rm.off = row_off;
+    rm.rows_total = p->rows;
+    rm.out = dev_out;
+    if (!p->last_ev) HIPCHK(hipEventCreateWithFlags(&p->last_ev, hipEventDisableTiming));
+    HIPCHK(launch_moments(ntask_rows, p->cols, p->bt, p->nb, p->stride, p->K, p->slot, p->ctrl, rm, st,
+                          LaunchEv{nullptr, p->last_ev}));
+    p->done_ev = p->last_ev;
+    for (int64_t t0 = 0; t0 < ntask_rows; t0 += row_block) {
+        const int64_t lo = (t0 / row_block) * row_stride + row_off;
+        const int64_t hi = std::min(lo + std::min(row_block, ntask_rows - t0), p->rows);
+        if (hi > lo) p->rows_done += hi - lo;
+    }
+    p->last_st = st;
+    return DML_OK;
+}
+
 int dml_prereduce_piece(dml_prereduce* p, int64_t row_block, int64_t row_stride, int64_t row_off, int64_t ntask_rows,
                         void* dev_out, void* stream) {
     if (!p || !dev_out || row_block <= 0 || ntask_rows < 0) return set_err(DML_E_INVALID_ARG, "bad piece arguments");
+    if (p->desc.ada_grad) return set_err(DML_E_UNSUPPORTED, "AdaGrad pre-reduce: dml_prereduce_moments_piece");
     hipStream_t st = (hipStream_t)stream;  // as given: 0 is HIP's null stream
     if (st != p->stream && !p->idx_waited) {
         // pieces on another stream (the index ran on a side stream, overlapping the

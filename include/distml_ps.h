@@ -238,6 +238,14 @@ int dml_store_kernel_name(dml_store* s, char* out, int32_t cap);
 /* Elementwise shard += src for a dense device buffer of rows*cols values in the
  * store's layout (owner-side apply after a reduce-scatter). */
 int dml_store_apply_dense_device(dml_store* s, const void* dev_src, int64_t elems);
+/* Two-moment AdaGrad owner apply: dev_src holds rows x [cols Σu |
+ * cols Σu²] f32 (the reduce-scattered dml_prereduce_moments_piece output of the
+ * shard's rows); data += Σu, delta += Σu², alpha = initialAlpha / (factor *
+ * sqrt(delta)) clamped to minAlpha where delta ends above 1, maxDelta updated
+ * (FloatMatrixStoreAdaGrad.java:262-277 for the summed update; ties of maxDelta
+ * go to the first element in row-major order). Within 1e-6 of the sequential
+ * reference, not bit-exact: the exact path is dml_group_push_exchange. */
+int dml_store_apply_adagrad_moments_device(dml_store* s, const void* dev_src, int64_t rows);
 
 /* Ordered reduce of n device-resident full-range buckets into a dense device
  * buffer `dev_out` (rows*cols values of `value_type`, row = key - first_key):
@@ -263,6 +271,13 @@ int dml_prereduce_begin(const dml_desc* desc, int64_t first_key, int64_t rows, i
 int dml_prereduce_piece(dml_prereduce* p, int64_t row_block, int64_t row_stride, int64_t row_off,
                         int64_t ntask_rows, void* dev_out, void* stream);
 int dml_prereduce_end(dml_prereduce* p);
+/* The two-moment piece of an AdaGrad matrix's pre-reduce (begun with its desc):
+ * task row t's Σu and Σu·u over the pushes, in push order, written as
+ * dev_out + t*2*cols = [cols Σu | cols Σu²] (f32; rows of whole 16-B vectors
+ * under 4 KiB). A call whose index found a key outside the matrix or a repeated
+ * row writes zeros (_end reports the error). */
+int dml_prereduce_moments_piece(dml_prereduce* p, int64_t row_block, int64_t row_stride, int64_t row_off,
+                                int64_t ntask_rows, void* dev_out, void* stream);
 /* Make `stream` wait (device side) for the pieces enqueued so far, e.g. the
  * communication stream that reduce-scatters the piece just written. */
 int dml_prereduce_stream_wait(dml_prereduce* p, void* stream);
@@ -341,6 +356,13 @@ int dml_group_push_full_range(dml_group* g, const void* const* dev_bufs, const i
  * rank calls with the same n (<= 64). The owner's pushes are asynchronous: their
  * errors surface at the next exchange call or at dml_group_flush. */
 int dml_group_push_exchange(dml_group* g, const void* const* dev_bufs, const int64_t* lens, int32_t n);
+/* AdaGrad's sharded path for many pushes per rank: the rank's n
+ * full-range pushes pre-reduced into Σu and Σu² (dml_prereduce_moments_piece),
+ * one ncclReduceScatter of both, the owner's
+ * dml_store_apply_adagrad_moments_device. xGMI bytes per rank: (world-1)/world
+ * x 2 x the model, whatever n is (the exchange path moves n pushes). Within
+ * 1e-6, not bit-exact; errors surface at the next call or the flush. */
+int dml_group_push_moments(dml_group* g, const void* const* dev_bufs, const int64_t* lens, int32_t n);
 int dml_group_flush(dml_group* g);
 void dml_group_destroy(dml_group* g);
 

@@ -37,3 +37,26 @@ def bits_equal(a, b) -> bool:
     a = np.ascontiguousarray(a)
     b = np.ascontiguousarray(b)
     return a.shape == b.shape and a.tobytes() == b.tobytes()
+
+
+def moments_within(got_data, got_alpha, got_delta, o, init, pushes, cols, what):
+    """The two-moment AdaGrad path's bound: data within the
+    summation-order bound of the plain sharded path and 1e-6 of sum|terms| from the
+    exact sum; delta (a sum of squares, no cancellation), alpha = f(delta) and
+    maxDelta within 1e-6 relative of the sequential oracle."""
+    n = len(pushes) + 1
+    terms = np.abs(init.astype(np.float64))
+    exact = init.astype(np.float64)
+    for h in pushes:
+        rec = np.frombuffer(h, np.uint8).reshape(-1, 4 + 4 * cols)
+        k = rec[:, :4].copy().view("<i4").ravel()
+        g = rec[:, 4:].copy().view("<f4").astype(np.float64)
+        np.add.at(terms, k, np.abs(g))
+        np.add.at(exact, k, g)
+    d = got_data.astype(np.float64)
+    assert np.all(np.abs(d - o.data) <= 2 * (n - 1) * 2.0 ** -24 * terms), what
+    assert float(np.max(np.abs(d - exact) / terms)) <= 1e-6, what
+    od, oa = o.delta.astype(np.float64), o.alpha.astype(np.float64)
+    assert float(np.max(np.abs(got_delta - od) / np.maximum(od, 1e-30))) <= 1e-6, what
+    assert float(np.max(np.abs(got_alpha - oa) / np.maximum(np.abs(oa), 1e-30))) <= 1e-6, what
+    assert (od > 1.0).any(), "the alpha update ran"

@@ -154,13 +154,13 @@ XADA = (0.025, 0.0001, 1.5)
 XCALLS = 4
 
 
-def _xbuckets(vt, rank, call=0):
+def _xbuckets(vt, rank, call=0, repeat=True):
     from distml_amd import encode_matrix_push
     out = []
     for b in range(XW):
         rng = np.random.default_rng(500 * rank + 50 * call + b)
         keys = rng.permutation(XR)[: rng.integers(XR // 4, XR)]
-        if call == 1 and b == 0 and rank == 0:
+        if repeat and call == 1 and b == 0 and rank == 0:
             keys[5] = keys[17]  # one row listed twice (the exact replay)
         vals = ((rng.standard_normal((len(keys), XC)) * 0.6).astype(np.float32) if vt == 1
                 else rng.integers(-2, 3, size=(len(keys), XC)).astype(np.int32))
@@ -236,3 +236,56 @@ def test_exchange_hip_multiprocess(tmp_path, oracle, world, vt):
             k = rec[:, :4].copy().view("<i4").ravel()
             assert so.push(rec[(k >= sh.firstKey) & (k <= sh.lastKey)].tobytes()) == 0
         assert tuple(np.load(tmp_path / f"md{r}.npy").tolist()) == tuple(float(x) for x in so.max_delta())
+
+
+# ---------------------------------------------------------------- two-moment AdaGrad path
+def _mworker(rank, world, port, out_dir):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    sys.path[:0] = [ROOT, os.path.join(ROOT, "oracle")]
+    import torch
+    import torch.distributed as dist
+
+    from distml_amd.datadesc import DataDesc
+    from distml_amd.group import ShardGroup
+
+    torch.cuda.set_device(0)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    fmt = DataDesc(1, 0, 1, False, True, True)
+    g = ShardGroup(fmt, XR, XC, rank, world, device=0, exchange_only=True)
+    sh = g.shard
+    g.store.load_values(_init(1, XR, XC)[sh.firstKey:sh.lastKey + 1])
+    g.store.setAlpha(*XADA)
+    keep = []
+    for call in range(XCALLS):
+        bufs = [torch.from_numpy(b).cuda() for b in _xbuckets(1, rank, call, repeat=False)]
+        torch.cuda.synchronize()
+        g.push_moments([b.data_ptr() for b in bufs], [b.numel() for b in bufs])
+        keep.append(bufs)
+    g.flush()
+    np.save(os.path.join(out_dir, f"data{rank}.npy"), g.store.values())
+    a, d = g.store.adagrad_state()
+    np.save(os.path.join(out_dir, f"alpha{rank}.npy"), a)
+    np.save(os.path.join(out_dir, f"delta{rank}.npy"), d)
+    g.store.close()
+    dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world", [2, 3])
+def test_moments_hip_multiprocess(tmp_path, oracle, world):
+    """ShardGroup.push_moments (the two-moment AdaGrad path) with the HIP kernels at
+    world 2-3 (ranks share cuda:0, gloo reduce-scatter), four calls of key-subset
+    pushes: within 1e-6 of one oracle store fed every call's pushes, rank-major."""
+    import torch.multiprocessing as mp
+    import kat
+    mp.spawn(_mworker, args=(world, _free_port(), str(tmp_path)), nprocs=world, join=True)
+    init = _init(1, XR, XC)
+    allb = [b for call in range(XCALLS) for r in range(world) for b in _xbuckets(1, r, call, repeat=False)]
+    o = oracle.OracleStore(1, 0, 1, 0, XR - 1, XC, 1, 1)
+    o.set_alpha(*XADA)
+    o.data[:] = init
+    for b in allb:
+        assert o.push(b.tobytes()) == 0
+    cat = {n: np.concatenate([np.load(tmp_path / f"{n}{r}.npy") for r in range(world)]).reshape(XR, XC)
+           for n in ("data", "alpha", "delta")}
+    kat.moments_within(cat["data"], cat["alpha"].astype(np.float64), cat["delta"].astype(np.float64), o, init,
+                       [b.tobytes() for b in allb], XC, f"world {world}")

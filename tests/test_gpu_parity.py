@@ -785,6 +785,64 @@ def test_sharded_speculation_world1(oracle, binding, vt):
             dist.destroy_process_group()
 
 
+@pytest.mark.parametrize("binding", ["torch", "native"])
+def test_adagrad_moments_world1(oracle, binding):
+    """The two-moment AdaGrad path at world 1 over RCCL: three calls
+    of four pushes (full-range ascending and permuted, and a key subset), no flush
+    between; data, alpha, delta and maxDelta within 1e-6 of the sequential oracle
+    (moments_within); maxDelta's (row, col) holds that value."""
+    import socket
+    import torch.distributed as dist
+    from distml_amd import DataDesc, encode_matrix_push
+    from distml_amd.group import NativeShardGroup, ShardGroup
+    rows, cols, calls, W = 1000, 200, 3, 4
+    ada = (0.025, 0.0001, 1.5)
+    fmt = DataDesc(1, 0, 1, False, True, True)
+    rng = np.random.default_rng(44)
+    host = []
+    for c in range(calls):
+        for b in range(W):
+            keys = (np.arange(rows) if b == 0 else rng.permutation(rows)[: rows if b < 3 else rows // 2])
+            host.append(encode_matrix_push(keys, (rng.standard_normal((len(keys), cols)) * 0.6).astype(np.float32),
+                                           0, 1))
+    dev = [torch.frombuffer(bytearray(h), dtype=torch.uint8).cuda() for h in host]
+    torch.cuda.synchronize()
+    port = None
+    if binding == "torch":
+        s = socket.socket()
+        s.bind(("127.0.0.1", 0))
+        port = s.getsockname()[1]
+        s.close()
+        dist.init_process_group("nccl", init_method=f"tcp://127.0.0.1:{port}", rank=0, world_size=1,
+                                device_id=torch.device("cuda", 0))
+        g = ShardGroup(fmt, rows, cols, 0, 1, device=0, exchange_only=True)
+    else:
+        g = NativeShardGroup(fmt, rows, cols, 0, 1, NativeShardGroup.unique_id(), device=0)
+    try:
+        g.store.setAlpha(*ada)
+        rng2 = np.random.default_rng(3)
+        init = (rng2.standard_normal((rows, cols)) * 0.1).astype(np.float32)
+        g.store.load_values(init)
+        for c in range(calls):
+            sl = dev[c * W:(c + 1) * W]
+            g.push_moments([d.data_ptr() for d in sl], [d.numel() for d in sl])
+        g.flush()
+        a, d = g.store.adagrad_state()
+        o = oracle_store(oracle, fmt, 0, rows - 1, cols)
+        o.set_alpha(*ada)
+        o.data[:] = init
+        for h in host:
+            assert o.push(h) == 0
+        kat.moments_within(g.store.values(), a.astype(np.float64), d.astype(np.float64), o, init, host, cols, binding)
+        mv, mr, mc = g.store.maxDelta()
+        ov = o.max_delta()[0]
+        assert abs(mv - ov) <= 1e-6 * ov and d[mr, mc] == np.float32(mv), (mv, mr, mc, o.max_delta())
+    finally:
+        g.close()
+        if port is not None:
+            dist.destroy_process_group()
+
+
 def test_prereduce_pieces_row_map(oracle):
     """dml_prereduce_{begin,piece,end}: slices laid out [rank][row] for a 3-way
     linearSplit of 1000 rows (step 334, last shard 332 rows + 2 padding rows),
