@@ -371,6 +371,9 @@ def headline(ctx: Ctx, L, args, out_line: dict):
             bs = bufs[:W] if k % 2 == 0 else bufs[W:]
             order = list(range(W))
             rnd.shuffle(order)
+            if args.shuffle_keep_parity:  # diagnostic: ascending pushes stay at even positions
+                ev, od = [j for j in order if j % 2 == 0], [j for j in order if j % 2 == 1]
+                order = [x for pair in zip(ev, od) for x in pair]
             shuffled_batches.append(DeviceBatch([bs[j].data_ptr() for j in order], [bs[j].numel() for j in order]))
         k_step = [0]
         cur = [batches]
@@ -441,6 +444,17 @@ def headline(ctx: Ctx, L, args, out_line: dict):
         shuffled["pushes_per_step"] = {k: round(cs[k] / max(cs["chunks"], 1), 2)
                                        for k in ("identity_pushes", "reused_pushes", "indexed_pushes")}
         shuffled["spec_reruns"] = cs["spec_reruns"]
+        # the in-order steps once more, right after: separates the arrival order's cost
+        # from the box's drift over a sustained run (the headline is measured first)
+        cur[0] = batches
+        k_step[0] = 0
+        el_a = timed_steps(ctx, step, finish, args.steps, min(args.warmup, 50), reset=reset)
+        ka_ms, ka_n = timed_store.kernel_time(reset=True)
+        timed_store.stats(reset=True)
+        if ka_n:
+            shuffled["in_order_again"] = {
+                "ms_per_step": round(el_a / args.steps * 1e3, 4), "avg_kernel_us": round(ka_ms / ka_n * 1e3, 2),
+                "frac": round(algo_per_rank / (ka_ms / ka_n / 1e3) / 1e9 / HBM_PEAK_GBS, 4)}
     timed_store.set_timing(False)
     value = algo_per_rank * world * args.steps / el / 2**30
     out_line.update({
@@ -719,9 +733,14 @@ def leg_config4_ada(ctx: Ctx, L, args) -> dict:
 
     calls = []  # host time of each call (diagnostic: the split's counts and the exchange wait there)
 
+    moments = args.c4a_path == "moments"
+
     def step():
         t = time.perf_counter()
-        group.push_exchange(ptrs, lens)
+        if moments:  # Σu / Σu² pre-reduce, one reduce-scatter, owner apply (within 1e-6)
+            group.push_moments(ptrs, lens)
+        else:        # exact: split, all-to-all, ordered owner apply
+            group.push_exchange(ptrs, lens)
         calls.append(time.perf_counter() - t)
 
     for _ in range(args.c4a_warmup):
@@ -736,8 +755,9 @@ def leg_config4_ada(ctx: Ctx, L, args) -> dict:
     # data and delta and writes alpha only where delta ends above 1, which these
     # gradients (|u| ~ 1e-3 from delta = 0) never reach: 4 state bytes moves per element
     algo = w * rows * rec + 4 * S * cols * 4
+    path = ("two-moment path (Σu, Σu² reduce-scatter; within 1e-6)" if moments else "exact exchange path")
     out = {"workload": f"config4 AdaGrad: FloatMatrixStoreAdaGrad {rows}x{cols} fp32 (data + alpha + delta), {w} "
-                       f"full-range pushes per GPU (rows ascending), exact exchange path",
+                       f"full-range pushes per GPU (rows ascending), {path}",
            "value": round(algo * world * args.c4a_steps / el / 2**30, 2), "unit": "GiB/s", "n_gpus": world,
            "pushes_per_gpu": w, "steps": args.c4a_steps, "ms_per_step": round(el / args.c4a_steps * 1e3, 3),
            "scaling": "weak", "dtype": "f32",
@@ -747,7 +767,9 @@ def leg_config4_ada(ctx: Ctx, L, args) -> dict:
            "host_ms_per_call": [round(x * 1e3, 2) for x in calls[-args.c4a_steps:]]}
     if k_n:
         k_s = k_ms / k_n / 1e3
-        owner = world * w * S * rec + 4 * S * cols * 4  # one owner launch: every rank's slices + data/delta RMW
+        # one owner launch: every rank's slices + data/delta RMW (moments: the received
+        # Σu / Σu² rows instead of the slices)
+        owner = (2 * S * cols * 4 if moments else world * w * S * rec) + 4 * S * cols * 4
         kn = store.kernel_name()
         tr = traffic_for("leg4a", kn) if world == 1 else {"traffic": None, "traffic_stale": "profiled at N = 1 only"}
         out["roofline"] = {"bound": "hbm", "achieved": round(owner / k_s / 1e9, 1), "peak": HBM_PEAK_GBS,
@@ -1016,6 +1038,7 @@ def main():
     ap.add_argument("--no-timing", action="store_true", help="no kernel timing events in the timed region")
     ap.add_argument("--sparse-steps", type=int, default=20, help="config-3 sparse leg steps (0 = skip; N=1 only)")
     ap.add_argument("--pieces", type=int, default=1, help="pre-reduce row slices per call (sharded path)")
+    ap.add_argument("--shuffle-keep-parity", action="store_true", help=argparse.SUPPRESS)
     ap.add_argument("--group", action="store_true",
                     help="use the sharded pre-reduce/reduce-scatter path even at N=1 (path check)")
     ap.add_argument("--legs", default="4,5,4a", help="model-level config legs in the line (4, 5, 4a; '' = none)")
@@ -1026,6 +1049,8 @@ def main():
     ap.add_argument("--c4-warmup", type=int, default=2)
     ap.add_argument("--c4a-pushes", type=int, default=2, help="config-4 AdaGrad full-range pushes per GPU")
     ap.add_argument("--c4a-steps", type=int, default=3)
+    ap.add_argument("--c4a-path", choices=["exchange", "moments"], default="exchange",
+                    help="config-4 AdaGrad leg: the exact exchange path, or the two-moment reduce-scatter")
     ap.add_argument("--c4a-warmup", type=int, default=3, help="(the exchange buffer pool fills in the first calls)")
     ap.add_argument("--c5-steps", type=int, default=20)
     ap.add_argument("--c5-warmup", type=int, default=4)

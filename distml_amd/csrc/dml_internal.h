@@ -183,14 +183,6 @@ constexpr int kMdParts = 256;
 hipError_t launch_maxdelta_finalize(DeltaCand* cand, int64_t n, MaxDelta* md, const Batch& bt, int nb,
                                     int64_t stride, int K, int V, hipStream_t st, int mode = kMdApply,
                                     const Ctrl* ctrl = nullptr);
-hipError_t launch_array_validate(const Batch& bt, int nb, int64_t max_nrec, int64_t stride,
-                                 int K, int64_t first, int64_t rows, Ctrl* ctrl, uint64_t tail_cut, hipStream_t st);
-hipError_t launch_array_apply(int vtype, void* shard, int64_t rows, const uint8_t* base, int64_t nrec,
-                              int b_global, int64_t stride, int K, int64_t first, Ctrl* ctrl,
-                              uint64_t tail_cut, const Ctrl* prev, hipStream_t st, LaunchEv ev = {},
-                              uint32_t* mark = nullptr, uint32_t tok = 0);
-hipError_t launch_array_exact_i32(int32_t* shard, int64_t rows, const Batch& bt, int nb, int64_t stride, int K,
-                                  int64_t first, uint64_t cut, Ctrl* ctrl, hipStream_t st);
 hipError_t launch_array_rollback_i32(int32_t* shard, int64_t rows, const uint8_t* base, int64_t nrec,
                                      int b_global, int64_t stride, int K, int64_t first, Ctrl* ctrl,
                                      uint64_t tail_cut, hipStream_t st);

@@ -10,9 +10,9 @@
 //                   summed over the batch's pushes in push order, one RMW of
 //                   the row (FloatMatrixStore.java:210-222, IntMatrixStore.java:164-178,
 //                   DoubleMatrixStore.java:163-175, FloatMatrixStoreAdaGrad.java:249-284)
-//   k_array_*       ordered sparse scatter-add for the array stores
-//                   (FloatArrayStore.java:110-122, IntArrayStore.java:97-113,
-//                   DoubleArrayStore.java:115-127), one launch per push
+//   k_array_rollback int32 array stores: undo every add after the first negative
+//                   counter (IntArrayStore.java:97-113); the arrays' ordered
+//                   scatter-add itself is the partition + leaf path of dml_sparse.hip
 //   k_fetch, k_bswap, k_fill, k_apply_dense, k_synth_*  — fetch / checkpoint /
 //                   init / owner-apply / synthetic data.
 #include "dml_device.h"
@@ -1665,94 +1665,9 @@ hipError_t launch_maxdelta_finalize(DeltaCand* cand, int64_t n, MaxDelta* md, co
 }
 
 // ---------------------------------------------------------------------------
-// Array stores. Records [key][value] at stride K+VS.
-// Four records per thread, loads issued together (one 8-B key load per record
-// leaves too few bytes in flight to stream the keys at HBM rate).
-constexpr int kValidateUnroll = 4;
-__global__ __launch_bounds__(256) void k_array_validate(const Batch bt, int64_t stride, int K,
-                                                        int64_t first, int64_t rows, Ctrl* __restrict__ ctrl,
-                                                        uint64_t tail_cut) {
-    const int b = blockIdx.y;
-    const int64_t r0 = (int64_t)blockIdx.x * blockDim.x * kValidateUnroll + threadIdx.x;
-    if (r0 == 0 && b == 0 && tail_cut != kNoPos) atomicMin(&ctrl->cutoff, (unsigned long long)tail_cut);
-    const int64_t n = bt.nrec[b];
-    int64_t key[kValidateUnroll];
-#pragma unroll
-    for (int j = 0; j < kValidateUnroll; ++j) {
-        const int64_t r = r0 + j * (int64_t)blockDim.x;
-        key[j] = r < n ? ld_key(bt.base[b] + r * stride, K) : first;
-    }
-#pragma unroll
-    for (int j = 0; j < kValidateUnroll; ++j) {
-        const int64_t r = r0 + j * (int64_t)blockDim.x;
-        if (r < n && row_index(key[j], first, rows) < 0)
-            atomicMin(&ctrl->cutoff, (unsigned long long)pos_of((uint64_t)bt.bidx[b], (uint64_t)(r * stride)));
-    }
-}
-
-hipError_t launch_array_validate(const Batch& bt, int nb, int64_t max_nrec, int64_t stride, int K,
-                                 int64_t first, int64_t rows, Ctrl* ctrl, uint64_t tail_cut, hipStream_t st) {
-    if (nb <= 0) return hipSuccess;
-    const int64_t per_block = 256 * kValidateUnroll;
-    dim3 grid((unsigned)std::max<int64_t>(1, (max_nrec + per_block - 1) / per_block), (unsigned)nb);
-    hipLaunchKernelGGL(k_array_validate, grid, dim3(256), 0, st, bt, stride, K, first, rows, ctrl, tail_cut);
-    return hipGetLastError();
-}
-
-// One thread per record of one push. Keys inside one push are distinct
-// (the writers serialize a HashMap), so each element receives at most one
-// add per launch and the atomics reproduce the sequential sum exactly;
-// pushes are ordered by the stream. int32 (CHECK): the counter's value after
-// the add is exact only when the key is unique in the push, so each record
-// also stamps mark[idx] with the push's token; a record that finds its own
-// push's token there marks the chunk (no_dup = 0) and the host re-runs it in
-// record order (k_array_seq_i32), which also finds the exact first negative.
-template <typename T, bool CHECK>
-__global__ __launch_bounds__(256) void k_array_apply(T* __restrict__ shard, int64_t rows, const uint8_t* __restrict__ base,
-                                                     int64_t nrec, int b_global, int64_t stride, int K,
-                                                     int64_t first, Ctrl* __restrict__ ctrl, uint64_t tail_cut,
-                                                     const Ctrl* __restrict__ prev, uint32_t* __restrict__ mark,
-                                                     uint32_t tok) {
-    const int64_t r = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (r >= nrec) return;
-    if (prev && ctrl_abnormal(prev)) return;
-    uint64_t cut = ctrl->cutoff;
-    if (tail_cut < cut) cut = tail_cut;
-    const int64_t off = r * stride;
-    if (pos_of((uint64_t)b_global, (uint64_t)off) >= cut) return;
-    const int64_t idx = row_index(ld_key(base + off, K), first, rows);
-    if (idx < 0) return;  // unreachable: validated, positions before the cutoff are in range
-    const T u = Elem<T>::load(base + off + K);
-    if constexpr (CHECK) {
-        if (mark && atomicExch(&mark[idx], tok) == tok) atomicAnd(&ctrl->no_dup, 0u);
-        const int32_t old = atomicAdd((int32_t*)&shard[idx], (int32_t)u);
-        if ((int32_t)((uint32_t)old + (uint32_t)u) < 0)
-            atomicMin(&ctrl->neg_pos, (unsigned long long)pos_of((uint64_t)b_global, (uint64_t)(off + K)));
-    } else {
-        atomicAdd(&shard[idx], u);
-    }
-}
-
-hipError_t launch_array_apply(int vtype, void* shard, int64_t rows, const uint8_t* base, int64_t nrec, int b_global,
-                              int64_t stride, int K, int64_t first, Ctrl* ctrl, uint64_t tail_cut, const Ctrl* prev,
-                              hipStream_t st, LaunchEv ev, uint32_t* mark, uint32_t tok) {
-    if (nrec <= 0) return hipSuccess;
-    const dim3 grid((unsigned)((nrec + 255) / 256));
-    if (vtype == kF32)
-        hipExtLaunchKernelGGL((k_array_apply<float, false>), grid, dim3(256), 0, st, ev.start, ev.stop, 0,
-                              (float*)shard, rows, base, nrec, b_global, stride, K, first, ctrl, tail_cut, prev,
-                              nullptr, 0u);
-    else if (vtype == kI32)
-        hipExtLaunchKernelGGL((k_array_apply<int32_t, true>), grid, dim3(256), 0, st, ev.start, ev.stop, 0,
-                              (int32_t*)shard, rows, base, nrec, b_global, stride, K, first, ctrl, tail_cut, prev,
-                              mark, tok);
-    else
-        hipExtLaunchKernelGGL((k_array_apply<double, false>), grid, dim3(256), 0, st, ev.start, ev.stop, 0,
-                              (double*)shard, rows, base, nrec, b_global, stride, K, first, ctrl, tail_cut, prev,
-                              nullptr, 0u);
-    return hipGetLastError();
-}
-
+// Array stores (int32): undo after the first negative counter. Records
+// [key][value] at stride K+VS; the ordered apply itself is the sorted leaf path
+// (dml_sparse.hip).
 // Undo (mod 2^32) every int32 array add positioned after the first negative.
 __global__ __launch_bounds__(256) void k_array_rollback(int32_t* __restrict__ shard, int64_t rows,
                                                         const uint8_t* __restrict__ base, int64_t nrec, int b_global,
@@ -1770,58 +1685,6 @@ __global__ __launch_bounds__(256) void k_array_rollback(int32_t* __restrict__ sh
     const int64_t idx = row_index(ld_key(base + off, K), first, rows);
     if (idx < 0) return;
     atomicSub(&shard[idx], (int32_t)ld32(base + off + K));
-}
-
-// Exact int32 array re-run (a push repeated a key, see k_array_apply): undo
-// every add the chunk's atomics made (positions before `cut`), then apply the
-// pushes in record order on one lane, stopping after the first add that leaves
-// a counter negative (IntArrayStore.java:97-113: the throw follows the add).
-__global__ __launch_bounds__(256) void k_array_undo_i32(int32_t* __restrict__ shard, int64_t rows,
-                                                        const uint8_t* __restrict__ base, int64_t nrec, int b_global,
-                                                        int64_t stride, int K, int64_t first, uint64_t cut) {
-    const int64_t r = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (r >= nrec) return;
-    const int64_t off = r * stride;
-    if (pos_of((uint64_t)b_global, (uint64_t)off) >= cut) return;
-    const int64_t idx = row_index(ld_key(base + off, K), first, rows);
-    if (idx < 0) return;
-    atomicSub(&shard[idx], (int32_t)ld32(base + off + K));
-}
-
-__global__ __launch_bounds__(64) void k_array_seq_i32(int32_t* __restrict__ shard, int64_t rows,
-                                                      const uint8_t* __restrict__ base, int64_t nrec, int b_global,
-                                                      int64_t stride, int K, int64_t first, uint64_t cut,
-                                                      Ctrl* __restrict__ ctrl) {
-    if (threadIdx.x != 0 || ctrl->neg_pos != kNoPos) return;
-    for (int64_t r = 0; r < nrec; ++r) {
-        const int64_t off = r * stride;
-        if (pos_of((uint64_t)b_global, (uint64_t)off) >= cut) return;
-        const int64_t idx = row_index(ld_key(base + off, K), first, rows);
-        if (idx < 0) return;  // unreachable: positions before the cutoff are in range
-        const int32_t v = (int32_t)((uint32_t)shard[idx] + ld32(base + off + K));
-        shard[idx] = v;
-        if (v < 0) {
-            ctrl->neg_pos = pos_of((uint64_t)b_global, (uint64_t)(off + K));
-            return;
-        }
-    }
-}
-
-hipError_t launch_array_exact_i32(int32_t* shard, int64_t rows, const Batch& bt, int nb, int64_t stride, int K,
-                                  int64_t first, uint64_t cut, Ctrl* ctrl, hipStream_t st) {
-    for (int b = 0; b < nb; ++b) {
-        if (bt.nrec[b] <= 0) continue;
-        hipLaunchKernelGGL(k_array_undo_i32, dim3((unsigned)((bt.nrec[b] + 255) / 256)), dim3(256), 0, st, shard,
-                           rows, bt.base[b], bt.nrec[b], bt.bidx[b], stride, K, first, cut);
-    }
-    hipError_t e = hipMemsetAsync(&ctrl->neg_pos, 0xFF, sizeof(ctrl->neg_pos), st);
-    if (e != hipSuccess) return e;
-    for (int b = 0; b < nb; ++b) {
-        if (bt.nrec[b] <= 0) continue;
-        hipLaunchKernelGGL(k_array_seq_i32, dim3(1), dim3(64), 0, st, shard, rows, bt.base[b], bt.nrec[b],
-                           bt.bidx[b], stride, K, first, cut, ctrl);
-    }
-    return hipGetLastError();
 }
 
 hipError_t launch_array_rollback_i32(int32_t* shard, int64_t rows, const uint8_t* base, int64_t nrec, int b_global,

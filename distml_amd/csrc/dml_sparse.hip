@@ -323,6 +323,10 @@ constexpr int kSpLeafThreads = 512;  // 8 waves per leaf
 constexpr int kSpLines = 2 * kSpLeafThreads;
 constexpr int kSpBucketMax = 64;
 
+// int32 leaves (IntArrayStore): the negativity check after every add
+template <typename T>
+constexpr bool kIntLeaf = sizeof(T) == 4 && T(0.5) == T(0);
+
 // A leaf record's fields. Full records: comp = row << 32 | sequence (+ value in
 // val[]); compact records (CMP): row within the level-1 bin << 38 | push << 32 |
 // value bits, ordered within a row by push.
@@ -336,9 +340,12 @@ struct LeafRec {
 };
 
 // A repeated row's records in ascending key (= push / sequence) order, added to x.
+// int32 (IntArrayStore): *neg receives the sequence of the first add that leaves
+// the counter negative (IntArrayStore.java:108-110), if any.
 template <typename T, bool CMP>
 __device__ inline T leaf_chain(T x, uint64_t row, uint64_t row0, int bshift, const uint32_t* bstart,
-                               const uint16_t* perm, const uint64_t* sc, const T* sv, const LeafRec<CMP>& lr) {
+                               const uint16_t* perm, const uint64_t* sc, const T* sv, const LeafRec<CMP>& lr,
+                               uint32_t* neg) {
     const uint32_t b = (uint32_t)((row - row0) >> bshift);
     const uint32_t bs = bstart[b], be = bstart[b + 1];
     bool started = false;
@@ -357,6 +364,8 @@ __device__ inline T leaf_chain(T x, uint64_t row, uint64_t row0, int bshift, con
         if (bj < 0) break;
         if constexpr (CMP) x = Elem<T>::add(x, __uint_as_float((uint32_t)sc[bj]));
         else x = Elem<T>::add(x, sv[bj]);
+        if constexpr (kIntLeaf<T>)
+            if (x < 0 && *neg == kSpSkip) *neg = (uint32_t)best;  // full records: key = row << 32 | sequence
         last = best;
         started = true;
     }
@@ -506,6 +515,7 @@ __global__ __launch_bounds__(kSpLeafThreads) void k_sp_leaf(T* __restrict__ shar
         }
         return;
     }
+    uint32_t neg = kSpSkip;  // int32: sequence of this thread's first add that left a counter negative
 #pragma unroll
     for (int k = 0; k < kPer; ++k) {
         const int i = tid + k * kT;
@@ -516,18 +526,27 @@ __global__ __launch_bounds__(kSpLeafThreads) void k_sp_leaf(T* __restrict__ shar
         T x = x0[k];
         if (!(f & 2)) {
             x = Elem<T>::add(x, u[k]);
+            if constexpr (kIntLeaf<T>)
+                if (x < 0) neg = min(neg, (uint32_t)sc[i]);
         } else {
-            x = leaf_chain<T, CMP>(x, row, row0, bshift, bstart, perm, sc, sv, lr);
+            uint32_t rn = kSpSkip;
+            x = leaf_chain<T, CMP>(x, row, row0, bshift, bstart, perm, sc, sv, lr, &rn);
+            neg = min(neg, rn);
         }
         shard[row] = x;
     }
+    // the chunk's first negative counter (min sequence); the host undoes every add
+    // after it, so the store holds what the reference's does when it throws
+    if constexpr (kIntLeaf<T>)
+        if (neg != kSpSkip) atomicMin(&ctrl->neg_pos, (unsigned long long)neg);
 }
 
 // Replay of flagged leaves from the fully sorted chunk (comp ascending).
 template <typename T>
 __global__ __launch_bounds__(256) void k_sp_runs(T* __restrict__ shard, const uint64_t* __restrict__ comp,
                                                  const T* __restrict__ val, int64_t n, int SL,
-                                                 const uint8_t* __restrict__ leafflag, uint32_t seq_cut) {
+                                                 const uint8_t* __restrict__ leafflag, uint32_t seq_cut,
+                                                 Ctrl* __restrict__ ctrl) {
     const int64_t p = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (p >= n) return;
     const uint64_t row = comp[p] >> 32;
@@ -536,8 +555,15 @@ __global__ __launch_bounds__(256) void k_sp_runs(T* __restrict__ shard, const ui
     if ((uint32_t)comp[p] >= seq_cut) return;  // the row's only records are at / past the cutoff
     T v = shard[row];
     // the row's run in sequence order; records past the cutoff sort last
-    for (int64_t q = p; q < n && (comp[q] >> 32) == row && (uint32_t)comp[q] < seq_cut; ++q)
+    bool neg = false;
+    for (int64_t q = p; q < n && (comp[q] >> 32) == row && (uint32_t)comp[q] < seq_cut; ++q) {
         v = Elem<T>::add(v, val[q]);
+        if constexpr (kIntLeaf<T>)
+            if (!neg && v < 0) {  // this row's first negative counter (int32 arrays)
+                neg = true;
+                atomicMin(&ctrl->neg_pos, (unsigned long long)(uint32_t)comp[q]);
+            }
+    }
     shard[row] = v;
 }
 
@@ -901,6 +927,7 @@ hipError_t launch_sparse_partition_fast(int vtype, const Batch& bt, const SpPlan
                                         uint64_t tail_cut, SpStat* hstat, hipStream_t st) {
     if (vtype == kF32) return partition_fast_t<float>(bt, pl, l, ws, stride, K, first, rows, ctrl, tail_cut, hstat, st);
     if (vtype == kF64) return partition_fast_t<double>(bt, pl, l, ws, stride, K, first, rows, ctrl, tail_cut, hstat, st);
+    if (vtype == kI32) return partition_fast_t<int32_t>(bt, pl, l, ws, stride, K, first, rows, ctrl, tail_cut, hstat, st);
     return hipErrorInvalidValue;
 }
 
@@ -909,6 +936,7 @@ hipError_t launch_sparse_partition(int vtype, const Batch& bt, const SpPlan& pl,
                                    uint64_t tail_cut, hipStream_t st) {
     if (vtype == kF32) return partition_t<float>(bt, pl, l, ws, stride, K, first, rows, ctrl, tail_cut, st);
     if (vtype == kF64) return partition_t<double>(bt, pl, l, ws, stride, K, first, rows, ctrl, tail_cut, st);
+    if (vtype == kI32) return partition_t<int32_t>(bt, pl, l, ws, stride, K, first, rows, ctrl, tail_cut, st);
     return hipErrorInvalidValue;
 }
 
@@ -936,9 +964,10 @@ hipError_t launch_sparse_leaf(int vtype, void* shard, const SpPlan& pl, const Sp
     // line buckets: leaf rows >> bshift < kSpLines
     int bshift = 0;
     while ((((int64_t)1 << pl.SL) >> bshift) > kSpLines) ++bshift;
-    g_kernel_name = vtype == kF64 ? "dml::k_sp_leaf<double, false>"
-                    : pl.compact  ? "dml::k_sp_leaf<float, true>"
-                                  : "dml::k_sp_leaf<float, false>";
+    g_kernel_name = vtype == kF64   ? "dml::k_sp_leaf<double, false>"
+                    : vtype == kI32 ? "dml::k_sp_leaf<int, false>"
+                    : pl.compact    ? "dml::k_sp_leaf<float, true>"
+                                    : "dml::k_sp_leaf<float, false>";
     if (vtype == kF32 && pl.compact)
         hipExtLaunchKernelGGL((k_sp_leaf<float, true>), grid, dim3(kSpLeafThreads), leaf_lds_pad<float, true>(), st,
                               ev.start, ev.stop, 0,
@@ -954,6 +983,11 @@ hipError_t launch_sparse_leaf(int vtype, void* shard, const SpPlan& pl, const Sp
                               ev.start, ev.stop, 0,
                               (double*)shard, bounds, cnt2, pl.cap2, comp2, (const double*)(ws + l.val2), pl.SL, pl.D2,
                               bshift, pl.seq_cut, flag, ctrl, prev);
+    else if (vtype == kI32)
+        hipExtLaunchKernelGGL((k_sp_leaf<int32_t, false>), grid, dim3(kSpLeafThreads), leaf_lds_pad<int32_t, false>(),
+                              st, ev.start, ev.stop, 0,
+                              (int32_t*)shard, bounds, cnt2, pl.cap2, comp2, (const int32_t*)(ws + l.val2), pl.SL,
+                              pl.D2, bshift, pl.seq_cut, flag, ctrl, prev);
     else
         return hipErrorInvalidValue;
     return hipGetLastError();
@@ -986,7 +1020,7 @@ hipError_t sparse_replay(int vtype, void* shard, const SpPlan& pl_in, const SpLa
         unsigned long long* packed = (unsigned long long*)(ws + l.stat + sizeof(SpStat));
         e = hipMemsetAsync(packed, 0, sizeof *packed, st);
         if (e == hipSuccess) {
-            if (vtype == kF32)
+            if (vtype == kF32 || vtype == kI32)  // 4-B values, moved as bits
                 hipLaunchKernelGGL(k_sp_pack_flagged<float>, dim3((unsigned)pl.nleaves), dim3(256), 0, st,
                                    (const uint32_t*)(ws + l.cur2), pl.cap2, (const uint8_t*)(ws + l.leafflag),
                                    (const uint64_t*)kin, (const float*)vin_p, packed, kout, (float*)vout_p);
@@ -1013,16 +1047,20 @@ hipError_t sparse_replay(int vtype, void* shard, const SpPlan& pl_in, const SpLa
     const int n = (int)nk;
     size_t tmp = 0;
     void* dtmp = nullptr;
-    if (vtype == kF32) {
+    if (vtype == kF32 || vtype == kI32) {
         uint32_t* vin = (uint32_t*)vin_p;
         uint32_t* vout = (uint32_t*)vout_p;
         e = hipcub::DeviceRadixSort::SortPairs(nullptr, tmp, kin, kout, vin, vout, n, 0, 64, st);
         if (e == hipSuccess) e = hipMallocAsync(&dtmp, tmp, st);
         if (e == hipSuccess) e = hipcub::DeviceRadixSort::SortPairs(dtmp, tmp, kin, kout, vin, vout, n, 0, 64, st);
-        if (e == hipSuccess)
+        if (e == hipSuccess && vtype == kF32)
             hipLaunchKernelGGL(k_sp_runs<float>, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, st, (float*)shard,
                                (const uint64_t*)kout, (const float*)vout, (int64_t)n, pl.SL,
-                               (const uint8_t*)(ws + l.leafflag), pl.seq_cut);
+                               (const uint8_t*)(ws + l.leafflag), pl.seq_cut, ctrl);
+        else if (e == hipSuccess)
+            hipLaunchKernelGGL(k_sp_runs<int32_t>, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, st,
+                               (int32_t*)shard, (const uint64_t*)kout, (const int32_t*)vout, (int64_t)n, pl.SL,
+                               (const uint8_t*)(ws + l.leafflag), pl.seq_cut, ctrl);
     } else {
         uint64_t* vin = (uint64_t*)vin_p;
         uint64_t* vout = (uint64_t*)vout_p;
@@ -1032,7 +1070,7 @@ hipError_t sparse_replay(int vtype, void* shard, const SpPlan& pl_in, const SpLa
         if (e == hipSuccess)
             hipLaunchKernelGGL(k_sp_runs<double>, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, st, (double*)shard,
                                (const uint64_t*)kout, (const double*)vout, (int64_t)n, pl.SL,
-                               (const uint8_t*)(ws + l.leafflag), pl.seq_cut);
+                               (const uint8_t*)(ws + l.leafflag), pl.seq_cut, ctrl);
     }
     if (e == hipSuccess) e = hipGetLastError();
     if (dtmp) (void)hipFreeAsync(dtmp, st);

@@ -7,7 +7,7 @@
 //
 // A push batch runs per chunk of <= kMaxW pushes:
 //   memset(Ctrl+slots) -> k_index -> k_reduce (matrix)   or
-//   memset(Ctrl) -> k_array_validate -> k_array_apply x pushes (array)
+//   memset(Ctrl) -> two-level partition by leaf -> k_sp_leaf (array; dml_sparse.hip)
 // and is "retired" later (next call, flush, or immediately in sync mode):
 // sync, read Ctrl, replay pushes that repeat a row (exact layered path), undo
 // int32 adds past the first negative counter (exact mod 2^32), and turn the
@@ -133,8 +133,6 @@ struct dml_store {
     int64_t cand_n = 0;
     MaxDelta* md = nullptr;
     float initial_alpha = 0.f, min_alpha = 0.f, factor = 1.5f;  // :22, :26
-    uint32_t* mark = nullptr;   // int32 arrays: per-element token of the last push that added to it
-    uint32_t mark_tok = 0;
     Workspace ws[kRing];
     size_t slot_bytes = 0, ws_bytes = 0;
     int next_ws = 0;
@@ -375,7 +373,7 @@ int launch_apply(dml_store* s, Chunk& c, Workspace& W, const Ctrl* prev) {
                                             kMdDeferIfRepeat, W.ctrl));
         if (!inpacket) HIPCHK(hipEventRecord(W.applied, s->stream));
         if (s->timing) s->ev_used.emplace_back(W.kstart, W.applied);
-    } else if (c.sorted) {
+    } else {
         LaunchEv ev{};
         if (s->timing) {
             auto p = ev_pair(s);
@@ -383,27 +381,6 @@ int launch_apply(dml_store* s, Chunk& c, Workspace& W, const Ctrl* prev) {
             s->ev_used.push_back(p);
         }
         HIPCHK(launch_sparse_leaf(vtype_of(s->desc), s->data, c.sp, c.spl, W.sp, W.ctrl, prev, s->stream, ev));
-        HIPCHK(hipEventRecord(W.applied, s->stream));
-    } else {
-        for (int b = 0; b < c.nb; ++b) {
-            LaunchEv ev{};
-            if (s->timing) {
-                auto p = ev_pair(s);
-                ev = {p.first, p.second};
-                s->ev_used.push_back(p);
-            }
-            uint32_t tok = 0;
-            if (s->mark) {
-                if (++s->mark_tok == 0) {  // tokens wrapped: forget every stamp
-                    HIPCHK(hipMemsetAsync(s->mark, 0, (size_t)s->rows * sizeof(uint32_t), s->stream));
-                    s->mark_tok = 1;
-                }
-                tok = s->mark_tok;
-            }
-            HIPCHK(launch_array_apply(vtype_of(s->desc), s->data, s->rows, c.bt.base[b], c.bt.nrec[b], c.bt.bidx[b],
-                                      s->stride, s->K, s->first, W.ctrl, c.tail_cut, prev, s->stream, ev, s->mark,
-                                      tok));
-        }
         HIPCHK(hipEventRecord(W.applied, s->stream));
     }
     // ctrl read-back on its own stream, so the next chunk's apply follows this one directly
@@ -453,15 +430,12 @@ int launch_chunk(dml_store* s, Chunk& c, Workspace& W, const Ctrl* prev) {
         HIPCHK(launch_index(c.bt, c.nb, c.max_nrec, s->stride, s->K, s->first, s->rows, W.slot, W.rowflag, W.ctrl,
                             c.tail_cut, is));
     } else {
-        // float / double arrays: partition the chunk by leaf (row range) for the ordered
-        // per-leaf apply (its first pass also finds the cutoff); int32 arrays keep the
-        // validated per-push atomic path (negativity check).
+        // arrays: partition the chunk by leaf (row range) for the ordered per-leaf
+        // apply (its first pass also finds the cutoff); int32 leaves check every add
+        // (IntArrayStore.java:108-110) and report the chunk's first negative counter
         const int vt = vtype_of(s->desc);
-        c.sorted = vt == kF32 || vt == kF64;
-        if (!c.sorted)
-            HIPCHK(launch_array_validate(c.bt, c.nb, c.max_nrec, s->stride, s->K, s->first, s->rows, W.ctrl,
-                                         c.tail_cut, is));
-        if (c.sorted) {
+        c.sorted = true;
+        {
             c.sp = sparse_plan(c.bt, c.nb, s->rows);
             // one 8-B word per fp32 record through the partition
             c.sp.compact = vt == kF32 && c.sp.SL + c.sp.D2 <= kSpCompactRowBits && c.tail_cut == kNoPos;
@@ -721,33 +695,38 @@ int retire_front(dml_store* s) {
     if (s->is_matrix && ctl.no_dup == 0u) {
         rc = replay_rows(s, c, W, &ctl);
         if (rc) return rc;
-    } else if (!s->is_matrix && ctl.no_dup == 0u && s->mark) {
-        // an int32 push repeated a key: the atomics' order decided which add saw a
-        // negative counter; re-run the chunk in record order for the exact first one
-        const uint64_t cut = std::min<uint64_t>(ctl.cutoff, c.tail_cut);
-        HIPCHK(launch_array_exact_i32((int32_t*)s->data, s->rows, c.bt, c.nb, s->stride, s->K, s->first, cut, W.ctrl,
-                                      s->stream));
+    } else if (!s->is_matrix && ctl.no_dup == 0u) {
+        // leaves too large for the LDS sort were skipped by the leaf kernel: apply them
+        // exactly (an int32 replay may find an earlier negative counter)
+        HIPCHK(sparse_replay(vtype_of(s->desc), s->data, c.sp, c.spl, W.sp, c.bt, s->stride, s->K, s->first, s->rows,
+                             W.ctrl, c.tail_cut, s->stream));
         HIPCHK(hipMemcpyAsync(&ctl.neg_pos, &W.ctrl->neg_pos, sizeof(ctl.neg_pos), hipMemcpyDeviceToHost,
                               s->stream));
         HIPCHK(hipStreamSynchronize(s->stream));
-    } else if (!s->is_matrix && ctl.no_dup == 0u) {
-        // leaves too large for the LDS sort were skipped by the leaf kernel: apply them exactly
-        HIPCHK(sparse_replay(vtype_of(s->desc), s->data, c.sp, c.spl, W.sp, c.bt, s->stride, s->K, s->first, s->rows,
-                             W.ctrl, c.tail_cut, s->stream));
-    } else if (ctl.neg_pos != kNoPos) {
-        if (s->is_matrix) {
-            // the reduce handed its slot rows back clean: rebuild the table (no row
-            // repeats here, so the rowflags stay zero; the index leaves neg_pos alone)
-            HIPCHK(hipMemsetAsync(W.slot, 0xFF, s->slot_bytes, s->stream));
-            HIPCHK(launch_index(c.bt, c.nb, c.max_nrec, s->stride, s->K, s->first, s->rows, W.slot, W.rowflag, W.ctrl,
-                                c.tail_cut, s->stream));
-            HIPCHK(launch_rollback_i32((int32_t*)s->data, s->rows, s->cols, c.bt, c.nb, s->stride, s->K, W.slot,
-                                       W.rowflag, W.ctrl, c.tail_cut, s->stream));
-        } else {
-            for (int b = 0; b < c.nb; ++b)
-                HIPCHK(launch_array_rollback_i32((int32_t*)s->data, s->rows, c.bt.base[b], c.bt.nrec[b], c.bt.bidx[b],
-                                                 s->stride, s->K, s->first, W.ctrl, c.tail_cut, s->stream));
-        }
+    }
+    if (!s->is_matrix && ctl.neg_pos != kNoPos) {
+        // int32 array: the leaves reported the sequence of the chunk's first add that left
+        // a counter negative; as a position (push, record) it bounds the rollback of every
+        // later add (exact mod 2^32), the state the reference leaves when it throws
+        const uint64_t seq = ctl.neg_pos;
+        int b = 0;
+        while (b + 1 < c.nb && (uint64_t)c.sp.rec_base[b + 1] <= seq) ++b;
+        const int64_t r = (int64_t)(seq - (uint64_t)c.sp.rec_base[b]);
+        ctl.neg_pos = pos_of((uint64_t)c.bt.bidx[b], (uint64_t)(r * s->stride + s->K));
+        HIPCHK(hipMemcpyAsync(&W.ctrl->neg_pos, &ctl.neg_pos, sizeof(ctl.neg_pos), hipMemcpyHostToDevice, s->stream));
+        for (int j = 0; j < c.nb; ++j)
+            HIPCHK(launch_array_rollback_i32((int32_t*)s->data, s->rows, c.bt.base[j], c.bt.nrec[j], c.bt.bidx[j],
+                                             s->stride, s->K, s->first, W.ctrl, c.tail_cut, s->stream));
+        HIPCHK(hipStreamSynchronize(s->stream));
+    } else if (s->is_matrix && ctl.neg_pos != kNoPos && ctl.no_dup != 0u) {
+        // (a chunk with repeated rows rolled back inside replay_rows) the reduce handed
+        // its slot rows back clean: rebuild the table (no row repeats here, so the
+        // rowflags stay zero; the index leaves neg_pos alone), then undo past neg_pos
+        HIPCHK(hipMemsetAsync(W.slot, 0xFF, s->slot_bytes, s->stream));
+        HIPCHK(launch_index(c.bt, c.nb, c.max_nrec, s->stride, s->K, s->first, s->rows, W.slot, W.rowflag, W.ctrl,
+                            c.tail_cut, s->stream));
+        HIPCHK(launch_rollback_i32((int32_t*)s->data, s->rows, s->cols, c.bt, c.nb, s->stride, s->K, W.slot, W.rowflag,
+                                   W.ctrl, c.tail_cut, s->stream));
         HIPCHK(hipStreamSynchronize(s->stream));
     }
     const uint64_t cut = std::min<uint64_t>(ctl.cutoff, c.tail_cut);
@@ -986,11 +965,6 @@ int dml_store_create_range(const dml_desc* desc, int64_t first_key, int64_t last
         if ((e = hipMalloc((void**)&s->md, sizeof(MaxDelta))) != hipSuccess) return fail(e, "md alloc");
         if ((e = hipMemsetAsync(s->md, 0, sizeof(MaxDelta), s->stream)) != hipSuccess) return fail(e, "md zero");
     }
-    if (!s->is_matrix && d.value_type == DML_ELEMENT_TYPE_INT) {
-        if ((e = hipMalloc((void**)&s->mark, (size_t)rows * sizeof(uint32_t))) != hipSuccess) return fail(e, "mark alloc");
-        if ((e = hipMemsetAsync(s->mark, 0, (size_t)rows * sizeof(uint32_t), s->stream)) != hipSuccess)
-            return fail(e, "mark zero");
-    }
     s->slot_bytes = s->is_matrix ? (size_t)rows * kMaxW * sizeof(int32_t) : 0;
     s->ws_bytes = sizeof(Ctrl) + s->slot_bytes + (s->is_matrix ? (size_t)rows * sizeof(uint32_t) : 0);
     if ((e = hipStreamCreateWithFlags(&s->istream, hipStreamNonBlocking)) != hipSuccess) return fail(e, "index stream");
@@ -1041,7 +1015,6 @@ void dml_store_destroy(dml_store* s) {
         (void)hipFree(s->delta);
         (void)hipFree(s->cand);
         (void)hipFree(s->md);
-        (void)hipFree(s->mark);
         (void)hipFree(s->neg_dev);
         if (s->neg_host) (void)hipHostFree(s->neg_host);
         if (s->neg_ev) (void)hipEventDestroy(s->neg_ev);

@@ -1340,11 +1340,12 @@ def test_empty_and_single_record_pushes(oracle, kind, api):
 def test_int_array_repeated_keys_exact_error_state(oracle, case):
     """IntArrayStore pushes that list a key several times (legal bytes, never produced by
     SparseArray.writeMap): the reference adds in record order and throws after the first add
-    that leaves a counter negative (IntArrayStore.java:97-113). Per-push atomics get the sums
-    right but not that position — e.g. 1 + (-2) + 5 is negative after the first add in record
-    order, never in the order (+5, -2). The store detects the repeat (per-element push tokens)
-    and re-runs the chunk in record order: data, error key and the no-further-pushes state
-    all equal the oracle's."""
+    that leaves a counter negative (IntArrayStore.java:97-113) — e.g. 1 + (-2) + 5 is
+    negative after the first add in record order, never in the order (+5, -2). int32 arrays
+    take the ordered partition + leaf path: every row's adds in sequence order with the
+    check after each (rows of ~25 records here: leaves beyond the LDS sort go to the exact
+    replay, which checks too), the chunk's first negative (min sequence) bounds the rollback
+    of every later add: data, error key and the no-further-pushes state equal the oracle's."""
     from distml_amd import DataDesc, DistMLException, encode_array_push
     rng = np.random.default_rng(hash(case) % 1000)
     first, rows = 10, 3000
