@@ -53,11 +53,8 @@ import time
 
 ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
-# One hardware queue per stream: the store (apply / index / copy), torch's default
-# stream and the group path's index / comm streams each need their own queue, or
-# HIP multiplexes them onto HIP's default 4 and work meant to overlap serializes
-# (measured on the --group path: the next call's key index queued behind the pieces).
-os.environ.setdefault("GPU_MAX_HW_QUEUES", "8")
+# HIP's default hardware queues (4 per process), as the PS JVM runs: the store and
+# group paths measured the same at 4 and 8 (scripts/gpu_queues.sh).
 
 METRIC = "device-resident gradient-bucket reduce GiB/s (dense fp32 + sparse scatter-add)"
 ROWS, COLS, W = 16384, 1024, 32

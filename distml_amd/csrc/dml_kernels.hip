@@ -1766,16 +1766,25 @@ __global__ __launch_bounds__(256) void k_apply_dense_i32chk(int32_t* __restrict_
     if (first != kNoPos) atomicMin(neg, first);
 }
 
+// The owner apply runs beside the next call's pre-reduce: a grid
+// that fills every free wave slot keeps the pre-reduce's next blocks from being
+// placed (its waves need most of a SIMD's VGPRs). kApplyBlocks bounds it to two
+// blocks per CU; it still moves a config-2 shard's 192 MB well inside one call.
+#ifndef DML_AB_APPLY_BLOCKS
+#define DML_AB_APPLY_BLOCKS 512
+#endif
+constexpr unsigned kApplyBlocks = DML_AB_APPLY_BLOCKS;
+
 hipError_t launch_apply_dense_i32chk(int32_t* shard, const int32_t* src, int64_t n, unsigned long long* neg,
                                      hipStream_t st) {
     if (n <= 0) return hipSuccess;
-    hipLaunchKernelGGL(k_apply_dense_i32chk, dim3(256 * 8), dim3(256), 0, st, shard, src, n, neg);
+    hipLaunchKernelGGL(k_apply_dense_i32chk, dim3(kApplyBlocks), dim3(256), 0, st, shard, src, n, neg);
     return hipGetLastError();
 }
 
 hipError_t launch_apply_dense(int vtype, void* shard, const void* src, int64_t n, hipStream_t st) {
     if (n <= 0) return hipSuccess;
-    const unsigned g = 256 * 8;
+    const unsigned g = kApplyBlocks;
     if (vtype == kF32) hipLaunchKernelGGL(k_apply_dense<float>, dim3(g), dim3(256), 0, st, (float*)shard, (const float*)src, n);
     else if (vtype == kI32) hipLaunchKernelGGL(k_apply_dense<int32_t>, dim3(g), dim3(256), 0, st, (int32_t*)shard, (const int32_t*)src, n);
     else hipLaunchKernelGGL(k_apply_dense<double>, dim3(g), dim3(256), 0, st, (double*)shard, (const double*)src, n);
