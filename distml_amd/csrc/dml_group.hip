@@ -117,8 +117,10 @@ int finish_front(dml_group* g) {
     if (rc == DML_OK) rc = dml_prereduce_stream_wait(c.h, g->rstream);
     const int64_t S = g->step_rows, P = g->pieces, blk = S / P, W = g->world, C = g->cols;
     uint8_t* part = (uint8_t*)g->partial[c.set];
-    uint8_t* rcv = (uint8_t*)g->recv[c.set];
-    for (int64_t j = 0; j < P && rc == DML_OK; ++j) {
+    // one rank: the [rank][row] slices are the shard's rows in order, the
+    // reduce-scatter would be a copy; the owner apply reads the partial itself
+    uint8_t* rcv = W == 1 ? part : (uint8_t*)g->recv[c.set];
+    for (int64_t j = 0; j < P && rc == DML_OK && W > 1; ++j) {
         const ncclResult_t r = ncclReduceScatter(part + (size_t)(j * W * blk * C) * g->vbytes,
                                                  rcv + (size_t)(j * blk * C) * g->vbytes, (size_t)(blk * C), g->dtype,
                                                  ncclSum, g->comm, g->rstream);
@@ -223,7 +225,7 @@ int ensure_partials(dml_group* g) {
     const size_t rcv = (size_t)g->step_rows * (size_t)g->cols * g->vbytes;
     for (int i = 0; i < 2; ++i) {
         GHIP(hipMalloc(&g->partial[i], part));
-        GHIP(hipMalloc(&g->recv[i], rcv));
+        if (g->world > 1) GHIP(hipMalloc(&g->recv[i], rcv));  // one rank applies the partial itself
     }
     GRC(dml_prectx_create(&g->desc, 0, g->total_rows, g->cols, g->device, &g->pctx));
     return DML_OK;

@@ -175,6 +175,10 @@ class ShardGroup:
             self._store_stream = (torch.cuda.ExternalStream(self.store.stream(), device=dev)
                                   if hasattr(self.store, "stream") else None)
 
+    def _local_rs(self) -> bool:
+        """World 1 with the default reduce-scatter: a copy of the partial, skipped."""
+        return self.world == 1 and self._rs == self._default_reduce_scatter
+
     def _default_reduce_scatter(self, out, inp) -> None:
         dist = self.dist
         if self.world == 1:
@@ -205,11 +209,13 @@ class ShardGroup:
         # rows past the matrix end (linearSplit's last shard may be short) stay zero
         self.ops.prereduce(self.fmt, 0, self.total_rows, self.cols, dev_ptrs, lens,
                            self.partial.data_ptr(), stream)
-        self._rs(self.recv, self.partial)
-        if self.recv.is_cuda:
+        recv = self.partial if self._local_rs() else self.recv
+        if recv is not self.partial:
+            self._rs(recv, self.partial)
+        if recv.is_cuda:
             torch.cuda.current_stream().synchronize()
         n = self.shard.size() * self.cols
-        self.ops.apply(self.store, self.recv.data_ptr(), n)
+        self.ops.apply(self.store, recv.data_ptr(), n)
 
     def _push_pipelined(self, dev_ptrs, lens) -> None:
         """Pre-reduce in `pieces` row slices; slice j holds rows [q*S + j*S/P, q*S + (j+1)*S/P)
@@ -262,8 +268,12 @@ class ShardGroup:
             self.ops.verify(h)
             self.ops.stream_wait(h, self.comm.cuda_stream)  # the pieces (or their re-run)
             partial, recv = self._partials[k], self._recvs[k]
+            if self._local_rs():
+                # one rank: the [rank][row] slices are the shard's rows in order, so
+                # the reduce-scatter is the identity and the apply reads the partial
+                recv = partial
             with torch.cuda.stream(self.comm):
-                for j in range(P):
+                for j in range(P if recv is not partial else 0):
                     self._rs(recv[j * blk * cols:(j + 1) * blk * cols],
                              partial[j * world * blk * cols:(j + 1) * world * blk * cols])
             self._rs_done[k].record(self.comm)
