@@ -362,15 +362,21 @@ def headline(ctx: Ctx, L, args, out_line: dict):
         # the same steps with the 32 pushes in a new seeded order every step: the PS
         # selector applies pushes in arrival order (PSAgent.java:166-186)
         import random
-        rnd = random.Random(2024)
         shuffled_batches = []
         for k in range(SHUFFLE_ORDERS):
             bs = bufs[:W] if k % 2 == 0 else bufs[W:]
             order = list(range(W))
-            rnd.shuffle(order)
+            # diagnostics: one order every step (--shuffle-orders 1), or only the
+            # ascending / only the permuted pushes shuffled among their own positions
+            rnd2 = random.Random(2024 + (k % args.shuffle_orders if args.shuffle_orders else k))
+            rnd2.shuffle(order)
+            ev, od = [j for j in order if j % 2 == 0], [j for j in order if j % 2 == 1]
             if args.shuffle_keep_parity:  # diagnostic: ascending pushes stay at even positions
-                ev, od = [j for j in order if j % 2 == 0], [j for j in order if j % 2 == 1]
                 order = [x for pair in zip(ev, od) for x in pair]
+            elif args.shuffle_only == "asc":
+                order = [x for pair in zip(ev, range(1, W, 2)) for x in pair]
+            elif args.shuffle_only == "perm":
+                order = [x for pair in zip(range(0, W, 2), od) for x in pair]
             shuffled_batches.append(DeviceBatch([bs[j].data_ptr() for j in order], [bs[j].numel() for j in order]))
         k_step = [0]
         cur = [batches]
@@ -1036,6 +1042,8 @@ def main():
     ap.add_argument("--sparse-steps", type=int, default=20, help="config-3 sparse leg steps (0 = skip; N=1 only)")
     ap.add_argument("--pieces", type=int, default=1, help="pre-reduce row slices per call (sharded path)")
     ap.add_argument("--shuffle-keep-parity", action="store_true", help=argparse.SUPPRESS)
+    ap.add_argument("--shuffle-orders", type=int, default=0, help=argparse.SUPPRESS)
+    ap.add_argument("--shuffle-only", choices=["", "asc", "perm"], default="", help=argparse.SUPPRESS)
     ap.add_argument("--group", action="store_true",
                     help="use the sharded pre-reduce/reduce-scatter path even at N=1 (path check)")
     ap.add_argument("--legs", default="4,5,4a", help="model-level config legs in the line (4, 5, 4a; '' = none)")
