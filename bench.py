@@ -261,11 +261,15 @@ def _sparse_perm(b, dim):
 
 
 # ---------------------------------------------------------------- config 2
-def make_buckets(L, torch, fmt, n, rows_total, value_seed: int = 1000):
+def make_buckets(L, torch, fmt, n, rows_total, value_seed: int = 1000, alloc_seed: int = 0):
     st = torch.cuda.current_stream().cuda_stream
     bufs = []
+    mem = [torch.empty(rows_total * REC, dtype=torch.uint8, device="cuda") for _ in range(n)]
+    if alloc_seed:  # diagnostic: bucket b in the alloc_order[b]-th allocation (addresses not in push order)
+        import random
+        random.Random(alloc_seed).shuffle(mem)
     for b in range(n):
-        t = torch.empty(rows_total * REC, dtype=torch.uint8, device="cuda")
+        t = mem[b]
         pa, pc = perm_for(b)
         rc = L.dml_synth_dense_bucket(t.data_ptr(), C.byref(fmt.to_c()), 0, rows_total, rows_total, COLS,
                                       value_seed + b, pa % rows_total, pc % rows_total, C.c_void_p(st))
@@ -357,7 +361,8 @@ def headline(ctx: Ctx, L, args, out_line: dict):
         store.synth_fill(7)
         # two bucket sets, stepped alternately: the same key order per push position
         # (a worker pushing the same key set), different gradient values every step
-        bufs = make_buckets(L, torch, fmt, W, ROWS) + make_buckets(L, torch, fmt, W, ROWS, value_seed=5000)
+        bufs = (make_buckets(L, torch, fmt, W, ROWS, alloc_seed=args.alloc_seed) +
+                make_buckets(L, torch, fmt, W, ROWS, value_seed=5000, alloc_seed=args.alloc_seed))
         batches = [DeviceBatch([b.data_ptr() for b in bs], [b.numel() for b in bs]) for bs in (bufs[:W], bufs[W:])]
         # the same steps with the 32 pushes in a new seeded order every step: the PS
         # selector applies pushes in arrival order (PSAgent.java:166-186)
@@ -1043,6 +1048,7 @@ def main():
     ap.add_argument("--pieces", type=int, default=1, help="pre-reduce row slices per call (sharded path)")
     ap.add_argument("--shuffle-keep-parity", action="store_true", help=argparse.SUPPRESS)
     ap.add_argument("--shuffle-orders", type=int, default=0, help=argparse.SUPPRESS)
+    ap.add_argument("--alloc-seed", type=int, default=0, help=argparse.SUPPRESS)
     ap.add_argument("--shuffle-only", choices=["", "asc", "perm"], default="", help=argparse.SUPPRESS)
     ap.add_argument("--group", action="store_true",
                     help="use the sharded pre-reduce/reduce-scatter path even at N=1 (path check)")
