@@ -204,8 +204,12 @@ class ShardGroup:
                 and self.step_rows % self.pieces == 0):
             return self._push_pipelined(dev_ptrs, lens)
         if self.partial.is_cuda:
-            # the one-shot path reuses buffer set 0: drain the pipelined calls that may still use it
+            # the one-shot path reuses buffer set 0: drain the pipelined calls that may still use it,
+            # and let the store's stream finish the owner applies that read partial / recv
+            # (a previous call's, pipelined or one-shot) before they are rewritten
             self._drain()
+            if self._store_stream is not None:
+                self._store_stream.synchronize()
         # rows past the matrix end (linearSplit's last shard may be short) stay zero
         self.ops.prereduce(self.fmt, 0, self.total_rows, self.cols, dev_ptrs, lens,
                            self.partial.data_ptr(), stream)

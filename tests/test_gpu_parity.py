@@ -709,6 +709,50 @@ def test_shard_group_rccl_world1(oracle):
         dist.destroy_process_group()
 
 
+def test_shard_group_oneshot_world1_consecutive(oracle):
+    """The one-shot full-range path (> 64 pushes per call) at world 1, where the owner
+    apply reads the partial itself: two calls back to back without a flush, so the second
+    call's pre-reduce rewrites the partial right after the first call's apply was
+    enqueued on the store's stream (it must wait for it). fp32 within the bound of
+    tests/test_group_gloo.py."""
+    import socket
+    import torch.distributed as dist
+    from distml_amd import DataDesc
+    from distml_amd.group import ShardGroup
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    dist.init_process_group("nccl", init_method=f"tcp://127.0.0.1:{port}", rank=0, world_size=1,
+                            device_id=torch.device("cuda", 0))
+    try:
+        rows, cols, W, calls = 1024, 256, 66, 2
+        fmt = DataDesc(1, 0, 1)
+        g = ShardGroup(fmt, rows, cols, 0, 1, device=0)
+        g.store.synth_fill(5)
+        o = oracle_store(oracle, fmt, 0, rows - 1, cols)
+        o.synth_fill(5)
+        terms = np.abs(o.data.astype(np.float64))
+        dev = []
+        for c in range(calls):
+            host = [oracle.synth_dense_bucket(0, 1, 0, rows, rows, cols, 700 + 100 * c + b, 2 * b + 1, 3 * b)
+                    for b in range(W)]
+            for h in host:
+                assert o.push(h.tobytes()) == 0
+                rec = h.reshape(rows, 4 + 4 * cols)
+                terms[rec[:, :4].copy().view("<i4").ravel()] += np.abs(rec[:, 4:].copy().view("<f4"))
+            dev.append([torch.from_numpy(h).cuda() for h in host])  # alive until the flush
+        torch.cuda.synchronize()
+        for d in dev:
+            g.push_full_range([t.data_ptr() for t in d], [t.numel() for t in d],
+                              torch.cuda.current_stream().cuda_stream)
+        g.flush()
+        diff = np.abs(g.store.values().astype(np.float64) - o.data.astype(np.float64))
+        assert np.all(diff <= 2 * calls * W * 2.0 ** -24 * terms)
+    finally:
+        dist.destroy_process_group()
+
+
 @pytest.mark.parametrize("binding", ["torch", "native"])
 @pytest.mark.parametrize("vt", [1, 0])
 def test_sharded_speculation_world1(oracle, binding, vt):
