@@ -412,7 +412,9 @@ def headline(ctx: Ctx, L, args, out_line: dict):
         algo_per_rank = W * BUCKET + 2 * group.shard.size() * COLS * 4
 
     timing = not args.no_timing
-    timed_store.set_timing(timing and not sharded)
+    # one chunk in 16 carries start/stop events: events in every dispatch lengthen the
+    # boundary between two reduces
+    timed_store.set_timing(timing and not sharded, every=16)
     t0 = time.perf_counter()
     for _ in range(args.warmup):
         step()

@@ -23,6 +23,19 @@ __device__ inline u32x4 ldg16_nt(const uint8_t* p) {
 }
 __device__ inline void stg16_nt(void* p, u32x4 v) { __builtin_nontemporal_store(v, (DML_GLOBAL u32x4_u*)(p)); }
 __device__ inline void stg16(void* p, u32x4 v) { *(DML_GLOBAL u32x4_u*)(p) = v; }
+// Write-through 16-B store (sc1: the line leaves the XCD's L2 at once), through a
+// buffer descriptor based at a wave-uniform `base` (byte offset `off` < nbytes):
+// rows a kernel writes last leave no dirty L2 lines for the kernel-end writeback
+// that holds up the next dispatch on the stream (MI355X_MICROARCH.md, kernel boundary).
+__device__ inline void stg16_wt(const void* base, uint32_t nbytes, uint32_t off, u32x4 v) {
+    const uint64_t b = (uint64_t)base;
+    const uint32_t lo = __builtin_amdgcn_readfirstlane((uint32_t)b);
+    const uint32_t hi = __builtin_amdgcn_readfirstlane((uint32_t)(b >> 32));
+    const uint32_t n = __builtin_amdgcn_readfirstlane(nbytes);
+    void* ub = (void*)(((uint64_t)hi << 32) | lo);
+    __amdgpu_buffer_rsrc_t rsrc = __builtin_amdgcn_make_buffer_rsrc(ub, (short)0, (int)n, 0x00020000);
+    __builtin_amdgcn_raw_buffer_store_b128(v, rsrc, (int)off, 0, 16);
+}
 
 __device__ inline uint32_t ld32(const uint8_t* p) { return ldg32(p); }
 __device__ inline int64_t ld_key(const uint8_t* p, int K) {

@@ -162,6 +162,8 @@ struct dml_store {
     // timing of the dominant kernel
     const char* kname = nullptr;  // its instantiation, as last launched (dml_store_kernel_name)
     bool timing = false;
+    int32_t timing_every = 1;  // time one matrix chunk in timing_every (dml_store_set_timing)
+    int64_t timing_k = 0;
     std::vector<std::pair<hipEvent_t, hipEvent_t>> ev_used, ev_free;
     double timed_ms = 0.0;
     int64_t timed_n = 0;
@@ -356,12 +358,15 @@ int launch_apply(dml_store* s, Chunk& c, Workspace& W, const Ctrl* prev) {
         }
     } name_on_exit{s};
     if (s->is_matrix) {
-        // Boundary between consecutive reduces (measured): a plain dispatch
-        // followed by one marker event ~7 µs; with timing, hipExtLaunchKernel's in-packet
-        // start/stop events (~10 µs) beat start+stop markers (~12 µs).
-        const bool inpacket = s->timing && !s->adagrad;
-        LaunchEv ev = inpacket ? LaunchEv{W.kstart, W.applied} : LaunchEv{};
-        if (s->timing && !inpacket) HIPCHK(hipEventRecord(W.kstart, s->stream));
+        // Boundary between consecutive reduces (measured): the chunk's
+        // completion event rides in the reduce's dispatch packet (a marker packet after
+        // it cost ~7 µs); a timed chunk also carries its start event there (start/stop
+        // in every packet ~10 µs, so the bench times a sample of the chunks). AdaGrad's
+        // finalize kernels follow the reduce: marker events around both.
+        const bool inpacket = !s->adagrad;
+        const bool timed = s->timing && (s->adagrad || s->timing_every <= 1 || s->timing_k++ % s->timing_every == 0);
+        LaunchEv ev = inpacket ? LaunchEv{timed ? W.kstart : nullptr, W.applied} : LaunchEv{};
+        if (timed && !inpacket) HIPCHK(hipEventRecord(W.kstart, s->stream));
         int64_t nblk = 0;
         W.clears = reduce_clears_slots(vtype_of(s->desc), reduce_mode(s), s->cols);
         c.bt.src = c.in != c.out ? c.in : nullptr;
@@ -371,8 +376,8 @@ int launch_apply(dml_store* s, Chunk& c, Workspace& W, const Ctrl* prev) {
             // finalized here unless the index saw a repeated row: then after its replay
             HIPCHK(launch_maxdelta_finalize(s->cand, nblk, s->md, c.bt, c.nb, s->stride, s->K, s->V, s->stream,
                                             kMdDeferIfRepeat, W.ctrl));
-        if (!inpacket) HIPCHK(hipEventRecord(W.applied, s->stream));
-        if (s->timing) s->ev_used.emplace_back(W.kstart, W.applied);
+        if (!inpacket || nblk <= 0) HIPCHK(hipEventRecord(W.applied, s->stream));  // (no dispatch: a marker)
+        if (timed && nblk > 0) s->ev_used.emplace_back(W.kstart, W.applied);
     } else {
         LaunchEv ev{};
         if (s->timing) {
@@ -1422,6 +1427,8 @@ int dml_store_set_timing(dml_store* s, int32_t enable) {
     if (int rc = check_store(s)) return rc;
     std::lock_guard<std::mutex> lk(s->mu);
     s->timing = enable != 0;
+    s->timing_every = enable > 1 ? enable : 1;
+    s->timing_k = 0;
     return DML_OK;
 }
 

@@ -330,8 +330,9 @@ class DataStore:
         check(_lib.load().dml_store_stream(self._h, C.byref(p)), self)
         return p.value or 0
 
-    def set_timing(self, on: bool):
-        check(_lib.load().dml_store_set_timing(self._h, int(on)), self)
+    def set_timing(self, on, every: int = 1):
+        """Kernel timing of the dominant reduce: every launch, or one chunk in `every`."""
+        check(_lib.load().dml_store_set_timing(self._h, (max(int(every), 1) if on else 0)), self)
 
     def kernel_name(self) -> str:
         """Instantiation of the dominant kernel last launched (dml_store_kernel_name)."""

@@ -224,9 +224,11 @@ void dml_host_free(void* host_ptr);
 
 /* hipStream_t of the store, as void*. */
 int dml_store_stream(dml_store* s, void** stream);
-/* When enabled, the store brackets every launch of its dominant reduce kernel
- * with HIP events on its stream; dml_store_kernel_time returns the summed
- * elapsed ms and the number of timed launches since the last reset. */
+/* When enabled, the store brackets launches of its dominant reduce kernel with
+ * HIP events on its stream: every launch for enable == 1, one matrix chunk in
+ * `enable` for enable > 1 (events in every dispatch lengthen the boundary between
+ * two reduces); dml_store_kernel_time returns the summed elapsed ms and the
+ * number of timed launches since the last reset. */
 int dml_store_set_timing(dml_store* s, int32_t enable);
 int dml_store_kernel_time(dml_store* s, double* total_ms, int64_t* launches, int32_t reset);
 /* The instantiation of that dominant kernel as last launched, in rocprof's
