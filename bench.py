@@ -556,7 +556,7 @@ def sparse_leg(ctx: Ctx, L, steps: int, cpu: bool):
         bufs.append(t)
     torch.cuda.synchronize()
     batch = DeviceBatch([b.data_ptr() for b in bufs], [b.numel() for b in bufs])
-    store.set_timing(True)
+    store.set_timing(True, every=2)  # start events on every other leaf launch
 
     def step():
         store.pushDevice(batch)

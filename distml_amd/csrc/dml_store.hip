@@ -379,14 +379,13 @@ int launch_apply(dml_store* s, Chunk& c, Workspace& W, const Ctrl* prev) {
         if (!inpacket || nblk <= 0) HIPCHK(hipEventRecord(W.applied, s->stream));  // (no dispatch: a marker)
         if (timed && nblk > 0) s->ev_used.emplace_back(W.kstart, W.applied);
     } else {
-        LaunchEv ev{};
-        if (s->timing) {
-            auto p = ev_pair(s);
-            ev = {p.first, p.second};
-            s->ev_used.push_back(p);
-        }
+        // the leaf launch carries the chunk's completion event (and, when timed, its start)
+        const bool launched = c.sp.nleaves > 0;
+        const bool timed = launched && s->timing && (s->timing_every <= 1 || s->timing_k++ % s->timing_every == 0);
+        const LaunchEv ev = launched ? LaunchEv{timed ? W.kstart : nullptr, W.applied} : LaunchEv{};
         HIPCHK(launch_sparse_leaf(vtype_of(s->desc), s->data, c.sp, c.spl, W.sp, W.ctrl, prev, s->stream, ev));
-        HIPCHK(hipEventRecord(W.applied, s->stream));
+        if (!launched) HIPCHK(hipEventRecord(W.applied, s->stream));
+        if (timed) s->ev_used.emplace_back(W.kstart, W.applied);
     }
     // ctrl read-back on its own stream, so the next chunk's apply follows this one directly
     HIPCHK(hipStreamWaitEvent(s->cstream, W.applied, 0));
