@@ -465,6 +465,10 @@ def headline(ctx: Ctx, L, args, out_line: dict):
             shuffled["in_order_again"] = {
                 "ms_per_step": round(el_a / args.steps * 1e3, 4), "avg_kernel_us": round(ka_ms / ka_n * 1e3, 2),
                 "frac": round(algo_per_rank / (ka_ms / ka_n / 1e3) / 1e9 / HBM_PEAK_GBS, 4)}
+        # the same steps with the buckets generated into the 32 buffers in a seeded
+        # order (which buffer holds which push is the PS's accident): DESIGN.md §4
+        shuffled["buffers_shuffled"] = buffers_shuffled_line(ctx, L, args, timed_store, step, finish, cur, k_step,
+                                                             fmt, algo_per_rank)
     timed_store.set_timing(False)
     value = algo_per_rank * world * args.steps / el / 2**30
     out_line.update({
@@ -512,6 +516,32 @@ def headline(ctx: Ctx, L, args, out_line: dict):
     del bufs
     torch.cuda.synchronize()
     torch.cuda.empty_cache()
+
+
+def buffers_shuffled_line(ctx: Ctx, L, args, store, step, finish, cur, k_step, fmt, algo_per_rank) -> dict:
+    """The in-order steps over two new bucket sets whose pushes were generated into
+    their buffers in a seeded order (make_buckets(alloc_seed=7)): the headline's
+    buffers hold the pushes in allocation order, a PS's receive buffers do not."""
+    torch = ctx.torch
+    from distml_amd.store import DeviceBatch
+    b2 = (make_buckets(L, torch, fmt, W, ROWS, alloc_seed=7) +
+          make_buckets(L, torch, fmt, W, ROWS, value_seed=5000, alloc_seed=7))
+    cur[0] = [DeviceBatch([b.data_ptr() for b in bs], [b.numel() for b in bs]) for bs in (b2[:W], b2[W:])]
+    k_step[0] = 0
+    el = timed_steps(ctx, step, finish, args.steps, min(args.warmup, 50),
+                     reset=lambda: (store.kernel_time(reset=True), store.stats(reset=True)))
+    k_ms, k_n = store.kernel_time(reset=True)
+    store.stats(reset=True)
+    out = {"pushes": "in order, over two bucket sets generated into their 32 buffers in a seeded order",
+           "value": round(algo_per_rank * args.steps / el / 2**30, 2), "unit": "GiB/s",
+           "ms_per_step": round(el / args.steps * 1e3, 4)}
+    if k_n:
+        out.update({"avg_kernel_us": round(k_ms / k_n * 1e3, 2),
+                    "frac": round(algo_per_rank / (k_ms / k_n / 1e3) / 1e9 / HBM_PEAK_GBS, 4)})
+    cur[0] = []
+    del b2
+    torch.cuda.synchronize()
+    return out
 
 
 def stream_peaks(L, torch, nbytes: int = 1 << 31, reps: int = 5):
