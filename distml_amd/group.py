@@ -238,11 +238,12 @@ class ShardGroup:
         blk = S // P
         k = self._k
         self._k ^= 1
-        # pieces run on the group's own stream, after whatever the caller's current
-        # stream has enqueued (the producers of the pushes)
+        # the key index (side stream) orders after whatever the caller's current stream
+        # has enqueued (the producers of the pushes); the pieces run on the group's own
+        # stream once the host has seen that index finish (dml_prereduce_piece waits for
+        # it), so they follow the producers too — without a cross-stream barrier packet
+        # ahead of them on the piece stream (~5 µs between two calls' pieces, measured)
         self._ready.record(torch.cuda.current_stream())
-        self.cstream.wait_event(self._ready)
-        # the key index reads the push keys too: it orders after the producers as well
         self.istream.wait_event(self._ready)
         st = self.cstream.cuda_stream
         partial = self._partials[k]
