@@ -261,10 +261,17 @@ def _sparse_perm(b, dim):
 
 
 # ---------------------------------------------------------------- config 2
+SLAB = [False]  # --one-slab (diagnostic)
+
+
 def make_buckets(L, torch, fmt, n, rows_total, value_seed: int = 1000, alloc_seed: int = 0):
     st = torch.cuda.current_stream().cuda_stream
     bufs = []
-    mem = [torch.empty(rows_total * REC, dtype=torch.uint8, device="cuda") for _ in range(n)]
+    if SLAB[0]:  # diagnostic: the n buckets as slices of one allocation
+        slab = torch.empty(n * rows_total * REC, dtype=torch.uint8, device="cuda")
+        mem = [slab[i * rows_total * REC:(i + 1) * rows_total * REC] for i in range(n)]
+    else:
+        mem = [torch.empty(rows_total * REC, dtype=torch.uint8, device="cuda") for _ in range(n)]
     if alloc_seed:  # diagnostic: bucket b in the alloc_order[b]-th allocation (addresses not in push order)
         import random
         random.Random(alloc_seed).shuffle(mem)
@@ -1081,6 +1088,7 @@ def main():
     ap.add_argument("--shuffle-keep-parity", action="store_true", help=argparse.SUPPRESS)
     ap.add_argument("--shuffle-orders", type=int, default=0, help=argparse.SUPPRESS)
     ap.add_argument("--alloc-seed", type=int, default=0, help=argparse.SUPPRESS)
+    ap.add_argument("--one-slab", action="store_true", help=argparse.SUPPRESS)
     ap.add_argument("--shuffle-only", choices=["", "asc", "perm"], default="", help=argparse.SUPPRESS)
     ap.add_argument("--group", action="store_true",
                     help="use the sharded pre-reduce/reduce-scatter path even at N=1 (path check)")
@@ -1105,6 +1113,7 @@ def main():
     # (RCCL refuses two ranks on one device); numbers from it are not measurements
     ap.add_argument("--rehearse-gloo", action="store_true", help=argparse.SUPPRESS)
     args = ap.parse_args()
+    SLAB[0] = args.one_slab
     if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
         sys.exit(launch_ranks(args.gpus, sys.argv[1:]))
     # stdout carries exactly the one JSON line: RCCL and other native libraries print
