@@ -1972,3 +1972,36 @@ def test_adagrad_identity_checked_large(oracle, case):
     assert kat.bits_equal(a, o.alpha) and kat.bits_equal(d, o.delta)
     assert s.maxDelta() == o.max_delta()
     s.close()
+
+
+@pytest.mark.parametrize("vt", [1, 3])
+def test_sampled_timing_and_write_through_rows(oracle, vt):
+    """dml_store_set_timing(s, every): one chunk in `every` carries start/stop events
+    (the others only the in-packet completion event), and the whole-KiB-row reduce
+    stores write-through (stg16_wt): 24 async calls of two full-range pushes (one
+    ascending, one permuted) on 4-KiB / 8-KiB rows, f32 and f64, bytes-equal against the
+    oracle, with 24 / 4 = 6 timed launches."""
+    from distml_amd import DataDesc
+    from distml_amd.store import DeviceBatch
+    rows, cols, calls = 512, 1024, 24
+    fmt = DataDesc(1, 0, vt)
+    s, _ = mk_store(fmt, 0, rows - 1, cols)
+    o = oracle_store(oracle, fmt, 0, rows - 1, cols)
+    s.synth_fill(9)
+    o.synth_fill(9)
+    host = [oracle.synth_dense_bucket(0, vt, 0, rows, rows, cols, 300 + b, 1 if b % 2 == 0 else 77, 0 if b % 2 == 0 else 5)
+            for b in range(4)]
+    dev = [torch.from_numpy(h).cuda() for h in host]
+    torch.cuda.synchronize()
+    s.set_timing(True, every=4)
+    for c in range(calls):
+        pair = dev[2 * (c % 2): 2 * (c % 2) + 2]
+        s.pushDevice(DeviceBatch([t.data_ptr() for t in pair], [t.numel() for t in pair]))
+        for h in host[2 * (c % 2): 2 * (c % 2) + 2]:
+            assert o.push(h.tobytes()) == 0
+    s.flush()
+    ms, n = s.kernel_time(reset=True)
+    s.set_timing(False)
+    assert n == calls // 4 and ms > 0.0
+    assert "k_reduce_rows" in s.kernel_name() and s.kernel_name().endswith(", 2>")
+    assert kat.bits_equal(s.values(), o.data)
