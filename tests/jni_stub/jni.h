@@ -1,8 +1,9 @@
-/* Minimal stand-in for the JDK's jni.h, for a compile-only (-fsyntax-only) check
- * of integration/jni/dml_jni.cc in an image without a JDK (tests/test_jni_shim.py).
- * It declares only the JNI types and JNIEnv members the shim uses, with the
- * JNI specification's signatures; it is never linked or run. A real build uses
- * $JAVA_HOME/include/jni.h (see the build line in dml_jni.cc). */
+/* Minimal stand-in for the JDK's jni.h, for checks of integration/jni/dml_jni.cc in
+ * an image without a JDK (tests/test_jni_shim.py): a -fsyntax-only compile, and a
+ * build linked with tests/jni_mock/mock_jvm.cc (an in-process JNIEnv implementing
+ * exactly these members) whose Java_* entry points the tests call. It declares only
+ * the JNI types and JNIEnv members the shim uses, with the JNI specification's
+ * signatures. A real build uses $JAVA_HOME/include/jni.h (see dml_jni.cc). */
 #ifndef DML_TEST_JNI_STUB_H
 #define DML_TEST_JNI_STUB_H
 #include <stdint.h>

@@ -4,11 +4,15 @@ types and JNIEnv members it uses, JNI-spec signatures) and the real
 include/distml_ps.h. Also: the shim's native methods are the ones
 GpuDataStore.java / GpuShardGroup.java declare, and nativePush copies the
 byte[] (GetByteArrayRegion) instead of holding a critical section across the
-GPU apply."""
+GPU apply. And the shim RUNS: linked with tests/jni_mock/mock_jvm.cc
+(an in-process JNIEnv), its Java_* entry points are called as GpuDataStore.java /
+GpuShardGroup.java would call them — exception mapping on the CPU, and on the GPU a
+store driven only through JNI, bytes-equal against the oracle."""
 import os
 import re
 import shutil
 import subprocess
+import sys
 
 import pytest
 
@@ -36,3 +40,187 @@ def test_native_methods_match():
 def test_push_does_not_pin_across_the_apply():
     cc = open(os.path.join(JNI, "dml_jni.cc")).read()
     assert "GetPrimitiveArrayCritical" not in cc
+
+
+# ---- the shim RUN through an in-process mock JNIEnv (tests/jni_mock) -----------
+class MockJVM:
+    """integration/jni/dml_jni.cc linked with tests/jni_mock/mock_jvm.cc: the Java_*
+    entry points called as the JVM calls them (JNIEnv*, jclass, args...), with Java
+    byte[] / long[] / DirectByteBuffer objects from the mock."""
+
+    def __init__(self):
+        import ctypes as C
+        sys.path.insert(0, ROOT)
+        from distml_amd import _lib
+        _lib.load()  # the product library first (and with it the HIP runtime the tests use)
+        path = os.path.join(ROOT, "tests", "jni_mock", "libdml_jni_mock.so")
+        if not os.path.exists(path):
+            subprocess.run(["make", "-s", "-C", os.path.dirname(path)], check=True)
+        self.C = C
+        L = self.L = C.CDLL(path)
+        P, I, J, F, D = C.c_void_p, C.c_int32, C.c_int64, C.c_float, C.c_double
+        L.mock_env.restype = P
+        for n, a, r in [("mock_byte_array", [P, I], P), ("mock_long_array", [P, I], P),
+                        ("mock_array_length", [P], I), ("mock_array_data", [P], P),
+                        ("mock_direct_address", [P], P), ("mock_direct_capacity", [P], J), ("mock_free", [P], None),
+                        ("mock_take_exception", [P, I, P, I], I), ("mock_calls", [], I)]:
+            getattr(L, n).argtypes, getattr(L, n).restype = a, r
+        self.env = L.mock_env()
+        sig = {
+            "nativeCreate": ([I, I, I, I, I, I, J, J, I, I, I], J), "nativePush": ([J, P], None),
+            "nativeRand": ([J, J], None), "nativeFetch": ([J, P], P), "nativeFetchRange": ([J, J, J], P),
+            "nativeShardBytes": ([J], J), "nativeWriteAll": ([J], P), "nativeReadAll": ([J, P], None),
+            "nativeSyncTo": ([J, I, I], P), "nativeSyncFrom": ([J, I, I, P], None), "nativeHostAlloc": ([J], P),
+            "nativeHostFree": ([P], None), "nativePushDirect": ([J, P, I, I], None), "nativeFill": ([J, D], None),
+            "nativeSetAlpha": ([J, F, F, F], None), "nativeDestroy": ([J], None),
+        }
+        gsig = {
+            "nativeUniqueId": ([], P), "nativeGroupCreate": ([P, I, I, I, I, I, I, I, I, I, J, I, I], J),
+            "nativeGroupPush": ([J, P, P, C.c_uint8], None), "nativeGroupFlush": ([J], None),
+            "nativeGroupStore": ([J], J), "nativeGroupDestroy": ([J], None),
+        }
+        self.fn = {}
+        for cls, table in (("GpuDataStore", sig), ("GpuShardGroup", gsig)):
+            for name, (args, res) in table.items():
+                f = getattr(L, f"Java_com_intel_distml_util_store_{cls}_{name}")
+                f.argtypes, f.restype = [P, P] + args, res
+                self.fn[name] = f
+
+    def call(self, name, *args):
+        """Call a native method; returns (result, (exception class, message) or None)."""
+        r = self.fn[name](self.env, None, *args)
+        cls, msg = self.C.create_string_buffer(256), self.C.create_string_buffer(1024)
+        exc = (cls.value.decode(), msg.value.decode()) if self.L.mock_take_exception(cls, 256, msg, 1024) else None
+        return r, exc
+
+    def bytes_(self, data: bytes):
+        return self.L.mock_byte_array(data, len(data))
+
+    def longs(self, vals):
+        arr = (self.C.c_int64 * max(len(vals), 1))(*vals)
+        return self.L.mock_long_array(arr, len(vals))
+
+    def read(self, arr) -> bytes:
+        n = self.L.mock_array_length(arr)
+        return self.C.string_at(self.L.mock_array_data(arr), n) if n > 0 else b""
+
+
+@pytest.mark.skipif(shutil.which("g++") is None, reason="no g++")
+def test_mock_jvm_exception_mapping_cpu():
+    """Runs the shim's create entry points without a GPU: DataStore.createStore's
+    IllegalArgumentException for an unknown matrix type (DataStore.java:91), a
+    RuntimeException for what the library does not support or cannot do (sparse-
+    column matrices; no HIP device here), GpuShardGroup's id-length check."""
+    import torch
+    jvm = MockJVM()
+    _, exc = jvm.call("nativeCreate", 7, 0, 1, 0, 1, 0, 0, 99, 4, 0, 0)  # data type 7
+    assert exc and exc[0] == "java/lang/IllegalArgumentException" and "Unrecognized" in exc[1]
+    _, exc = jvm.call("nativeCreate", 1, 0, 1, 0, 0, 0, 0, 99, 4, 0, 0)  # sparse-column matrix
+    assert exc and exc[0] == "java/lang/RuntimeException"
+    if not torch.cuda.is_available():
+        h, exc = jvm.call("nativeCreate", 1, 0, 1, 0, 1, 0, 0, 99, 4, 0, 0)
+        assert h == 0 and exc and exc[0] == "java/lang/RuntimeException" and "device" in exc[1]
+    short = jvm.bytes_(b"\0" * 64)
+    _, exc = jvm.call("nativeGroupCreate", short, 1, 0, 0, 1, 0, 1, 0, 1, 0, 100, 8, 1)
+    assert exc == ("java/lang/IllegalArgumentException", "unique id must be 128 bytes")
+    jvm.L.mock_free(short)
+    assert jvm.L.mock_calls() > 0
+
+
+@pytest.mark.gpu
+def test_mock_jvm_store_on_gpu(oracle):
+    """A FloatMatrixStore and an IntMatrixStore on cuda:0 driven only through the JNI
+    shim's entry points, as GpuDataStore.java calls them: readAll of the oracle's
+    writeAll bytes, byte[] pushes (PSAgent.handle, PSAgent.java:278-281), a push from
+    a pinned DirectByteBuffer (nativeHostAlloc + nativePushDirect), fetch by keys and
+    by range, writeAll; a key outside the shard (ArrayIndexOutOfBoundsException) and a
+    negative counter (IllegalStateException, IntMatrixStore.java:174-176) leave the
+    state the reference's store leaves. Then the native group at world 1 (unique id,
+    create, two full-range device pushes, flush, its store's writeAll). Every result
+    bytes-equal against the oracle."""
+    import ctypes as C
+
+    import numpy as np
+    import torch
+    from distml_amd import encode_matrix_push
+    jvm = MockJVM()
+    rng = np.random.default_rng(31)
+    rows, cols = 1000, 64
+    h, exc = jvm.call("nativeCreate", 1, 0, 1, 0, 1, 0, 0, rows - 1, cols, 0, 0)
+    assert exc is None and h
+    o = oracle.OracleStore(1, 0, 1, 0, rows - 1, cols)
+    o.synth_fill(3)
+    _, exc = jvm.call("nativeReadAll", h, jvm.bytes_(o.write_all()))
+    assert exc is None
+    n, _ = jvm.call("nativeShardBytes", h)
+    assert n == len(o.write_all())
+    for b in range(6):
+        keys = rng.permutation(rows)[: rows - 37 * b]
+        p = encode_matrix_push(keys, (rng.standard_normal((len(keys), cols)) * 0.01).astype(np.float32), 0, 1)
+        _, exc = jvm.call("nativePush", h, jvm.bytes_(p))
+        assert exc is None and o.push(p) == 0
+    # a push the NIO channel read straight into pinned memory
+    keys = rng.permutation(rows)[:300]
+    p = encode_matrix_push(keys, (rng.standard_normal((300, cols)) * 0.01).astype(np.float32), 0, 1)
+    buf, exc = jvm.call("nativeHostAlloc", len(p) + 64)
+    assert exc is None and jvm.L.mock_direct_capacity(buf) == len(p) + 64
+    C.memmove(jvm.L.mock_direct_address(buf) + 64, p, len(p))
+    _, exc = jvm.call("nativePushDirect", h, buf, 64, len(p))
+    assert exc is None and o.push(p) == 0
+    jvm.call("nativeHostFree", buf)
+    wa, exc = jvm.call("nativeWriteAll", h)
+    assert exc is None and jvm.read(wa) == o.write_all()
+    ks = [5, 999, 0, 500, 42]
+    fa, exc = jvm.call("nativeFetch", h, jvm.longs(ks))
+    assert exc is None and jvm.read(fa) == o.fetch(ks)
+    fr, exc = jvm.call("nativeFetchRange", h, 10, 20)
+    assert exc is None and jvm.read(fr) == o.fetch(list(range(10, 21)))
+    # a key outside the shard: the adds before it stay, the store refuses later pushes
+    keys = np.array([3, 4, rows + 5, 6])
+    p = encode_matrix_push(keys, np.ones((4, cols), np.float32), 0, 1)
+    _, exc = jvm.call("nativePush", h, jvm.bytes_(p))
+    assert exc and exc[0] == "java/lang/ArrayIndexOutOfBoundsException"
+    assert o.push(p) != 0
+    wa, _ = jvm.call("nativeWriteAll", h)
+    assert jvm.read(wa) == o.write_all()
+    jvm.call("nativeDestroy", h)
+
+    # IntMatrixStore: a counter below zero throws after the add (the add stays)
+    hi, exc = jvm.call("nativeCreate", 1, 0, 0, 0, 1, 0, 0, 99, 8, 0, 0)
+    assert exc is None
+    oi = oracle.OracleStore(1, 0, 0, 0, 99, 8)
+    oi.synth_fill(4)
+    jvm.call("nativeReadAll", hi, jvm.bytes_(oi.write_all()))
+    vals = rng.integers(-2, 3, size=(100, 8)).astype(np.int32)
+    vals[37, 5] = -1000
+    p = encode_matrix_push(rng.permutation(100), vals, 0, 0)
+    _, exc = jvm.call("nativePush", hi, jvm.bytes_(p))
+    assert exc and exc[0] == "java/lang/IllegalStateException"
+    assert oi.push(p) != 0
+    wa, _ = jvm.call("nativeWriteAll", hi)
+    assert jvm.read(wa) == oi.write_all()
+    jvm.call("nativeDestroy", hi)
+
+    # GpuShardGroup at world 1: device-resident full-range int32 pushes (exact)
+    uid, exc = jvm.call("nativeUniqueId")
+    assert exc is None and jvm.L.mock_array_length(uid) == 128
+    g, exc = jvm.call("nativeGroupCreate", uid, 1, 0, 0, 1, 0, 0, 0, 1, 0, rows, cols, 1)
+    assert exc is None and g
+    og = oracle.OracleStore(1, 0, 0, 0, rows - 1, cols)
+    dev = []
+    for b in range(4):
+        p = encode_matrix_push(rng.permutation(rows), rng.integers(0, 3, size=(rows, cols)).astype(np.int32), 0, 0)
+        assert og.push(p) == 0
+        dev.append(torch.frombuffer(bytearray(p), dtype=torch.uint8).cuda())
+    torch.cuda.synchronize()
+    for pair in (dev[:2], dev[2:]):
+        _, exc = jvm.call("nativeGroupPush", g, jvm.longs([t.data_ptr() for t in pair]),
+                          jvm.longs([t.numel() for t in pair]), 0)
+        assert exc is None
+    _, exc = jvm.call("nativeGroupFlush", g)
+    assert exc is None
+    st, exc = jvm.call("nativeGroupStore", g)
+    assert exc is None and st
+    wa, _ = jvm.call("nativeWriteAll", st)
+    assert jvm.read(wa) == og.write_all()
+    jvm.call("nativeGroupDestroy", g)
