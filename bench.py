@@ -619,6 +619,9 @@ def sparse_leg(ctx: Ctx, L, steps: int, cpu: bool):
                            "launches": k_n,
                            "note": "random 4-B RMW into a 4 GB array: line-granular (64-B read / 32-B write "
                                    "sectors), so counted traffic is ~3.9x the algorithmic bytes (DESIGN.md §4)"}
+        tr = out["roofline"].get("traffic")
+        if tr:  # the effective (counted-bytes) rate beside the algorithmic one
+            out["roofline"]["effective_GBps"] = round(tr / k_s / 1e9, 1)
     store.close()
     del bufs
     torch.cuda.empty_cache()
