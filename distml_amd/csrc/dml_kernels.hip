@@ -1466,16 +1466,19 @@ static hipError_t launch_flat_t(void* shard, int64_t rows, int32_t cols, const B
     return hipGetLastError();
 }
 
-// JMAX 8 vectors per lane (R = 10 rows at 200 columns), one push per round:
-// measured within 2 % of 4 x 1, 4 x 2, 8 x 2 and 4 x 4 (config 4, ascending
-// and permuted), and of occupancy caps at 1-3 blocks per CU (all slower);
-// nt record loads 2-3 % faster than cached ones.
+// One push per round: JMAX 8 (R = 10 rows at 200 columns) measured within 2 % of
+// 4 x 1, 4 x 2, 8 x 2 and 4 x 4 (config 4, ascending and permuted), and of
+// occupancy caps at 1-3 blocks per CU (all slower); nt record loads 2-3 % faster
+// than cached ones; JMAX 12 (below) beat 8 on permuted pushes.
 template <typename T, int MODE>
 static hipError_t launch_flat(void* shard, int64_t rows, int32_t cols, const Batch& bt, int nb, int64_t stride, int K,
                               const int32_t* slot, const uint32_t* rowflag, Ctrl* ctrl, uint64_t tail_cut,
                               hipStream_t st, int64_t* nblocks_out, LaunchEv ev, RowMap rm) {
-    return launch_flat_t<T, MODE, 8, 1>(shard, rows, cols, bt, nb, stride, K, slot, rowflag, ctrl, tail_cut, st,
-                                        nblocks_out, ev, rm);
+    // JMAX 12: config 4's 800-B rows as 15 rows per wave (750 of 768 vector slots);
+    // permuted pushes 4 775-4 801 -> 4 905-4 925 GiB/s against JMAX 8 (10 rows),
+    // ascending equal, JMAX 16 in between (same box, 2 rounds)
+    return launch_flat_t<T, MODE, 12, 1>(shard, rows, cols, bt, nb, stride, K, slot, rowflag, ctrl, tail_cut, st,
+                                         nblocks_out, ev, rm);
 }
 
 // The flat narrow-row kernels apply to plain sums (and AdaGrad chunks of at most 4
