@@ -2005,3 +2005,48 @@ def test_sampled_timing_and_write_through_rows(oracle, vt):
     assert n == calls // 4 and ms > 0.0
     assert "k_reduce_rows" in s.kernel_name() and s.kernel_name().endswith(", 2>")
     assert kat.bits_equal(s.values(), o.data)
+
+
+@pytest.mark.parametrize("vt,cols", [(1, 4), (1, 8), (1, 100), (1, 200), (1, 700), (1, 1020), (3, 2), (3, 250), (3, 510)])
+def test_flat_kernel_widths_exact(oracle, vt, cols):
+    """k_reduce_flat's row packing (R = min(16, JMAX * 64 / vectors per row) rows per
+    wave, JMAX = 12) at widths from one vector to just under 4 KiB, on a row count
+    that no R divides: host batches of dense pushes (ascending, permuted, half the
+    rows, one push listing a row twice -> the exact replay) and device calls of
+    full-range pushes (identity speculation, slot reuse on the second pair of
+    calls). Bytes-equal against the oracle."""
+    from distml_amd import DataDesc, encode_matrix_push
+    from distml_amd.store import DeviceBatch
+    rng = np.random.default_rng(1000 + cols)
+    rows = 1237
+    fmt = DataDesc(1, 0, vt)
+    dt = np.float32 if vt == 1 else np.float64
+    s, _ = mk_store(fmt, 0, rows - 1, cols)
+    o = oracle_store(oracle, fmt, 0, rows - 1, cols)
+    s.synth_fill(21)
+    o.synth_fill(21)
+    pushes = []
+    for b in range(5):
+        keys = np.arange(rows) if b == 0 else rng.permutation(rows)[: rows if b < 3 else rows // 2 + 40 * b]
+        if b == 4:
+            keys = keys.copy()
+            keys[5] = keys[100]  # one push lists a row twice
+        pushes.append(encode_matrix_push(keys, rng.standard_normal((len(keys), cols)).astype(dt), 0, vt))
+    s.handlePushBatch(fmt, pushes)
+    for p in pushes:
+        assert o.push(p) == 0
+    assert kat.bits_equal(s.values(), o.data)
+    # device calls of full-range pushes: ascending + a fixed permutation, twice, so the
+    # third and fourth calls find the permutation kept by the workspace ring
+    perm = rng.permutation(rows)
+    host = [encode_matrix_push(np.arange(rows) if j % 2 == 0 else perm,
+                               rng.standard_normal((rows, cols)).astype(dt), 0, vt) for j in range(8)]
+    dev = [torch.frombuffer(bytearray(h), dtype=torch.uint8).cuda() for h in host]
+    torch.cuda.synchronize()
+    for c in range(4):
+        pair = dev[2 * c: 2 * c + 2]
+        s.pushDevice(DeviceBatch([t.data_ptr() for t in pair], [t.numel() for t in pair]))
+        for h in host[2 * c: 2 * c + 2]:
+            assert o.push(h) == 0
+    s.flush()
+    assert kat.bits_equal(s.values(), o.data)
