@@ -1,5 +1,6 @@
+# Two A/B runs in one call: nt shard-row loads in k_reduce_rows (config 2 line) and in
+# k_reduce_flat (config 4 shards).
 set -e
 export TMPDIR=/tmp; mkdir -p gpurun_out
-timeout -k 10 400 python -u -m pytest tests/test_gpu_parity.py -v --timeout 200 --timeout-method thread -p no:cacheprovider -k "flat_kernel_widths" > gpurun_out/flatw.log 2>&1 || { tail -30 gpurun_out/flatw.log; exit 1; }
-tail -1 gpurun_out/flatw.log
-V=prent bash scripts/gpu_ab_group4.sh
+VARIANTS="rowsnt" bash scripts/gpu_ab_order.sh
+VARIANTS="flatnt" CONFIGS="4 4-perm" bash scripts/gpu_ab_cfg.sh
