@@ -657,8 +657,15 @@ __global__ __launch_bounds__(256) void k_sp_l2_fast(const SpPlan pl, const uint3
     __shared__ Stage st;
     constexpr int kRowShift = CMP ? 38 : 32;  // the record's row (within its level-1 bin if CMP)
     const int tid = threadIdx.x;
-    const int bin = (int)(blockIdx.x / pl.tiles2_per_bin);
-    const int64_t t = blockIdx.x - (int64_t)bin * pl.tiles2_per_bin;
+    // Every tile of a level-1 bin runs on one XCD (blocks b and b + 8 share one; the
+    // grid is padded to a multiple of 8 bins): the runs that neighbouring tiles write
+    // into one leaf region meet in that XCD's L2 instead of leaving partial lines in
+    // two. Config-3 step 1.406-1.409 -> 1.369-1.372 ms against bin-major tiles (same
+    // box, 3 rounds).
+    const int64_t s8 = blockIdx.x / 8u;
+    const int bin = (int)(blockIdx.x % 8u) + 8 * (int)(s8 / pl.tiles2_per_bin);
+    const int64_t t = s8 % pl.tiles2_per_bin;
+    if (bin >= pl.nbins1) return;
     const int64_t nbin = min((int64_t)cur1[bin], pl.cap1);
     const int64_t lo = t * kSpTile;
     if (lo >= nbin) return;
@@ -898,7 +905,7 @@ static hipError_t partition_fast_t(const Batch& bt, const SpPlan& pl, const SpLa
     if (e == hipSuccess) e = hipMemsetAsync(stat, 0, sizeof(SpStat), st);
     if (e != hipSuccess) return e;
     if (pl.ntiles1 > 0) {
-        const dim3 g1((unsigned)pl.ntiles1), g2((unsigned)(pl.nbins1 * pl.tiles2_per_bin));
+        const dim3 g1((unsigned)pl.ntiles1), g2((unsigned)((pl.nbins1 + 7) / 8 * 8 * pl.tiles2_per_bin));
         uint64_t* c1 = (uint64_t*)(ws + l.comp1);
         uint64_t* c2 = (uint64_t*)(ws + l.comp2);
         if constexpr (sizeof(T) == 4) {
