@@ -299,16 +299,35 @@ def _pre_time(L, every: int, reset: bool):
 DEVICE_SOURCES = ("dml_device.h", "dml_internal.h", "dml_kernels.hip", "dml_sparse.hip", "dml_split.hip")
 
 
-def device_src_hash() -> str:
-    """sha256 (16 hex digits) of the device-code sources; scripts/gpu_prof.sh records it
-    with every profile, and a stored traffic figure counts only while it still matches."""
+# the sources each profiled kernel is built from: the dense reduce kernels
+# (dml_kernels.hip) and the sparse partition / leaf kernels (dml_sparse.hip)
+KERNEL_SOURCES = {"dense": ("dml_device.h", "dml_internal.h", "dml_kernels.hip"),
+                  "sparse": ("dml_device.h", "dml_internal.h", "dml_sparse.hip")}
+TRAFFIC_GROUP = {"sparse": "sparse", "sparse_l1": "sparse", "sparse_l2": "sparse"}  # others: dense
+
+
+def device_src_hash(files=DEVICE_SOURCES, read=None) -> str:
+    """sha256 (16 hex digits) of device-code sources (all of them by default);
+    scripts/gpu_prof.sh records it with every profile, and a stored traffic figure
+    counts only while the sources of its kernel still match. `read(f)` returns a
+    file's bytes (default: the working tree)."""
     import hashlib
     h = hashlib.sha256()
-    for f in DEVICE_SOURCES:
+    for f in files:
         h.update(f.encode())
-        with open(os.path.join(ROOT, "distml_amd", "csrc", f), "rb") as fh:
-            h.update(fh.read())
+        if read is not None:
+            h.update(read(f))
+        else:
+            with open(os.path.join(ROOT, "distml_amd", "csrc", f), "rb") as fh:
+                h.update(fh.read())
     return h.hexdigest()[:16]
+
+
+def device_src_hashes(read=None) -> dict:
+    """device_src_hash of every kernel group (KERNEL_SOURCES) and of all sources."""
+    out = {g: device_src_hash(fs, read) for g, fs in KERNEL_SOURCES.items()}
+    out["all"] = device_src_hash(DEVICE_SOURCES, read)
+    return out
 
 
 def _kernel_sig(name: str) -> str:
@@ -332,11 +351,14 @@ def traffic_for(key: str, kernel_ran: str) -> dict:
     prof = _kernel_sig(e.get("kernel", ""))
     if prof != kernel_ran:
         return {"traffic": None, "traffic_stale": f"profiled {prof or '?'}, ran {kernel_ran or '?'}"}
-    if e.get("src_sha") != device_src_hash():
-        return {"traffic": None, "traffic_stale": f"device sources {device_src_hash()} differ from the profiled "
-                                                  f"{e.get('src_sha')}"}
+    group = TRAFFIC_GROUP.get(key, "dense")
+    by = e.get("src_sha_by_group") or {}
+    want, have = (by.get(group), device_src_hash(KERNEL_SOURCES[group])) if by.get(group) else \
+        (e.get("src_sha"), device_src_hash())
+    if want != have:
+        return {"traffic": None, "traffic_stale": f"device sources {have} differ from the profiled {want}"}
     return {"traffic": e["hbm_bytes_per_launch"],
-            "traffic_source": f"{e.get('source', '?')}; commit {e.get('commit', '?')}; src {e['src_sha']}"}
+            "traffic_source": f"{e.get('source', '?')}; commit {e.get('commit', '?')}; {group} sources {have}"}
 
 
 def prereduce_roofline(L, ctx, pieces, pre_ms, pre_n, pre_bytes, label):

@@ -12,7 +12,7 @@ T=${TAG:?TAG required}
 A=${ARGS:-}
 O=$PWD/gpurun_out
 # the device sources these counters stand for (bench.py's traffic_for checks it)
-python3 -c "import bench; print(bench.device_src_hash())" > "$O/prof_${T}_src.txt"
+python3 -c "import bench, json; print(json.dumps(bench.device_src_hashes()))" > "$O/prof_${T}_src.txt"
 timeout -k 10 300 rocprofv3 --kernel-trace --stats -d "$O/prof_${T}_stats" -o run --output-format csv -- python3 bench.py $A > "$O/prof_${T}_stats.log" 2>&1
 timeout -s KILL 240 rocprofv3 --pmc FETCH_SIZE -d "$O/prof_${T}_fetch" -o run --output-format csv -- python3 bench.py $A > "$O/prof_${T}_fetch.log" 2>&1
 timeout -s KILL 240 rocprofv3 --pmc WRITE_SIZE -d "$O/prof_${T}_write" -o run --output-format csv -- python3 bench.py $A > "$O/prof_${T}_write.log" 2>&1

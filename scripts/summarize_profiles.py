@@ -48,7 +48,11 @@ def main(rnd, tag, cmd, *specs):
     pj = os.path.join(PROF, "pmc_traffic.json")
     d = json.load(open(pj)) if os.path.exists(pj) else {}
     d = {"per_config": d.get("per_config", {})}
-    src_sha = open(os.path.join(OUT, f"prof_{tag}_src.txt")).read().strip()
+    src_txt = open(os.path.join(OUT, f"prof_{tag}_src.txt")).read().strip()
+    # gpu_prof.sh writes bench.device_src_hashes() (per kernel group + "all"); older
+    # runs wrote the one all-sources hash
+    by_group = json.loads(src_txt) if src_txt.startswith("{") else {}
+    src_sha = by_group.pop("all", src_txt) if by_group else src_txt
     try:
         commit = subprocess.run(["git", "-C", ROOT, "rev-parse", "--short", "HEAD"], capture_output=True,
                                 text=True, check=True).stdout.strip()
@@ -84,6 +88,8 @@ def main(rnd, tag, cmd, *specs):
                  "rocprof_avg_ns": avg_ns, "achieved_algorithmic_GBps": round(algo / avg_ns, 1),
                  "source": f"profiles/{rnd}_{tag}_kernel_stats.csv + FETCH_SIZE/WRITE_SIZE passes ({cmd})",
                  "src_sha": src_sha, "commit": commit}
+        if by_group:
+            entry["src_sha_by_group"] = by_group
         d["per_config"][key] = entry
         md += ["", f"## {key}: `{kpart}` ({nf}/{nw} dispatches sampled)", "",
                (f"- FETCH_SIZE {fetch_kib:.0f} KiB x 1024 x 2 = {read_b/1e9:.4f} GB read (gfx950 wide-read correction)"
