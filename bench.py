@@ -441,9 +441,10 @@ def headline(ctx: Ctx, L, args, out_line: dict):
         algo_per_rank = W * BUCKET + 2 * group.shard.size() * COLS * 4
 
     timing = not args.no_timing
-    # one chunk in 16 carries start/stop events: events in every dispatch lengthen the
-    # boundary between two reduces
-    timed_store.set_timing(timing and not sharded, every=16)
+    # one chunk in 4 carries start/stop events (>= 5 launches averaged over the default
+    # 20 steps): events in every dispatch lengthen the boundary between two reduces
+    # 
+    timed_store.set_timing(timing and not sharded, every=4)
     t0 = time.perf_counter()
     for _ in range(args.warmup):
         step()
@@ -456,7 +457,7 @@ def headline(ctx: Ctx, L, args, out_line: dict):
         else:
             group.prereduce_stats(reset=True)
         if sharded and timing:
-            _pre_time(L, every=16, reset=True)
+            _pre_time(L, every=4, reset=True)
 
     el = timed_steps(ctx, step, finish, args.steps, 0, ramp_s=max(0.0, 0.3 - (time.perf_counter() - t0)),
                      reset=reset)

@@ -17,6 +17,8 @@
 #include "dml_internal.h"
 
 #include <algorithm>
+#include <cmath>
+#include <limits>
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
@@ -45,6 +47,99 @@ int dml::set_error(int code, const std::string& msg) { return set_err(code, msg)
     } while (0)
 
 namespace {
+
+// java.util.Random as its specification defines it: 48-bit LCG (multiplier
+// 0x5DEECE66D, addend 0xB), setSeed's scramble, nextDouble from 26 + 27 bits, and
+// nextGaussian by the polar method with StrictMath.log (fdlibm's e_log.c, below)
+// and StrictMath.sqrt (IEEE). Used by dml_store_rand for DoubleMatrixStore.rand().
+struct JavaRandom {
+    uint64_t x;
+    bool have = false;
+    double spare = 0.0;
+    explicit JavaRandom(int64_t seed) : x(((uint64_t)seed ^ 0x5DEECE66DULL) & kMask) {}
+    static constexpr uint64_t kMask = (1ULL << 48) - 1;
+    int32_t next(int bits) {
+        x = (x * 0x5DEECE66DULL + 0xBULL) & kMask;
+        return (int32_t)(uint32_t)(x >> (48 - bits));
+    }
+    double next_double() {
+        const int64_t hi = next(26);
+        return (double)((hi << 27) + next(27)) * 0x1.0p-53;
+    }
+    static double strict_log(double v);
+    double next_gaussian() {
+        if (have) {
+            have = false;
+            return spare;
+        }
+        double a, b, q;
+        do {
+            a = 2 * next_double() - 1;
+            b = 2 * next_double() - 1;
+            q = a * a + b * b;
+        } while (q >= 1 || q == 0);
+        const double m = std::sqrt(-2 * strict_log(q) / q);
+        spare = b * m;
+        have = true;
+        return a * m;
+    }
+};
+
+// fdlibm __ieee754_log: reduce to x = 2^k (1 + f) with sqrt(2)/2 < 1 + f < sqrt(2),
+// then log(1 + f) = f - f^2/2 + s (f^2/2 + R(s^2)), s = f / (2 + f), R a degree-14
+// minimax polynomial in s (its published coefficients Lg1..Lg7).
+double JavaRandom::strict_log(double v) {
+    constexpr double ln2_hi = 6.93147180369123816490e-01, ln2_lo = 1.90821492927058770002e-10,
+                     two54 = 1.80143985094819840000e+16;
+    constexpr double L1 = 6.666666666666735130e-01, L2 = 3.999999999940941908e-01, L3 = 2.857142874366239149e-01,
+                     L4 = 2.222219843214978396e-01, L5 = 1.818357216161805012e-01, L6 = 1.531383769920937332e-01,
+                     L7 = 1.479819860511658591e-01;
+    uint64_t u;
+    memcpy(&u, &v, 8);
+    int32_t hx = (int32_t)(u >> 32), k = 0;
+    if (hx < 0x00100000) {
+        if (((hx & 0x7fffffff) | (int32_t)(uint32_t)u) == 0) return -std::numeric_limits<double>::infinity();
+        if (hx < 0) return std::numeric_limits<double>::quiet_NaN();
+        k = -54;
+        v *= two54;
+        memcpy(&u, &v, 8);
+        hx = (int32_t)(u >> 32);
+    }
+    if (hx >= 0x7ff00000) return v + v;
+    k += (hx >> 20) - 1023;
+    hx &= 0x000fffff;
+    const int32_t i0 = (hx + 0x95f64) & 0x100000;
+    u = ((uint64_t)(uint32_t)(hx | (i0 ^ 0x3ff00000)) << 32) | (u & 0xffffffffULL);
+    memcpy(&v, &u, 8);
+    k += i0 >> 20;
+    const double f = v - 1.0, dk = (double)k;
+    if ((0x000fffff & (2 + hx)) < 3) {
+        if (f == 0.0) return k == 0 ? 0.0 : dk * ln2_hi + dk * ln2_lo;
+        const double R = f * f * (0.5 - 0.33333333333333333 * f);
+        return k == 0 ? f - R : dk * ln2_hi - ((R - dk * ln2_lo) - f);
+    }
+    const double s = f / (2.0 + f), z = s * s, w = z * z;
+    const double t1 = w * (L2 + w * (L4 + w * L6));
+    const double t2 = z * (L1 + w * (L3 + w * (L5 + w * L7)));
+    const double R = t2 + t1;
+    if (((hx - 0x6147a) | (0x6b851 - hx)) > 0) {
+        const double hfsq = 0.5 * f * f;
+        return k == 0 ? f - (hfsq - s * (hfsq + R)) : dk * ln2_hi - ((hfsq - (s * (hfsq + R) + dk * ln2_lo)) - f);
+    }
+    return k == 0 ? f - s * (f - R) : dk * ln2_hi - ((s * (f - R) - dk * ln2_lo) - f);
+}
+
+// One row of DoubleMatrixStore.rand() (DoubleMatrixStore.java:196-206).
+void java_unit_abs_gaussian_row(JavaRandom& jr, double* row, int64_t cols) {
+    double sum = 0.0;
+    for (int64_t j = 0; j < cols; ++j) {
+        row[j] = std::fabs(jr.next_gaussian());
+        sum += row[j] * row[j];
+    }
+    sum = std::sqrt(sum);
+    for (int64_t j = 0; j < cols; ++j) row[j] = row[j] / sum;
+}
+
 
 struct DeviceGuard {
     int prev = -1;
@@ -2255,6 +2350,21 @@ int dml_store_rand(dml_store* s, uint64_t seed) {
     if (int rc = begin_call(s)) return rc;
     const int vt = vtype_of(s->desc);
     if (!s->is_matrix || vt == kI32) return DML_OK;  // DataStore.rand(): no-op (DataStore.java:22)
+    if (vt == kF64) {
+        // DoubleMatrixStore.rand() seeds Random(1L) on every shard: reproduced exactly,
+        // on the host (init, not the push path), a block of rows at a time
+        const int64_t cols = s->cols, rb = std::max<int64_t>(1, (int64_t(1) << 21) / cols);
+        JavaRandom jr(1);
+        std::vector<double> blk((size_t)(std::min(rb, s->rows) * cols));
+        for (int64_t r0 = 0; r0 < s->rows; r0 += rb) {
+            const int64_t nr = std::min(rb, s->rows - r0);
+            for (int64_t i = 0; i < nr; ++i) java_unit_abs_gaussian_row(jr, blk.data() + i * cols, cols);
+            HIPCHK(hipMemcpyAsync((double*)s->data + r0 * cols, blk.data(), (size_t)(nr * cols) * 8,
+                                  hipMemcpyHostToDevice, s->stream));
+            HIPCHK(hipStreamSynchronize(s->stream));
+        }
+        return DML_OK;
+    }
     HIPCHK(launch_rand(vt, s->data, s->rows, s->cols, splitmix64(seed ^ 0x5241'4e44ull), s->stream));
     HIPCHK(hipStreamSynchronize(s->stream));
     return DML_OK;

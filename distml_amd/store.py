@@ -68,6 +68,43 @@ def check(rc: int, store: Optional["DataStore"] = None):
     raise _EXC.get(rc, NativeError)(_lib.last_error() or f"distml_ps status {rc}", rc, key, col)
 
 
+def java_parse_float(text: str) -> float:
+    """Float.parseFloat: the decimal (or hex) string rounded ONCE to the nearest
+    float32, ties to even — not through a double, whose second rounding can differ.
+    Leading/trailing whitespace and a trailing f/F/d/D are accepted, like Java's."""
+    from fractions import Fraction
+    t = text.strip(" \t\n\r\x0b\x0c\x00")
+    if t[-1:] in ("f", "F", "d", "D") and not t.lower().endswith(("infinity", "nan")):
+        t = t[:-1]
+    body = t.lstrip("+-")
+    neg = t.startswith("-")
+    if body in ("NaN", "Infinity"):
+        v = float("nan") if body == "NaN" else float("inf")
+        return -v if neg else v
+    if body.lower().startswith("0x"):
+        exact = Fraction(float.fromhex(t)) if "p" in body.lower() else None
+        if exact is None:
+            raise ValueError(f"NumberFormatException: {text!r}")
+    else:
+        if not body or body.lower() in ("inf", "nan", "infinity") or "_" in body:
+            raise ValueError(f"NumberFormatException: {text!r}")
+        exact = Fraction(t)
+    with np.errstate(over="ignore"):
+        d = np.float32(float(exact))  # within one float32 ulp of the exact value
+    if not np.isfinite(d):
+        return float(d)
+    best = d
+    for c in (np.nextafter(d, np.float32(-np.inf)), np.nextafter(d, np.float32(np.inf))):
+        if not np.isfinite(c):
+            continue
+        e0, e1 = abs(Fraction(float(best)) - exact), abs(Fraction(float(c)) - exact)
+        if e1 < e0 or (e1 == e0 and int(c.view(np.uint32)) % 2 == 0):
+            best = c
+    if best == 0 and neg:
+        return -0.0
+    return float(best)
+
+
 class DataStore:
     """One shard of one matrix, resident in HBM (a `dml_store`)."""
 
@@ -135,11 +172,13 @@ class DataStore:
         return self._cols
 
     def rand(self, seed: int = 1):
-        """DataStore.rand (dml_store_rand): the reference's distributions, drawn from a
-        counter-based generator instead of java.util.Random — float matrices
-        (a/100f - 0.5f)/rowSize with a uniform in 0..99 (FloatMatrixStore.java:39-51,
-        FloatMatrixStoreAdaGrad.java:55-66), double matrices |N(0,1)| rows scaled to unit
-        norm (DoubleMatrixStore.java:192-207); the other stores keep DataStore's no-op."""
+        """DataStore.rand (dml_store_rand). DoubleMatrixStore: the reference's values
+        exactly (java.util.Random(1L) per shard, |nextGaussian()| rows scaled to unit
+        norm, DoubleMatrixStore.java:192-207; `seed` unused). Float matrices draw from an
+        unseeded Random in the reference (FloatMatrixStore.java:44), so here
+        (a/100f - 0.5f)/rowSize with a uniform in 0..99 from a generator seeded by
+        `seed` (FloatMatrixStore.java:39-51, FloatMatrixStoreAdaGrad.java:55-66); the
+        other stores keep DataStore's no-op (DataStore.java:22)."""
         check(_lib.load().dml_store_rand(self._h, seed), self)
 
     def synth_fill(self, seed: int = 7):
@@ -148,10 +187,19 @@ class DataStore:
         check(_lib.load().dml_synth_fill_store(self._h, seed), self)
 
     def zero(self):
-        check(_lib.load().dml_store_fill(self._h, 0.0), self)
+        """DataStore.zero(): a no-op on every store (DataStore.java:24). The float
+        stores' zero(String) is an overload that PSActor's OP_ZERO never calls
+        (FloatMatrixStore.java:57, PSActor.java:185-188). Use fill(0.0) to clear."""
 
     def set(self, value: str):
-        # FloatMatrixStore.set -> setValue(Float.parseFloat(value)) (:53-71)
+        """DataStore.set(String): FloatMatrixStore / FloatMatrixStoreAdaGrad fill every
+        value with Float.parseFloat(value) (FloatMatrixStore.java:53-55,61-71,
+        FloatMatrixStoreAdaGrad.java:69-71); a no-op on the other stores (DataStore.java:26)."""
+        if self.format.dataType == DataDesc.DATA_TYPE_MATRIX and self.format.valueType == DataDesc.ELEMENT_TYPE_FLOAT:
+            self.fill(java_parse_float(value))
+
+    def fill(self, value: float):
+        """Every value := value (dml_store_fill): test and tool access, not a reference API."""
         check(_lib.load().dml_store_fill(self._h, float(value)), self)
 
     @staticmethod

@@ -170,15 +170,21 @@ int dml_store_device_ptr(dml_store* s, void** dev_ptr);
 /* AdaGrad side arrays (FloatMatrixStoreAdaGrad.java:23-24), f32 row-major. */
 int dml_store_read_adagrad(dml_store* s, float* alpha_dst, float* delta_dst, int64_t elems);
 
-/* DataStore.rand() (DataStore.java:22; PSActor OP_RAND, PSActor.java:181-201):
- * the reference's distributions from a counter-based generator seeded by `seed`
- * (java.util.Random's stream is not reproduced): float matrices, AdaGrad
- * included, (a/100f - 0.5f)/rowSize with a uniform in 0..99 in float arithmetic
- * (FloatMatrixStore.java:39-51, FloatMatrixStoreAdaGrad.java:55-66); double
- * matrices |N(0,1)| per element, each row divided by its L2 norm
- * (DoubleMatrixStore.java:192-207); other stores: no-op (DataStore.java:22). */
+/* DataStore.rand() (DataStore.java:22; PSActor OP_RAND, PSActor.java:181-201).
+ * DoubleMatrixStore: exactly the reference's values — java.util.Random(1L) on every
+ * shard, |nextGaussian()| per element, each row divided by its L2 norm
+ * (DoubleMatrixStore.java:192-207); `seed` is not used. Float matrices, AdaGrad
+ * included, draw from an unseeded java.util.Random in the reference
+ * (FloatMatrixStore.java:44, FloatMatrixStoreAdaGrad.java:60), which nothing can
+ * reproduce: here (a/100f - 0.5f)/rowSize with a uniform a in 0..99, in float
+ * arithmetic, from a counter-based generator seeded by `seed`. Other stores: no-op. */
 int dml_store_rand(dml_store* s, uint64_t seed);
-/* set(String)/zero()/setValue (FloatMatrixStore.java:53-71): fill every value. */
+/* Fill every value with v: FloatMatrixStore.setValue (FloatMatrixStore.java:61-71), what
+ * set(String) does on the float matrix stores (:53-55, FloatMatrixStoreAdaGrad.java:69-71).
+ * The reference's zero() is a no-op on every store (DataStore.java:24; the float stores'
+ * zero(String) is an overload OP_ZERO never calls) and set() a no-op on the others: the
+ * DataStore mirrors (GpuDataStore.java, distml_amd/store.py) call this only where the
+ * reference's store would change. */
 int dml_store_fill(dml_store* s, double v);
 /* FloatMatrixStoreAdaGrad.setAlpha(initialAlpha, minAlpha, factor) (:77-82). */
 int dml_store_set_alpha(dml_store* s, float initial_alpha, float min_alpha, float factor);

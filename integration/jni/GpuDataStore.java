@@ -23,11 +23,14 @@ public class GpuDataStore extends DataStore {
     private final KeyRange localRows;
     private final int rowSize;
     private final int valueBytes;
+    private final boolean floatMatrix;  // FloatMatrixStore / FloatMatrixStoreAdaGrad: the stores set() acts on
 
     public GpuDataStore(DataDesc format, KeyRange keys, int cols, int device) {
         this.localRows = keys;
         this.rowSize = format.dataType == DataDesc.DATA_TYPE_MATRIX ? cols : 1;
         this.valueBytes = format.valueType == DataDesc.ELEMENT_TYPE_DOUBLE ? 8 : 4;
+        this.floatMatrix = format.dataType == DataDesc.DATA_TYPE_MATRIX
+                && format.valueType == DataDesc.ELEMENT_TYPE_FLOAT;
         this.handle = nativeCreate(format.dataType, format.keyType, format.valueType,
                 format.denseRow ? 1 : 0, format.denseColumn ? 1 : 0, format.adaGrad ? 1 : 0,
                 keys.firstKey, keys.lastKey, cols, device, 0);
@@ -36,12 +39,19 @@ public class GpuDataStore extends DataStore {
     public KeyCollection rows() { return localRows; }
     public int rowSize() { return rowSize; }
 
-    /** DataStore.rand() / PSActor OP_RAND (PSActor.java:181-201): FloatMatrixStore's
-     *  (nextInt(100)/100f - 0.5f)/rowSize (FloatMatrixStore.java:39-51), DoubleMatrixStore's
-     *  unit-norm |gaussian| rows (DoubleMatrixStore.java:192-207); a no-op for the others. */
+    /** DataStore.rand() / PSActor OP_RAND (PSActor.java:181-201): DoubleMatrixStore's
+     *  Random(1L) unit-norm |gaussian| rows, value for value (DoubleMatrixStore.java:192-207);
+     *  FloatMatrixStore's (nextInt(100)/100f - 0.5f)/rowSize from an unseeded generator
+     *  (FloatMatrixStore.java:39-51); a no-op for the others. */
     public void rand() { nativeRand(handle, System.nanoTime()); }
-    public void zero() { nativeFill(handle, 0.0); }
-    public void set(String value) { nativeFill(handle, Float.parseFloat(value)); }
+    /** DataStore.zero() is a no-op on every store (DataStore.java:24): the float stores'
+     *  zero(String) is an overload, so OP_ZERO (PSActor.java:185-188) changes nothing. */
+    public void zero() { }
+    /** set(String) fills only the float matrix stores (FloatMatrixStore.java:53-55,
+     *  FloatMatrixStoreAdaGrad.java:69-71); DataStore's default is a no-op (DataStore.java:26). */
+    public void set(String value) {
+        if (floatMatrix) nativeFill(handle, Float.parseFloat(value));
+    }
     public void setAlpha(float initialAlpha, float minAlpha, float factor) {
         nativeSetAlpha(handle, initialAlpha, minAlpha, factor);
     }

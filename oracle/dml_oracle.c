@@ -489,3 +489,145 @@ void orc_synth_fill(orc_store* s, uint64_t seed) {
         else ((int32_t*)s->data)[i] = 64 + (int32_t)(h % 51);
     }
 }
+
+/* ---- DoubleMatrixStore.rand() (DoubleMatrixStore.java:192-207) -----------
+ * new Random(1L) per shard; per row: cols x Math.abs(nextGaussian()), the sum of
+ * squares in double (row order, no FMA), Math.sqrt, then every element / sum.
+ * java.util.Random is the 48-bit LCG of its published specification (Random's
+ * class documentation: setSeed scramble, next(bits), nextDouble = 53 bits, and
+ * nextGaussian = Marsaglia's polar method with StrictMath.log / StrictMath.sqrt).
+ * StrictMath.log is fdlibm's __ieee754_log (e_log.c), restated below: glibc's log
+ * is closer to correctly rounded and differs from it in ~7 % of arguments. */
+typedef struct {
+    uint64_t seed;
+    int have_next;
+    double next_next;
+} jrandom;
+
+static void jr_init(jrandom* r, int64_t seed) {
+    r->seed = ((uint64_t)seed ^ 0x5DEECE66DULL) & ((1ULL << 48) - 1);
+    r->have_next = 0;
+    r->next_next = 0.0;
+}
+static int32_t jr_next(jrandom* r, int bits) {
+    r->seed = (r->seed * 0x5DEECE66DULL + 0xBULL) & ((1ULL << 48) - 1);
+    return (int32_t)(uint32_t)(r->seed >> (48 - bits));
+}
+static double jr_next_double(jrandom* r) {
+    const int64_t a = jr_next(r, 26), b = jr_next(r, 27);
+    return (double)((a << 27) + b) * 0x1.0p-53;
+}
+
+static inline int32_t hi_word(double x) { uint64_t u; memcpy(&u, &x, 8); return (int32_t)(u >> 32); }
+static inline uint32_t lo_word(double x) { uint64_t u; memcpy(&u, &x, 8); return (uint32_t)u; }
+static inline double with_hi(double x, int32_t h) {
+    uint64_t u; memcpy(&u, &x, 8);
+    u = ((uint64_t)(uint32_t)h << 32) | (u & 0xffffffffULL);
+    memcpy(&x, &u, 8);
+    return x;
+}
+
+double orc_fdlibm_log(double x) {
+    static const double ln2_hi = 6.93147180369123816490e-01, ln2_lo = 1.90821492927058770002e-10,
+                        two54 = 1.80143985094819840000e+16, Lg1 = 6.666666666666735130e-01,
+                        Lg2 = 3.999999999940941908e-01, Lg3 = 2.857142874366239149e-01,
+                        Lg4 = 2.222219843214978396e-01, Lg5 = 1.818357216161805012e-01,
+                        Lg6 = 1.531383769920937332e-01, Lg7 = 1.479819860511658591e-01;
+    volatile double zero = 0.0;
+    int32_t hx = hi_word(x), k = 0, i, j;
+    const uint32_t lx = lo_word(x);
+    if (hx < 0x00100000) { /* x < 2^-1022 */
+        if (((hx & 0x7fffffff) | (int32_t)lx) == 0) return -two54 / zero;
+        if (hx < 0) return (x - x) / zero;
+        k -= 54;
+        x *= two54;
+        hx = hi_word(x);
+    }
+    if (hx >= 0x7ff00000) return x + x;
+    k += (hx >> 20) - 1023;
+    hx &= 0x000fffff;
+    i = (hx + 0x95f64) & 0x100000;
+    x = with_hi(x, hx | (i ^ 0x3ff00000)); /* normalize x or x/2 */
+    k += (i >> 20);
+    const double f = x - 1.0;
+    double dk, R;
+    if ((0x000fffff & (2 + hx)) < 3) { /* |f| < 2^-20 */
+        if (f == 0.0) {
+            if (k == 0) return 0.0;
+            dk = (double)k;
+            return dk * ln2_hi + dk * ln2_lo;
+        }
+        R = f * f * (0.5 - 0.33333333333333333 * f);
+        if (k == 0) return f - R;
+        dk = (double)k;
+        return dk * ln2_hi - ((R - dk * ln2_lo) - f);
+    }
+    const double s = f / (2.0 + f);
+    dk = (double)k;
+    const double z = s * s;
+    i = hx - 0x6147a;
+    const double w = z * z;
+    j = 0x6b851 - hx;
+    const double t1 = w * (Lg2 + w * (Lg4 + w * Lg6));
+    const double t2 = z * (Lg1 + w * (Lg3 + w * (Lg5 + w * Lg7)));
+    i |= j;
+    R = t2 + t1;
+    if (i > 0) {
+        const double hfsq = 0.5 * f * f;
+        if (k == 0) return f - (hfsq - s * (hfsq + R));
+        return dk * ln2_hi - ((hfsq - (s * (hfsq + R) + dk * ln2_lo)) - f);
+    }
+    if (k == 0) return f - s * (f - R);
+    return dk * ln2_hi - ((s * (f - R) - dk * ln2_lo) - f);
+}
+
+static double jr_next_gaussian(jrandom* r) {
+    if (r->have_next) {
+        r->have_next = 0;
+        return r->next_next;
+    }
+    double v1, v2, s;
+    do {
+        v1 = 2 * jr_next_double(r) - 1;
+        v2 = 2 * jr_next_double(r) - 1;
+        s = v1 * v1 + v2 * v2;
+    } while (s >= 1 || s == 0);
+    const double multiplier = sqrt(-2 * orc_fdlibm_log(s) / s); /* StrictMath.sqrt: IEEE */
+    r->next_next = v2 * multiplier;
+    r->have_next = 1;
+    return v1 * multiplier;
+}
+
+void orc_java_random_ints(int64_t seed, int32_t n, int32_t* out) {
+    jrandom r;
+    jr_init(&r, seed);
+    for (int32_t i = 0; i < n; ++i) out[i] = jr_next(&r, 32);
+}
+
+void orc_java_random_gaussians(int64_t seed, int32_t n, double* out) {
+    jrandom r;
+    jr_init(&r, seed);
+    for (int32_t i = 0; i < n; ++i) out[i] = jr_next_gaussian(&r);
+}
+
+int orc_rand(orc_store* s) {
+    /* DataStore.rand() is a no-op (DataStore.java:22) except for the matrix stores;
+     * the float matrices draw from an unseeded Random (FloatMatrixStore.java:44), which
+     * no restatement can reproduce, so only DoubleMatrixStore is restated here. */
+    if (s->data_type != 1 || s->value_type != 3) return ORC_E_INVALID_ARG;
+    jrandom r;
+    jr_init(&r, 1);
+    double* d = (double*)s->data;
+    const int32_t cols = s->cols;
+    for (int64_t i = 0; i < s->rows; ++i) {
+        double* row = d + i * cols;
+        double sum = 0.0;
+        for (int32_t j = 0; j < cols; ++j) {
+            row[j] = fabs(jr_next_gaussian(&r));
+            sum += row[j] * row[j];
+        }
+        sum = sqrt(sum);
+        for (int32_t j = 0; j < cols; ++j) row[j] = row[j] / sum;
+    }
+    return ORC_OK;
+}

@@ -70,6 +70,15 @@ void orc_synth_sparse_bucket(uint8_t* out, int32_t key_type, int32_t value_type,
                              uint64_t perm_a, uint64_t perm_c);
 void orc_synth_fill(orc_store* s, uint64_t seed);
 
+/* DoubleMatrixStore.rand() (DoubleMatrixStore.java:192-207): java.util.Random(1L),
+ * |nextGaussian()| rows scaled to unit norm; ORC_E_INVALID_ARG for other stores.
+ * The pieces, for known-answer tests: Random(seed).nextInt() x n,
+ * Random(seed).nextGaussian() x n, and fdlibm's log (StrictMath.log). */
+int orc_rand(orc_store* s);
+void orc_java_random_ints(int64_t seed, int32_t n, int32_t* out);
+void orc_java_random_gaussians(int64_t seed, int32_t n, double* out);
+double orc_fdlibm_log(double x);
+
 /* Bench baseline: n sequential pushes, timed by the caller; optional threads>1
  * runs the dense matrix loop row-partitioned over OpenMP-free pthreads. */
 int orc_push_many(orc_store* s, const uint8_t* const* bufs, const int64_t* lens, int32_t n, int32_t threads);

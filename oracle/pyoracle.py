@@ -63,6 +63,12 @@ def lib():
         L.orc_synth_dense_bucket.argtypes = [vp, i32, i32, i64, i64, i64, i32, u64, u64, u64]
         L.orc_synth_sparse_bucket.argtypes = [vp, i32, i32, i32, i64, i64, i64, u64, u64, u64]
         L.orc_synth_fill.argtypes = [vp, u64]
+        L.orc_rand.restype = C.c_int
+        L.orc_rand.argtypes = [vp]
+        L.orc_java_random_ints.argtypes = [i64, i32, vp]
+        L.orc_java_random_gaussians.argtypes = [i64, i32, vp]
+        L.orc_fdlibm_log.restype = C.c_double
+        L.orc_fdlibm_log.argtypes = [C.c_double]
         _lib = L
     return _lib
 
@@ -152,6 +158,28 @@ class OracleStore:
 
     def synth_fill(self, seed):
         lib().orc_synth_fill(self._h, seed)
+
+    def rand(self) -> int:
+        """DoubleMatrixStore.rand() (DoubleMatrixStore.java:192-207), bit-exact."""
+        return lib().orc_rand(self._h)
+
+
+def java_random_ints(seed, n) -> np.ndarray:
+    """new java.util.Random(seed).nextInt() x n."""
+    out = np.empty(n, np.int32)
+    lib().orc_java_random_ints(seed, n, out.ctypes.data)
+    return out
+
+
+def java_random_gaussians(seed, n) -> np.ndarray:
+    """new java.util.Random(seed).nextGaussian() x n (StrictMath = fdlibm log)."""
+    out = np.empty(n, np.float64)
+    lib().orc_java_random_gaussians(seed, n, out.ctypes.data)
+    return out
+
+
+def fdlibm_log(x: float) -> float:
+    return lib().orc_fdlibm_log(x)
 
 
 def linear_split(first, last, n):

@@ -369,7 +369,7 @@ def test_write_all_read_all_round_trip(oracle):
         o.data[:] = init
         blob = s.writeAll()
         assert blob == o.write_all()
-        s.zero()
+        s.fill(0.0)
         assert not s.values().any()
         s.readAll(io.BytesIO(blob))
         assert kat.bits_equal(s.values(), init)
@@ -399,11 +399,11 @@ def test_large_fetch_checkpoint_bounce_and_pinned():
     assert pin.tobytes() == want
     be = vals.astype(">f4").tobytes()
     assert s.writeAll() == be
-    s.zero()
+    s.fill(0.0)
     s.readAll(io.BytesIO(be))
     assert kat.bits_equal(s.values(), vals)
     # pinned source for readAll-equivalent syncFrom of every row
-    s.zero()
+    s.fill(0.0)
     pin_be = pinned_empty(len(be))
     pin_be[:] = np.frombuffer(be, np.uint8)
     s.syncFrom(pin_be, 0, rows - 1)
@@ -971,7 +971,7 @@ def test_native_group_int32_negative_final_counter():
     fmt = DataDesc(1, 0, 0)
     g = NativeShardGroup(fmt, rows, cols, 0, 1, NativeShardGroup.unique_id(), device=0, pieces=4)
     try:
-        g.store.set("3")
+        g.store.fill(3)
         vals = np.zeros((rows, cols), np.int32)
         vals[40, 5] = -4   # final 3 - 4 = -1: the first negative in row-major order
         vals[41, 0] = -9
@@ -1487,12 +1487,16 @@ def test_pinned_push_matches_oracle(oracle, async_push):
         st.close()
 
 
-def test_rand_reference_distributions():
-    """DataStore.rand (dml_store_rand): FloatMatrixStore's (nextInt(100)/100f - 0.5f)
-    / rowSize values (FloatMatrixStore.java:39-51; AdaGrad :55-66) — every value one of
-    the 100 float results, each a near-uniform share; DoubleMatrixStore's |gaussian|
-    rows of unit norm (DoubleMatrixStore.java:192-207); int / array stores unchanged
-    (DataStore.rand is a no-op, DataStore.java:22). Seeded: same seed, same values."""
+def test_rand_reference_distributions(oracle):
+    """DataStore.rand (dml_store_rand). DoubleMatrixStore: bit-exact against the
+    oracle's restatement of DoubleMatrixStore.java:192-207 (java.util.Random(1L) per
+    shard, fdlibm log in nextGaussian, |g| rows divided by their norm; the oracle's
+    Random is pinned by Java's published outputs, tests/test_oracle_kat.py), on two
+    shards of one matrix (both start from Random(1L)). FloatMatrixStore's
+    (nextInt(100)/100f - 0.5f) / rowSize values (FloatMatrixStore.java:39-51; AdaGrad
+    :55-66) come from an unseeded Random there: every value one of the 100 float
+    results, each a near-uniform share, same seed same values. int / array stores
+    unchanged (DataStore.rand is a no-op, DataStore.java:22)."""
     from distml_amd import DataDesc, DataStore, KeyRange
     rows, cols = 2000, 50
     allowed = {((np.float32(a) / np.float32(100.0)) - np.float32(0.5)) / np.float32(cols) for a in range(100)}
@@ -1508,17 +1512,40 @@ def test_rand_reference_distributions():
         assert cnt.min() > 0.8 * v.size / 100 and cnt.max() < 1.2 * v.size / 100
         st.close()
         st2.close()
-    st = DataStore(DataDesc(1, 1, 3), KeyRange(0, rows - 1), 10)
-    st.rand(9)
-    v = st.values()
-    assert np.all(v >= 0)
-    assert np.allclose(np.sqrt((v * v).sum(axis=1)), 1.0, rtol=1e-12)
-    assert 0.2 < np.median(v) < 0.3  # median of |N(0,1)| / sqrt(10 E[g^2]) ~ 0.674 / 3.16
-    st.close()
+    # ragged shapes, a shard past 2^21 elements (the host generates blocks of rows)
+    for first, last, c in ((0, 999, 10), (1000, 1536, 10), (0, 2, 1), (5, 9000, 300)):
+        st = DataStore(DataDesc(1, 1, 3), KeyRange(first, last), c)
+        st.rand(9)
+        v = st.values()
+        o = oracle.OracleStore(1, 1, 3, first, last, c)
+        assert o.rand() == 0
+        assert v.tobytes() == o.data.tobytes(), (first, last, c)
+        assert np.all(v >= 0) and np.allclose(np.sqrt((v * v).sum(axis=1)), 1.0, rtol=1e-12)
+        st.close()
     for fmt, c in ((DataDesc(1, 0, 0), 7), (DataDesc(0, 1, 1), 1), (DataDesc(0, 0, 0), 1)):
         st = DataStore(fmt, KeyRange(0, 99), c)
         st.rand(1)
         assert not st.values().any()
+        st.close()
+
+
+def test_zero_set_reference_semantics():
+    """DataStore.zero() is a no-op on every store (DataStore.java:24; the float
+    stores' zero(String) is an overload OP_ZERO never calls, FloatMatrixStore.java:57);
+    set(String) fills the float matrix stores with Float.parseFloat
+    (FloatMatrixStore.java:53-55, FloatMatrixStoreAdaGrad.java:69-71) and is a no-op
+    on the others (DataStore.java:26)."""
+    from distml_amd import DataDesc, DataStore, KeyRange
+    for fmt, c in ((DataDesc(1, 0, 1), 5), (DataDesc(1, 0, 1, False, True, True), 5), (DataDesc(1, 0, 0), 5),
+                   (DataDesc(1, 1, 3), 5), (DataDesc(0, 1, 1), 1), (DataDesc(0, 0, 3), 1), (DataDesc(0, 0, 0), 1)):
+        st = DataStore(fmt, KeyRange(0, 63), c)
+        st.fill(2)
+        st.zero()
+        assert np.all(st.values() == 2), fmt
+        st.set("0.1")
+        floatm = fmt.dataType == 1 and fmt.valueType == 1
+        want = np.float32(0.1) if floatm else 2
+        assert np.all(st.values() == want), fmt
         st.close()
 
 

@@ -5,6 +5,8 @@ numpy restatement plus literal hand-computed values. Parity of the oracle
 with the Java reference itself is UNPINNED (no JDK, no reference fixtures);
 see DESIGN.md §Oracle.
 """
+import math
+
 import numpy as np
 import pytest
 
@@ -94,3 +96,63 @@ def test_oracle_push_many_threads_matches_sequential(oracle):
     assert s1.push_many(bufs, threads=1) == 0
     assert s4.push_many(bufs, threads=4) == 0
     assert kat.bits_equal(s1.data, s4.data)
+
+
+def test_java_random_known_answers(oracle):
+    """java.util.Random restated for DoubleMatrixStore.rand (DoubleMatrixStore.java:
+    192-207), pinned by outputs the JDK prints for these seeds (widely published:
+    new Random(42).nextInt() = -1170105035; nextGaussian() of seeds 42 / 0 / 1 =
+    1.1419053154730547 / 0.8025330637390305 / 1.561581040188955). The gaussians go
+    through the polar method's StrictMath.log, so they also pin the fdlibm log."""
+    assert int(oracle.java_random_ints(42, 1)[0]) == -1170105035
+    assert repr(float(oracle.java_random_gaussians(42, 1)[0])) == "1.1419053154730547"
+    assert repr(float(oracle.java_random_gaussians(0, 1)[0])) == "0.8025330637390305"
+    assert repr(float(oracle.java_random_gaussians(1, 1)[0])) == "1.561581040188955"
+    # the second gaussian of a pair is the cached nextNextGaussian
+    g = oracle.java_random_gaussians(1, 4)
+    assert len(set(g.tolist())) == 4
+
+
+def test_fdlibm_log(oracle):
+    """StrictMath.log = fdlibm's __ieee754_log: specials, exact points, and within
+    one ulp of the C library's log everywhere (it is not the same function: they
+    differ in the last bit for a few percent of arguments)."""
+    import math
+    L = oracle.fdlibm_log
+    assert L(1.0) == 0.0 and L(0.0) == -math.inf and L(-0.0) == -math.inf
+    assert math.isnan(L(-1.0)) and L(math.inf) == math.inf and math.isnan(L(math.nan))
+    assert L(2.0) == 0.6931471805599453 and L(5e-324) == -744.4400719213812
+    rng = np.random.default_rng(4)
+    xs = np.concatenate([rng.random(20000), rng.random(2000) * 1e-310, np.exp(rng.uniform(-700, 700, 20000))])
+    diff = 0
+    for x in xs.tolist():
+        a, b = L(x), math.log(x)
+        assert abs(a - b) <= math.ulp(b), x
+        diff += a != b
+    assert 0 < diff < len(xs) // 5
+
+
+def test_oracle_double_matrix_rand(oracle):
+    """orc_rand: one Random(1L) stream over the shard's rows (cols |g| each), rows of
+    unit norm; the first row is exactly |gaussian| x 3 / norm in double."""
+    s = oracle.OracleStore(1, 1, 3, 100, 109, 3)
+    assert s.rand() == 0
+    g = np.abs(oracle.java_random_gaussians(1, 30)).reshape(10, 3)
+    for i in range(10):
+        nrm = math.sqrt(g[i, 0] * g[i, 0] + g[i, 1] * g[i, 1] + g[i, 2] * g[i, 2])
+        assert s.data[i].tolist() == [g[i, j] / nrm for j in range(3)]
+    assert oracle.OracleStore(1, 0, 1, 0, 9, 3).rand() != 0  # float matrices: unseeded in the reference
+
+
+def test_java_parse_float():
+    """Float.parseFloat for DataStore.set(String): one rounding to float32."""
+    from distml_amd.store import java_parse_float as pf
+    assert pf("0.1") == float(np.float32(0.1)) and pf(" 3 ") == 3.0 and pf("2.5f") == 2.5 and pf("-0") == 0.0
+    assert math.copysign(1, pf("-0.0")) == -1 and pf("Infinity") == math.inf and math.isnan(pf("NaN"))
+    assert pf("0x1.8p1") == 3.0 and pf("1e-50") == 0.0 and pf("1e39") == math.inf
+    # the exact float32 tie 1 + 2^-24 goes to the even side; one digit above it rounds up,
+    # where a detour through double (which holds the tie exactly) would round down
+    up = float(np.nextafter(np.float32(1), np.float32(2)))
+    assert pf("1.000000059604644775390625") == 1.0 and pf("1.000000059604644775390626") == up
+    with pytest.raises(ValueError):
+        pf("abc")
