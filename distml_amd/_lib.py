@@ -95,6 +95,8 @@ SIGNATURES = {
     "dml_group_store": (C.c_int, [_vp, _P(_vp)]),
     "dml_group_prereduce_stats": (C.c_int, [_vp, _P(dml_store_counters), _i32]),
     "dml_group_push_full_range": (C.c_int, [_vp, _P(_vp), _P(_i64), _i32]),
+    "dml_group_push_local": (C.c_int, [_vp, _P(_vp), _P(_i64), _i32]),
+    "dml_group_debug_fail_verify": (C.c_int, [_vp, _i32]),
     "dml_group_flush": (C.c_int, [_vp]),
     "dml_group_destroy": (None, [_vp]),
     "dml_synth_dense_bucket": (C.c_int, [_vp, _P(dml_desc), _i64, _i64, _i64, _i32, _u64, _u64, _u64, _vp]),

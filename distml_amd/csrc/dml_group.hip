@@ -69,9 +69,11 @@ struct dml_group {
     // calls whose pieces are enqueued but whose partial is not yet reduce-scattered:
     // the reduce-scatter waits for the call's verdict (dml_prereduce_verify)
     struct Call {
-        dml_prereduce* h;
-        int set;  // partial / recv buffer set
+        dml_prereduce* h;  // null when the call failed before its pieces were recorded
+        int set;           // partial / recv buffer set
+        int rc;            // a local failure of the call's pre-reduce (DML_OK otherwise)
     };
+    int fail_verify_at = 0;  // fault injection (dml_group_debug_fail_verify): the n-th next verdict fails
     std::deque<Call> pending;
     int k = 0;
     bool plain = true;  // plain-sum dense matrix: the full-range pre-reduce path applies
@@ -110,22 +112,47 @@ namespace {
 // The oldest pending call: read its verdict (a failed speculation re-runs its
 // pieces exactly), then reduce-scatter its partial on the communication stream
 // and apply the received rows on the store's stream; its errors are returned.
+//
+// Every rank issues the same collectives in the same order whatever happens
+// locally: a rank whose call failed here (its verdict, its re-run, a
+// HIP error before the pieces) still enters the reduce-scatter, with a zeroed
+// partial, and skips only its own apply; the error is returned to its caller.
+// The other ranks' shards then hold every rank's sums except that rank's call.
 int finish_front(dml_group* g) {
     dml_group::Call c = g->pending.front();
     g->pending.pop_front();
-    int rc = dml_prereduce_verify(c.h, nullptr);
+    int rc = c.rc;
+    if (rc == DML_OK) {
+        rc = dml_prereduce_verify(c.h, nullptr);
+        if (rc == DML_OK && g->fail_verify_at > 0 && --g->fail_verify_at == 0)
+            rc = set_error(DML_E_HIP, "injected verify failure (dml_group_debug_fail_verify)");
+    }
     if (rc == DML_OK) rc = dml_prereduce_stream_wait(c.h, g->rstream);
     const int64_t S = g->step_rows, P = g->pieces, blk = S / P, W = g->world, C = g->cols;
     uint8_t* part = (uint8_t*)g->partial[c.set];
     // one rank: the [rank][row] slices are the shard's rows in order, the
     // reduce-scatter would be a copy; the owner apply reads the partial itself
     uint8_t* rcv = W == 1 ? part : (uint8_t*)g->recv[c.set];
-    for (int64_t j = 0; j < P && rc == DML_OK && W > 1; ++j) {
+    const int local = rc;
+    if (local != DML_OK && W > 1) {
+        // contribute zeros: the pieces (or their re-run) are done with the partial first
+        (void)hipStreamSynchronize(g->cstream);
+        if (c.h) (void)dml_prereduce_stream_wait(c.h, g->rstream);
+        (void)hipMemsetAsync(part, 0, (size_t)(W * S * C) * g->vbytes, g->rstream);
+    }
+    int crc = DML_OK;  // the collective's own status
+    for (int64_t j = 0; j < P && W > 1; ++j) {
         const ncclResult_t r = ncclReduceScatter(part + (size_t)(j * W * blk * C) * g->vbytes,
                                                  rcv + (size_t)(j * blk * C) * g->vbytes, (size_t)(blk * C), g->dtype,
                                                  ncclSum, g->comm, g->rstream);
-        if (r != ncclSuccess) rc = set_error(DML_E_HIP, std::string("ncclReduceScatter: ") + ncclGetErrorString(r));
+        if (r != ncclSuccess && crc == DML_OK)
+            crc = set_error(DML_E_HIP, std::string("ncclReduceScatter: ") + ncclGetErrorString(r));
     }
+    if (local != DML_OK) {
+        if (c.h) (void)dml_prereduce_end(c.h);
+        return local;
+    }
+    rc = crc;
     if (rc == DML_OK && hipEventRecord(g->rs_done[c.set], g->rstream) != hipSuccess) rc = set_error(DML_E_HIP, "event");
     if (rc == DML_OK && hipStreamWaitEvent(g->sstream, g->rs_done[c.set], 0) != hipSuccess)
         rc = set_error(DML_E_HIP, "stream wait");
@@ -332,20 +359,27 @@ int dml_group_push_full_range(dml_group* g, const void* const* dev_bufs, const i
     const int k = g->k;
     g->k ^= 1;
     dml_prereduce* h = nullptr;
-    GRC(dml_prereduce_begin_ctx(g->pctx, dev_bufs, lens, n, g->istream, &h));
+    int rc = dml_prereduce_begin_ctx(g->pctx, dev_bufs, lens, n, g->istream, &h);
     // buffer set k was used two calls ago: its apply (behind its reduce-scatter) is done
-    int rc = hipEventSynchronize(g->applied[k]) == hipSuccess ? DML_OK : set_error(DML_E_HIP, "applied wait");
+    if (rc == DML_OK && hipEventSynchronize(g->applied[k]) != hipSuccess) rc = set_error(DML_E_HIP, "applied wait");
     uint8_t* part = (uint8_t*)g->partial[k];
     for (int64_t j = 0; j < P && rc == DML_OK; ++j)
         rc = dml_prereduce_piece(h, blk, S, j * blk, W * blk, part + (size_t)(j * W * blk * C) * g->vbytes,
                                  g->cstream);
-    if (rc != DML_OK) {
+    if (rc != DML_OK && h) {
         (void)dml_prereduce_end(h);
-        return rc;
+        h = nullptr;
     }
-    g->pending.push_back({h, k});
+    // a call that failed here still takes its place in the collective sequence
+    // (finish_front contributes zeros for it and reports rc)
+    g->pending.push_back({h, k, rc});
     // the previous call: verdict, reduce-scatter (under this call's pieces), apply, errors
-    return end_pending(g, 1);
+    const int r1 = end_pending(g, 1);
+    if (rc != DML_OK) {
+        const int r2 = end_pending(g, 0);  // this call's failure, reported now
+        return r1 != DML_OK ? r1 : r2;
+    }
+    return r1;
 }
 
 int dml_group_push_exchange(dml_group* g, const void* const* dev_bufs, const int64_t* lens, int32_t n) {
@@ -386,10 +420,15 @@ int dml_group_push_exchange(dml_group* g, const void* const* dev_bufs, const int
     int64_t total = 0;
     for (int b = 0; b < n; ++b) total += lens[b];
     GHIP(hipEventSynchronize(g->xsent[i]));  // the set's last all-to-all (two calls ago) read xsend[i]
-    GRC(grow(&g->xsend[i], &g->xsend_cap[i], total));
-    std::vector<int64_t> cnt((size_t)n * W);  // [push][dest]
-    GRC(dml_shard_split(&g->desc, g->cols, g->total_rows, W, dev_bufs, lens, n, g->xsend[i], g->xsend_cap[i],
-                        cnt.data(), g->cstream));
+    std::vector<int64_t> cnt((size_t)n * W, 0);  // [push][dest]
+    // a local failure (a push that is not whole records, a HIP error) still takes part
+    // in both exchanges, sending nothing, so that no peer waits for this rank; the
+    // error is returned after them
+    int local = grow(&g->xsend[i], &g->xsend_cap[i], total);
+    if (local == DML_OK)
+        local = dml_shard_split(&g->desc, g->cols, g->total_rows, W, dev_bufs, lens, n, g->xsend[i],
+                                g->xsend_cap[i], cnt.data(), g->cstream);
+    if (local != DML_OK) std::fill(cnt.begin(), cnt.end(), 0);
     // counts per destination, then per source: mine[d][b] out, theirs[q][b] in (n per peer)
     std::vector<int64_t> mine((size_t)W * n), theirs((size_t)W * n);
     for (int d = 0; d < W; ++d)
@@ -449,7 +488,7 @@ int dml_group_push_exchange(dml_group* g, const void* const* dev_bufs, const int
         }
     g->xheld = true;
     g->xheld_set = i;
-    return DML_OK;
+    return local;
 }
 
 int dml_group_push_moments(dml_group* g, const void* const* dev_bufs, const int64_t* lens, int32_t n) {
@@ -475,19 +514,27 @@ int dml_group_push_moments(dml_group* g, const void* const* dev_bufs, const int6
     const int k = g->mk;
     g->mk ^= 1;
     dml_prereduce* h = nullptr;
-    GRC(dml_prereduce_begin(&g->desc, 0, g->total_rows, g->cols, dev_bufs, lens, n, g->istream, &h));
+    int rc = dml_prereduce_begin(&g->desc, 0, g->total_rows, g->cols, dev_bufs, lens, n, g->istream, &h);
     // buffer set k was used two calls ago: its apply (behind its reduce-scatter) is done
-    int rc = hipEventSynchronize(g->mapplied[k]) == hipSuccess ? DML_OK : set_error(DML_E_HIP, "applied wait");
+    if (rc == DML_OK && hipEventSynchronize(g->mapplied[k]) != hipSuccess) rc = set_error(DML_E_HIP, "applied wait");
     if (rc == DML_OK) rc = dml_prereduce_moments_piece(h, S, S, 0, W * S, g->mpart[k], g->cstream);
     if (rc == DML_OK) rc = dml_prereduce_stream_wait(h, g->rstream);
-    if (rc == DML_OK) {
-        const ncclResult_t r = ncclReduceScatter(g->mpart[k], g->mrecv[k], (size_t)(S * 2 * C), ncclFloat32, ncclSum,
-                                                 g->comm, g->rstream);
-        if (r != ncclSuccess) rc = set_error(DML_E_HIP, std::string("ncclReduceScatter: ") + ncclGetErrorString(r));
+    const int local = rc;
+    if (local != DML_OK) {
+        // the same collective on every rank: zeros from this one, no apply here
+        (void)hipStreamSynchronize(g->cstream);
+        (void)hipEventSynchronize(g->mapplied[k]);
+        (void)hipMemsetAsync(g->mpart[k], 0, (size_t)(W * S * 2 * C) * sizeof(float), g->rstream);
     }
-    if (rc != DML_OK) {
+    const ncclResult_t r = ncclReduceScatter(g->mpart[k], g->mrecv[k], (size_t)(S * 2 * C), ncclFloat32, ncclSum,
+                                             g->comm, g->rstream);
+    if (local != DML_OK) {
+        if (h) (void)dml_prereduce_end(h);
+        return local;
+    }
+    if (r != ncclSuccess) {
         (void)dml_prereduce_end(h);
-        return rc;
+        return set_error(DML_E_HIP, std::string("ncclReduceScatter: ") + ncclGetErrorString(r));
     }
     GHIP(hipEventRecord(g->mrs_done[k], g->rstream));
     GHIP(hipStreamWaitEvent(g->sstream, g->mrs_done[k], 0));
@@ -495,6 +542,27 @@ int dml_group_push_moments(dml_group* g, const void* const* dev_bufs, const int6
     GHIP(hipEventRecord(g->mapplied[k], g->sstream));
     g->mpending.push_back(h);
     return end_moments(g, 1);  // the previous call's errors
+}
+
+// Pushes already split to this shard (the reference client's per-partition split,
+// SparseMatrix.java:46-60): the store's exact ordered push, after every earlier
+// group call, so the store applies calls in the order they were made.
+int dml_group_push_local(dml_group* g, const void* const* dev_bufs, const int64_t* lens, int32_t n) {
+    if (!g || n < 0 || n > kMaxW || (n > 0 && (!dev_bufs || !lens)))
+        return set_error(DML_E_INVALID_ARG, "bad push arguments (n must be <= 64)");
+    GHIP(hipSetDevice(g->device));
+    if (g->xheld) {  // the last exchange call's slices
+        GHIP(hipStreamSynchronize(g->rstream));
+        GRC(hand_over(g));
+    }
+    GRC(end_pending(g, 0));  // full-range calls waiting for their reduce-scatter and apply
+    return dml_store_push_batch_device(g->store, dev_bufs, lens, n);
+}
+
+int dml_group_debug_fail_verify(dml_group* g, int32_t nth) {
+    if (!g || nth < 0) return set_error(DML_E_INVALID_ARG, "bad fault-injection arguments");
+    g->fail_verify_at = nth;
+    return DML_OK;
 }
 
 int dml_group_flush(dml_group* g) {

@@ -270,17 +270,28 @@ class ShardGroup:
         S, P, cols, world = self.step_rows, self.pieces, self.cols, self.world
         blk = S // P
         try:
-            self.ops.verify(h)
-            self.ops.stream_wait(h, self.comm.cuda_stream)  # the pieces (or their re-run)
             partial, recv = self._partials[k], self._recvs[k]
             if self._local_rs():
                 # one rank: the [rank][row] slices are the shard's rows in order, so
                 # the reduce-scatter is the identity and the apply reads the partial
                 recv = partial
+            failed = None
+            try:
+                self.ops.verify(h)
+                self.ops.stream_wait(h, self.comm.cuda_stream)  # the pieces (or their re-run)
+            except Exception as e:
+                # every rank runs the same collectives whatever fails locally:
+                # this rank contributes zeros, skips its apply and raises afterwards
+                failed = e
+                self.cstream.synchronize()
+                with torch.cuda.stream(self.comm):
+                    partial.zero_()
             with torch.cuda.stream(self.comm):
                 for j in range(P if recv is not partial else 0):
                     self._rs(recv[j * blk * cols:(j + 1) * blk * cols],
                              partial[j * world * blk * cols:(j + 1) * world * blk * cols])
+            if failed is not None:
+                raise failed
             self._rs_done[k].record(self.comm)
             if self._store_stream is not None:
                 self._store_stream.wait_event(self._rs_done[k])
@@ -500,7 +511,14 @@ class ShardGroup:
             self._xpool = [x for x in self._xpool if x is not small]
 
     def push_local(self, dev_ptrs: Sequence[int], lens: Sequence[int]) -> None:
-        """Pushes already split to this shard: exact ordered apply, no exchange."""
+        """Pushes already split to this shard: exact ordered apply, no exchange — after
+        every earlier group call's apply (the store applies calls in call order).
+        Reads of `self.store` between calls see only what was applied: flush() first."""
+        if getattr(self, "_held", None) is not None:
+            if self.partial.is_cuda:
+                self.torch.cuda.current_stream(self.partial.device).synchronize()
+            self._hand_over()
+        self._end_pending(0)
         self.store.pushDevice(dev_ptrs, lens)
 
     def _drain(self) -> None:
@@ -585,6 +603,18 @@ class NativeShardGroup:
         ptrs = (C.c_void_p * max(n, 1))(*dev_ptrs)
         ls = (C.c_int64 * max(n, 1))(*lens)
         check(self._L.dml_group_push_moments(C.c_void_p(self._h), ptrs, ls, n), self.store)
+
+    def push_local(self, dev_ptrs: Sequence[int], lens: Sequence[int]) -> None:
+        """Pushes already split to this shard (dml_group_push_local): the exact ordered
+        apply, after every earlier group call's."""
+        n = len(dev_ptrs)
+        ptrs = (C.c_void_p * max(n, 1))(*dev_ptrs)
+        ls = (C.c_int64 * max(n, 1))(*lens)
+        check(self._L.dml_group_push_local(C.c_void_p(self._h), ptrs, ls, n), self.store)
+
+    def debug_fail_verify(self, nth: int) -> None:
+        """Fault injection (tests): the nth full-range call finished from now fails its verdict."""
+        check(self._L.dml_group_debug_fail_verify(C.c_void_p(self._h), nth))
 
     def push_exchange(self, dev_ptrs: Sequence[int], lens: Sequence[int]) -> None:
         """The exact split / all-to-all / ordered-owner-apply path (dml_group_push_exchange)."""

@@ -344,7 +344,17 @@ int dml_shard_split(const dml_desc* desc, int32_t cols, int64_t total_rows, int3
  * asynchronous: buffers stay valid until the next dml_group_flush, and a
  * call's key / repeated-row errors surface at the next call or the flush.
  * fp32 results differ from the sequential order only by summation order
- * (DESIGN.md §6); int32 is exact. */
+ * (DESIGN.md §6); int32 is exact.
+ * Store order: the group applies its calls to its store in call order; a push made
+ * straight to the dml_group_store handle bypasses that order, and a read of that
+ * handle sees only the calls applied so far — call dml_group_flush before either,
+ * or push through dml_group_push_local.
+ * Collective order: every rank issues the same collectives in the same order
+ * whatever fails locally; a rank whose call fails (a push that is not whole
+ * records, a HIP error, a failed re-run) contributes zeros to that call's
+ * collective, skips its own apply and returns the error. The group is then in an
+ * undefined state for that rank (the reference's PS thread ends on an exception,
+ * PSAgent.java:188-191): destroy it. */
 typedef struct dml_group dml_group;
 int dml_group_unique_id(uint8_t* out, int32_t cap);
 int dml_group_create(const uint8_t* unique_id, int32_t world, int32_t rank, int32_t device, const dml_desc* desc,
@@ -371,8 +381,15 @@ int dml_group_push_exchange(dml_group* g, const void* const* dev_bufs, const int
  * x 2 x the model, whatever n is (the exchange path moves n pushes). Within
  * 1e-6, not bit-exact; errors surface at the next call or the flush. */
 int dml_group_push_moments(dml_group* g, const void* const* dev_bufs, const int64_t* lens, int32_t n);
+/* Pushes the client already split to this shard (SparseMatrix.java:46-60): the
+ * store's exact ordered device push (dml_store_push_batch_device), queued after
+ * every earlier group call's apply; no collective. */
+int dml_group_push_local(dml_group* g, const void* const* dev_bufs, const int64_t* lens, int32_t n);
 int dml_group_flush(dml_group* g);
 void dml_group_destroy(dml_group* g);
+/* Fault injection for tests: the nth full-range call finished from now on (1 = the
+ * next) fails its verdict as a local HIP error would (0 = off). */
+int dml_group_debug_fail_verify(dml_group* g, int32_t nth);
 
 /* --- synthetic workload generators (bench/test support) ----------------- *
  * Counter-based (SplitMix64) so the CPU oracle regenerates the same bytes.

@@ -25,19 +25,29 @@ public class GpuShardGroup implements AutoCloseable {
     }
 
     /** Device pointers (HBM, this GPU) and byte lengths of up to 64 full-range pushes. */
-    public void pushFullRange(long[] devPtrs, long[] lens) { nativeGroupPush(handle, devPtrs, lens, false); }
+    public void pushFullRange(long[] devPtrs, long[] lens) { nativeGroupPush(handle, devPtrs, lens, 0); }
 
     /**
      * Exact path for AdaGrad, int32-checked, array or key-subset pushes: split by owner
      * (SparseMatrix.push's per-partition split), exchanged with RCCL send/recv, applied by
      * each owner in rank-major push order. Every rank passes the same number of pushes.
      */
-    public void pushExchange(long[] devPtrs, long[] lens) { nativeGroupPush(handle, devPtrs, lens, true); }
+    public void pushExchange(long[] devPtrs, long[] lens) { nativeGroupPush(handle, devPtrs, lens, 1); }
+
+    /** AdaGrad with many pushes per rank: Σu and Σu² reduce-scattered, within 1e-6 (not bit-exact). */
+    public void pushMoments(long[] devPtrs, long[] lens) { nativeGroupPush(handle, devPtrs, lens, 2); }
+
+    /**
+     * Pushes the client already split to this shard (SparseMatrix.java:46-60): the exact
+     * ordered apply, after every earlier call of this group. Push to storeHandle() directly
+     * only after flush(): the group applies its calls in call order.
+     */
+    public void pushLocal(long[] devPtrs, long[] lens) { nativeGroupPush(handle, devPtrs, lens, 3); }
 
     /** Every call applied; throws the first deferred key / repeated-row error. */
     public void flush() { nativeGroupFlush(handle); }
 
-    /** dml_store* of this rank's shard (owned by the group), for fetch / checkpoint. */
+    /** dml_store* of this rank's shard (owned by the group), for fetch / checkpoint after flush(). */
     public long storeHandle() { return nativeGroupStore(handle); }
 
     public void close() {
@@ -51,7 +61,7 @@ public class GpuShardGroup implements AutoCloseable {
     private static native long nativeGroupCreate(byte[] id, int world, int rank, int device, int dataType,
                                                  int keyType, int valueType, int denseRow, int denseColumn,
                                                  int adaGrad, long totalRows, int cols, int pieces);
-    private static native void nativeGroupPush(long g, long[] devPtrs, long[] lens, boolean exchange);
+    private static native void nativeGroupPush(long g, long[] devPtrs, long[] lens, int mode);
     private static native void nativeGroupFlush(long g);
     private static native long nativeGroupStore(long g);
     private static native void nativeGroupDestroy(long g);

@@ -228,8 +228,9 @@ JNIEXPORT jlong JNICALL GFN(nativeGroupCreate)(JNIEnv* env, jclass, jbyteArray i
     return reinterpret_cast<jlong>(g);
 }
 
+// mode: 0 full-range pre-reduce, 1 exact exchange, 2 two-moment AdaGrad, 3 local (already split)
 JNIEXPORT void JNICALL GFN(nativeGroupPush)(JNIEnv* env, jclass, jlong g, jlongArray ptrs, jlongArray lens,
-                                             jboolean exchange) {
+                                             jint mode) {
     const jsize n = env->GetArrayLength(ptrs);
     std::vector<jlong> p((size_t)n), l((size_t)n);
     env->GetLongArrayRegion(ptrs, 0, n, p.data());
@@ -240,8 +241,14 @@ JNIEXPORT void JNICALL GFN(nativeGroupPush)(JNIEnv* env, jclass, jlong g, jlongA
         dp[(size_t)i] = reinterpret_cast<const void*>(p[(size_t)i]);
         dl[(size_t)i] = l[(size_t)i];
     }
-    const int rc = exchange ? dml_group_push_exchange(G(g), dp.data(), dl.data(), (int32_t)n)
-                            : dml_group_push_full_range(G(g), dp.data(), dl.data(), (int32_t)n);
+    int rc = DML_E_INVALID_ARG;
+    switch (mode) {
+        case 0: rc = dml_group_push_full_range(G(g), dp.data(), dl.data(), (int32_t)n); break;
+        case 1: rc = dml_group_push_exchange(G(g), dp.data(), dl.data(), (int32_t)n); break;
+        case 2: rc = dml_group_push_moments(G(g), dp.data(), dl.data(), (int32_t)n); break;
+        case 3: rc = dml_group_push_local(G(g), dp.data(), dl.data(), (int32_t)n); break;
+        default: break;
+    }
     if (rc) throw_for(env, rc);
 }
 

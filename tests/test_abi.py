@@ -109,3 +109,18 @@ def test_dmatrix_partition_and_factory_dispatch():
     bad.partition(1)
     with pytest.raises(IllegalArgumentException):
         DataStore.createStore(0, bad)
+
+
+def test_rccl_double_covers_the_library_imports():
+    """tests/rccl_double (the stand-in the native group's N > 1 tests load ahead of
+    libdistml_ps.so) defines every nccl* symbol the product library imports."""
+    import subprocess
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    subprocess.run(["make", "-s", "-C", os.path.join(root, "tests", "rccl_double")], check=True)
+
+    def syms(path, kind):
+        out = subprocess.run(["nm", "-D", path], check=True, capture_output=True, text=True).stdout
+        return {ln.split()[-1] for ln in out.splitlines() if ln.split()[-2:-1] == [kind] and "nccl" in ln}
+    need = syms(os.path.join(root, "distml_amd", "libdistml_ps.so"), "U")
+    have = syms(os.path.join(root, "tests", "rccl_double", "librccl_double.so"), "T")
+    assert need and need <= have, need - have

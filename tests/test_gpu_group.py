@@ -119,6 +119,11 @@ def test_shard_group_hip_multiprocess(tmp_path, oracle, world, vt, rows, pieces,
     if vt == 0:
         assert np.array_equal(got, o.data)
         return
+    check_full_range(got, o, init, all_b, rows, cols)
+
+
+def check_full_range(got, o, init, all_b, rows, cols):
+    """fp32 sharded sums against the sequential oracle `o`."""
     terms = np.abs(init.astype(np.float64))
     exact = init.astype(np.float64)
     for b in all_b:
@@ -210,8 +215,14 @@ def test_exchange_hip_multiprocess(tmp_path, oracle, world, vt):
     bit-exact against one oracle store fed every call's pushes, rank-major per call; each shard's maxDelta against an oracle
     shard fed the same pushes restricted to its keys."""
     import torch.multiprocessing as mp
-    from distml_amd.datadesc import KeyRange
     mp.spawn(_xworker, args=(world, _free_port(), vt, str(tmp_path)), nprocs=world, join=True)
+    check_exchange(tmp_path, oracle, world, vt, lambda n, r: np.load(tmp_path / f"{n}{r}.npy"))
+
+
+def check_exchange(tmp_path, oracle, world, vt, load):
+    """Exchange-path shards (load(name, rank): data / alpha / delta / md) bit-exact against
+    one oracle store fed every call's pushes rank-major, maxDelta per shard."""
+    from distml_amd.datadesc import KeyRange
     init = _init(vt, XR, XC)
     allb = [b for call in range(XCALLS) for r in range(world) for b in _xbuckets(vt, r, call)]
     o = oracle.OracleStore(1, 0, vt, 0, XR - 1, XC, 1, int(vt == 1))
@@ -220,12 +231,12 @@ def test_exchange_hip_multiprocess(tmp_path, oracle, world, vt):
     o.data[:] = init
     for b in allb:
         assert o.push(b.tobytes()) == 0
-    got = np.concatenate([np.load(tmp_path / f"data{r}.npy") for r in range(world)]).reshape(XR, XC)
+    got = np.concatenate([load("data", r) for r in range(world)]).reshape(XR, XC)
     assert got.tobytes() == o.data.tobytes()
     if vt != 1:
         return
     for name, ref in (("alpha", o.alpha), ("delta", o.delta)):
-        g = np.concatenate([np.load(tmp_path / f"{name}{r}.npy") for r in range(world)]).reshape(XR, XC)
+        g = np.concatenate([load(name, r) for r in range(world)]).reshape(XR, XC)
         assert g.tobytes() == ref.tobytes()
     for r, sh in enumerate(KeyRange(0, XR - 1).linearSplit(world)):
         so = oracle.OracleStore(1, 0, 1, sh.firstKey, sh.lastKey, XC, 1, 1)
@@ -235,7 +246,7 @@ def test_exchange_hip_multiprocess(tmp_path, oracle, world, vt):
             rec = b.reshape(-1, 4 + 4 * XC)
             k = rec[:, :4].copy().view("<i4").ravel()
             assert so.push(rec[(k >= sh.firstKey) & (k <= sh.lastKey)].tobytes()) == 0
-        assert tuple(np.load(tmp_path / f"md{r}.npy").tolist()) == tuple(float(x) for x in so.max_delta())
+        assert tuple(load("md", r).tolist()) == tuple(float(x) for x in so.max_delta())
 
 
 # ---------------------------------------------------------------- two-moment AdaGrad path

@@ -76,7 +76,7 @@ class MockJVM:
         }
         gsig = {
             "nativeUniqueId": ([], P), "nativeGroupCreate": ([P, I, I, I, I, I, I, I, I, I, J, I, I], J),
-            "nativeGroupPush": ([J, P, P, C.c_uint8], None), "nativeGroupFlush": ([J], None),
+            "nativeGroupPush": ([J, P, P, I], None), "nativeGroupFlush": ([J], None),
             "nativeGroupStore": ([J], J), "nativeGroupDestroy": ([J], None),
         }
         self.fn = {}
