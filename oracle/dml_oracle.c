@@ -631,3 +631,36 @@ int orc_rand(orc_store* s) {
     }
     return ORC_OK;
 }
+
+/* ---- row-subset generators (full-size parity on sampled rows) --------------
+ * The synthetic dense spec makes a full-range push's record for row `row` depend
+ * only on (seed, row): orc_synth_dense_rows writes, for each sampled row rows[i],
+ * the record orc_synth_dense_bucket would hold for it, keyed i (a compact store of
+ * the sampled rows); orc_synth_fill_rows the orc_synth_fill values of those rows of
+ * a `cols`-wide store. Per-element results of full-range pushes do not depend on
+ * record order, so the compact store reproduces the sampled rows exactly. */
+void orc_synth_dense_rows(uint8_t* out, int32_t key_type, int32_t value_type, const int64_t* rows, int64_t n,
+                          int32_t cols, uint64_t seed) {
+    const int K = key_type == 0 ? 4 : 8, V = value_type == 3 ? 8 : 4;
+    const int64_t stride = K + (int64_t)V * cols;
+    const uint64_t s0 = orc_splitmix64(seed);
+    for (int64_t i = 0; i < n; ++i) {
+        uint8_t* rec = out + i * stride;
+        if (K == 4) wr_i32(rec, (int32_t)i); else wr_i64(rec, i);
+        for (int32_t c = 0; c < cols; ++c)
+            put_value(rec + K + (int64_t)V * c, value_type,
+                      orc_splitmix64(s0 + (uint64_t)rows[i] * (uint64_t)cols + (uint64_t)c));
+    }
+}
+
+void orc_synth_fill_rows(orc_store* s, const int64_t* rows, uint64_t seed) {
+    const uint64_t s0 = orc_splitmix64(seed);
+    for (int64_t i = 0; i < s->rows; ++i)
+        for (int32_t c = 0; c < s->cols; ++c) {
+            const int64_t at = i * s->cols + c;
+            const uint64_t h = orc_splitmix64(s0 + (uint64_t)rows[i] * (uint64_t)s->cols + (uint64_t)c);
+            if (s->value_type == 1) ((float*)s->data)[at] = (float)((int32_t)(h % 100) - 50) * 0x1p-17f;
+            else if (s->value_type == 3) ((double*)s->data)[at] = (double)((int32_t)(h % 100) - 50) * 0x1p-17;
+            else ((int32_t*)s->data)[at] = 64 + (int32_t)(h % 51);
+        }
+}

@@ -69,6 +69,10 @@ void orc_synth_sparse_bucket(uint8_t* out, int32_t key_type, int32_t value_type,
                              int64_t first_key, int64_t key_space, int64_t nrec, uint64_t seed,
                              uint64_t perm_a, uint64_t perm_c);
 void orc_synth_fill(orc_store* s, uint64_t seed);
+/* The same generators restricted to sampled rows (record i / store row i = rows[i]). */
+void orc_synth_dense_rows(uint8_t* out, int32_t key_type, int32_t value_type, const int64_t* rows, int64_t n,
+                          int32_t cols, uint64_t seed);
+void orc_synth_fill_rows(orc_store* s, const int64_t* rows, uint64_t seed);
 
 /* DoubleMatrixStore.rand() (DoubleMatrixStore.java:192-207): java.util.Random(1L),
  * |nextGaussian()| rows scaled to unit norm; ORC_E_INVALID_ARG for other stores.

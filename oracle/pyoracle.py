@@ -63,6 +63,8 @@ def lib():
         L.orc_synth_dense_bucket.argtypes = [vp, i32, i32, i64, i64, i64, i32, u64, u64, u64]
         L.orc_synth_sparse_bucket.argtypes = [vp, i32, i32, i32, i64, i64, i64, u64, u64, u64]
         L.orc_synth_fill.argtypes = [vp, u64]
+        L.orc_synth_dense_rows.argtypes = [vp, i32, i32, vp, i64, i32, u64]
+        L.orc_synth_fill_rows.argtypes = [vp, vp, u64]
         L.orc_rand.restype = C.c_int
         L.orc_rand.argtypes = [vp]
         L.orc_java_random_ints.argtypes = [i64, i32, vp]
@@ -159,6 +161,12 @@ class OracleStore:
     def synth_fill(self, seed):
         lib().orc_synth_fill(self._h, seed)
 
+    def synth_fill_rows(self, rows, seed):
+        """orc_synth_fill's values of `rows` of a self.cols-wide store, as rows 0..n-1."""
+        r = np.ascontiguousarray(rows, np.int64)
+        assert len(r) == self.rows
+        lib().orc_synth_fill_rows(self._h, r.ctypes.data, seed)
+
     def rand(self) -> int:
         """DoubleMatrixStore.rand() (DoubleMatrixStore.java:192-207), bit-exact."""
         return lib().orc_rand(self._h)
@@ -200,6 +208,16 @@ def synth_dense_bucket(key_type, value_type, first_key, shard_rows, nrec, cols, 
     out = np.empty(nrec * (K + V * cols), np.uint8)
     lib().orc_synth_dense_bucket(out.ctypes.data, key_type, value_type, first_key, shard_rows,
                                  nrec, cols, seed, perm_a, perm_c)
+    return out
+
+
+def synth_dense_rows(key_type, value_type, rows, cols, seed) -> np.ndarray:
+    """The records synth_dense_bucket holds for `rows` (any push order), keyed 0..n-1."""
+    r = np.ascontiguousarray(rows, np.int64)
+    K = 4 if key_type == 0 else 8
+    V = 8 if value_type == 3 else 4
+    out = np.empty(len(r) * (K + V * cols), np.uint8)
+    lib().orc_synth_dense_rows(out.ctypes.data, key_type, value_type, r.ctypes.data, len(r), cols, seed)
     return out
 
 

@@ -1602,6 +1602,89 @@ def test_config4_full_shard_bit_exact(oracle, ada, asc):
     st.close()
 
 
+def _config4_rows(rows):
+    """Sampled rows of the 10 M-row model: every 4 099th row, and every row of the last
+    262 144, whose 800-B rows lie past 2^32 bytes of each array (and the pushes' 804-B
+    records past 2^32 bytes of each push)."""
+    return np.unique(np.concatenate([np.arange(0, rows, 4099), np.arange(rows - 262_144, rows)]))
+
+
+def _perm10m(b, rows):
+    import math
+    a = (3000 + b) * 2654435761 % rows | 1
+    while math.gcd(a, rows) != 1:
+        a += 2
+    return a, b * 7919 % rows
+
+
+@pytest.mark.parametrize("case", ["sum_ascending", "sum_permuted", "adagrad", "prereduce_world8"])
+def test_config4_model_size_sampled_rows(oracle, case):
+    """The config-4 legs at the size bench.py times: the 10 M x 200 fp32
+    model (8 GB per array; byte offsets past 2^32), device-resident full-range pushes,
+    compared on sampled rows (_config4_rows) against the oracle fed the same rows'
+    records (pyoracle.synth_dense_rows: a full-range push's per-element result does not
+    depend on record order). sum_*: k_reduce_flat, 4 pushes (FloatMatrixStore.java:
+    200-222), ascending (identity speculation) or permuted; adagrad: k_ada_flat, 2
+    pushes, data / alpha / delta (FloatMatrixStoreAdaGrad.java:262-277); prereduce_world8:
+    the kPreReduce partial a rank writes at N = 8 ([rank][row], 8 x 1 250 000 rows), one
+    ascending and one permuted push summed in push order. All bit-exact."""
+    import ctypes as C
+    from distml_amd import DataDesc, DataStore, KeyList, KeyRange, _lib
+    from distml_amd.group import HipOps
+    rows, cols = 10_000_000, 200
+    ada = case == "adagrad"
+    W = {"adagrad": 2, "prereduce_world8": 2}.get(case, 4)
+    fmt = DataDesc(1, 0, 1, False, True, ada)
+    L = _lib.load()
+    pick = _config4_rows(rows)
+    s0 = torch.cuda.current_stream().cuda_stream
+    dev = []
+    for b in range(W):
+        pa, pc = (1, 0) if case == "sum_ascending" or (case != "sum_permuted" and b == 0) else _perm10m(b, rows)
+        t = torch.empty(rows * (4 + 4 * cols), dtype=torch.uint8, device="cuda")
+        assert L.dml_synth_dense_bucket(t.data_ptr(), C.byref(fmt.to_c()), 0, rows, rows, cols, 3000 + b, pa, pc,
+                                        C.c_void_p(s0)) == 0
+        dev.append(t)
+    torch.cuda.synchronize()
+    o = oracle.OracleStore(1, 0, 1, 0, len(pick) - 1, cols, 1, int(ada))
+    if case == "prereduce_world8":
+        S = rows // 8
+        part = torch.empty(8 * S * cols, dtype=torch.float32, device="cuda")
+        ops = HipOps()
+        h = ops.begin(fmt, 0, rows, cols, [t.data_ptr() for t in dev], [t.numel() for t in dev], s0)
+        try:
+            ops.piece(h, S, S, 0, 8 * S, part.data_ptr(), s0)
+        finally:
+            ops.end(h)
+        torch.cuda.synchronize()
+        got = part.view(-1, cols)[torch.from_numpy(pick).cuda()].cpu().numpy()
+        del part
+    else:
+        st = DataStore(fmt, KeyRange(0, rows - 1), cols)
+        if ada:
+            st.setAlpha(0.025, 0.0001, 1.0)
+            o.set_alpha(0.025, 0.0001, 1.0)
+        st.synth_fill(13)
+        o.synth_fill_rows(pick, 13)
+        st.pushDevice([t.data_ptr() for t in dev], [t.numel() for t in dev])
+        st.flush()
+        rec = np.frombuffer(st.handleFetch(fmt, KeyList(pick.tolist())), np.uint8).reshape(len(pick), 4 + 4 * cols)
+        assert rec[:, :4].copy().view("<i4").ravel().tolist() == pick.tolist()
+        got = rec[:, 4:].copy().view("<f4")
+        if ada:
+            a, d = st.adagrad_state()
+            ga, gd = a.reshape(rows, cols)[pick], d.reshape(rows, cols)[pick]
+            del a, d
+        st.close()
+    del dev
+    torch.cuda.empty_cache()
+    for b in range(W):
+        assert o.push(oracle.synth_dense_rows(0, 1, pick, cols, 3000 + b).tobytes()) == 0
+    assert got.tobytes() == o.data.tobytes(), case
+    if ada:
+        assert ga.tobytes() == o.alpha.tobytes() and gd.tobytes() == o.delta.tobytes()
+
+
 def _sampled_rows(oracle, b, rows):
     """The record positions k_ident_check samples in push b of a chunk (32 evenly
     spaced + 32 hashed), so a test can corrupt records the sample does not see."""

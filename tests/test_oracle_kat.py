@@ -156,3 +156,24 @@ def test_java_parse_float():
     assert pf("1.000000059604644775390625") == 1.0 and pf("1.000000059604644775390626") == up
     with pytest.raises(ValueError):
         pf("abc")
+
+
+def test_row_subset_generators_match_full(oracle):
+    """synth_dense_rows / synth_fill_rows (the full-size tests' sampled rows) hold
+    exactly the values the full generators give those rows, whatever the push order."""
+    rows, cols = 1000, 7
+    pick = np.array([0, 5, 6, 999, 512, 3])
+    for vt in (0, 1, 3):
+        V = 8 if vt == 3 else 4
+        dt = {0: "<i4", 1: "<f4", 3: "<f8"}[vt]
+        full = oracle.synth_dense_bucket(0, vt, 0, rows, rows, cols, 77, 3, 11).reshape(rows, 4 + V * cols)
+        keys = full[:, :4].copy().view("<i4").ravel()
+        byrow = {int(k): full[i, 4:].tobytes() for i, k in enumerate(keys)}
+        sub = oracle.synth_dense_rows(0, vt, pick, cols, 77).reshape(len(pick), 4 + V * cols)
+        assert sub[:, :4].copy().view("<i4").ravel().tolist() == list(range(len(pick)))
+        assert [sub[i, 4:].tobytes() for i in range(len(pick))] == [byrow[int(r)] for r in pick]
+        s = oracle.OracleStore(1, 0, vt, 0, rows - 1, cols)
+        s.synth_fill(9)
+        t = oracle.OracleStore(1, 0, vt, 0, len(pick) - 1, cols)
+        t.synth_fill_rows(pick, 9)
+        assert t.data.view(dt).tobytes() == s.data[pick].tobytes()
