@@ -548,6 +548,63 @@ def headline(ctx: Ctx, L, args, out_line: dict):
     torch.cuda.empty_cache()
 
 
+def leg_native_group(ctx: Ctx, L, args) -> dict:
+    """The config-2 workload through the native shard group (dml_group_*, the RCCL
+    communicator libdistml_ps creates itself; what the JNI's GpuShardGroup binds):
+    the same per-rank work as the headline's sharded path — 32 full-range pushes per
+    GPU, ordered pre-reduce, ncclReduceScatter of the [rank][row] slices over xGMI, the
+    owner apply — run by every N > 1 line (and at N = 1 with --native-group). The
+    unique id travels from rank 0 over torch.distributed."""
+    torch, dist = ctx.torch, ctx.dist
+    from distml_amd import DataDesc
+    from distml_amd.group import NativeShardGroup
+    world, rank = ctx.world, ctx.rank
+    fmt = DataDesc(DataDesc.DATA_TYPE_MATRIX, DataDesc.KEY_TYPE_INT, DataDesc.ELEMENT_TYPE_FLOAT)
+    hbm_check(torch, "native_group", {"pushes": 2 * W * BUCKET,
+                                      "store": store_bytes((ROWS - 1 + world) // world, COLS, 4),
+                                      "group": group_bytes(world, ROWS, COLS, 4)})
+    uid = [NativeShardGroup.unique_id() if rank == 0 else None]
+    if world > 1:
+        dist.broadcast_object_list(uid, src=0)
+    g = NativeShardGroup(fmt, ROWS, COLS, rank, world, uid[0], device=ctx.local, pieces=args.pieces)
+    g.store.synth_fill(7)
+    bufs = make_buckets(L, torch, fmt, W, ROWS) + make_buckets(L, torch, fmt, W, ROWS, value_seed=5000)
+    sets = [([b.data_ptr() for b in bs], [b.numel() for b in bs]) for bs in (bufs[:W], bufs[W:])]
+    k_step = [0]
+
+    def step():
+        g.push_full_range(*sets[k_step[0] & 1])
+        k_step[0] += 1
+
+    timing = not args.no_timing
+
+    def reset():
+        g.prereduce_stats(reset=True)
+        if timing:
+            _pre_time(L, every=4, reset=True)
+
+    el = timed_steps(ctx, step, g.flush, args.steps, args.warmup, ramp_s=0.3, reset=reset)
+    pre_ms, pre_n = _pre_time(L, every=0, reset=True)
+    pst = g.prereduce_stats(reset=True)
+    shard_rows = g.shard.size()
+    algo = W * BUCKET + 2 * shard_rows * COLS * 4
+    out = {"workload": "config2 through dml_group (native RCCL communicator, the JNI binding's path)",
+           "value": round(algo * world * args.steps / el / 2**30, 2), "unit": "GiB/s",
+           "ms_per_step": round(el / args.steps * 1e3, 4), "n_gpus": world, "pieces": args.pieces,
+           "pushes_per_step": {k: round(pst.get(k, 0) / max(pst.get("chunks", 0), 1), 2)
+                               for k in ("identity_pushes", "reused_pushes", "indexed_pushes")},
+           "spec_reruns": pst.get("spec_reruns", 0)}
+    if pre_n > 0:
+        step_rows = (ROWS - 1 + world) // world
+        out["roofline"] = prereduce_roofline(L, ctx, args.pieces, pre_ms, pre_n,
+                                             W * BUCKET + world * step_rows * COLS * 4, "config 2, native group")
+    g.close()
+    del bufs
+    torch.cuda.synchronize()
+    torch.cuda.empty_cache()
+    return out
+
+
 def buffers_shuffled_line(ctx: Ctx, L, args, store, step, finish, cur, k_step, fmt, algo_per_rank) -> dict:
     """The in-order steps over two new bucket sets whose pushes were generated into
     their buffers in a seeded order (make_buckets(alloc_seed=7)): the headline's
@@ -1116,6 +1173,8 @@ def main():
     ap.add_argument("--alloc-seed", type=int, default=0, help=argparse.SUPPRESS)
     ap.add_argument("--one-slab", action="store_true", help=argparse.SUPPRESS)
     ap.add_argument("--shuffle-only", choices=["", "asc", "perm"], default="", help=argparse.SUPPRESS)
+    ap.add_argument("--native-group", action="store_true",
+                    help="also run the config-2 workload through dml_group at N = 1 (always at N > 1)")
     ap.add_argument("--group", action="store_true",
                     help="use the sharded pre-reduce/reduce-scatter path even at N=1 (path check)")
     ap.add_argument("--legs", default="4,5,4a", help="model-level config legs in the line (4, 5, 4a; '' = none)")
@@ -1192,6 +1251,8 @@ def main():
         line["config5"] = leg_config5(ctx, L, args)
     if "4a" in legs:
         line["config4_ada"] = leg_config4_ada(ctx, L, args)
+    if (world > 1 and not args.rehearse_gloo) or args.native_group:
+        line["native_group"] = leg_native_group(ctx, L, args)
     if world == 1 and not args.group and args.sparse_steps > 0:
         line["sparse"] = sparse_leg(ctx, L, args.sparse_steps, cpu=not args.no_cpu)
     if rank == 0 and world == 1 and not args.no_cpu and not args.group:

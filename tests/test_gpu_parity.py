@@ -1668,10 +1668,12 @@ def test_config4_model_size_sampled_rows(oracle, case):
         o.synth_fill_rows(pick, 13)
         st.pushDevice([t.data_ptr() for t in dev], [t.numel() for t in dev])
         st.flush()
-        rec = np.frombuffer(st.handleFetch(fmt, KeyList(pick.tolist())), np.uint8).reshape(len(pick), 4 + 4 * cols)
-        assert rec[:, :4].copy().view("<i4").ravel().tolist() == pick.tolist()
-        got = rec[:, 4:].copy().view("<f4")
-        if ada:
+        if not ada:
+            rec = np.frombuffer(st.handleFetch(fmt, KeyList(pick.tolist())), np.uint8).reshape(len(pick), 4 + 4 * cols)
+            assert rec[:, :4].copy().view("<i4").ravel().tolist() == pick.tolist()
+            got = rec[:, 4:].copy().view("<f4")
+        else:  # (AdaGrad's fetch interleaves alpha, FloatMatrixStoreAdaGrad.java:150-174)
+            got = st.values().reshape(rows, cols)[pick]
             a, d = st.adagrad_state()
             ga, gd = a.reshape(rows, cols)[pick], d.reshape(rows, cols)[pick]
             del a, d
