@@ -1770,6 +1770,7 @@ struct PreWs {
     hipEvent_t ctrl_ev = nullptr;   // that copy done
     hipEvent_t free_ev = nullptr;   // the workspace's last call ended (pieces / re-run done)
     bool used = false, clean = false, kept = false;
+    bool busy = false;              // a call holds it: begun, not yet ended
     int kept_nb = 0;
     uint64_t perm = 0;              // kept columns holding verified permutations (see Workspace)
 };
@@ -2119,6 +2120,7 @@ int dml_prereduce_end(dml_prereduce* p) {
                   reduce_clears_slots(p->desc.value_type, kPreReduce, p->cols);
         if (rc != DML_OK) W.kept = false;
         (void)hipEventRecord(W.free_ev, x->xstream);
+        W.busy = false;
         prereduce_free(p);
         return rc;
     }
@@ -2227,6 +2229,10 @@ int dml_prereduce_begin_ctx(dml_prectx* x, const void* const* dev_bufs, const in
         return set_err(DML_E_INVALID_ARG, "bad pre-reduce arguments (n must be <= 64)");
     std::lock_guard<std::mutex> lk(x->mu);
     DeviceGuard g(x->device);
+    // the ring's next workspace must have been ended: a call still holding it would
+    // have its Ctrl and slot table rewritten under its pieces
+    if (x->ws[x->next].busy)
+        return set_err(DML_E_INVALID_ARG, "three calls of this pre-reduce context are outstanding: end one first");
     auto* p = new (std::nothrow) dml_prereduce();
     if (!p) return set_err(DML_E_NOMEM, "out of host memory");
     p->desc = x->desc;
@@ -2277,6 +2283,7 @@ int dml_prereduce_begin_ctx(dml_prectx* x, const void* const* dev_bufs, const in
     if (e == hipSuccess && !(W.clean || W.kept)) e = hipMemsetAsync(W.rowflag, 0, (size_t)x->rows * sizeof(uint32_t), st);
     W.clean = W.kept = false;
     W.used = true;
+    W.busy = true;
     if (e == hipSuccess && p->spec) {
         e = launch_ident_check(p->bt, n, p->stride, p->K, x->first, x->rows, W.slot, W.ctrl, st);
         if (e == hipSuccess && p->bt.kept_cols) e = launch_assign_cols(W.ctrl, n, st);
@@ -2293,6 +2300,7 @@ int dml_prereduce_begin_ctx(dml_prectx* x, const void* const* dev_bufs, const in
     if (e != hipSuccess) {
         (void)hipStreamSynchronize(st);
         (void)hipEventRecord(W.free_ev, st);
+        W.busy = false;
         prereduce_free(p);
         return set_err(DML_E_HIP, hipGetErrorString(e));
     }

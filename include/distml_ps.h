@@ -307,7 +307,9 @@ int dml_prereduce_kernel_time(double* ms, int64_t* launches, int32_t reset);
  * table, full key index, every piece as launched) on the context's stream and
  * sets *rerun. Consume the partial (reduce-scatter) only after verify, behind
  * dml_prereduce_stream_wait; _end then reports the call's errors as before.
- * dml_prectx_stats counts calls as dml_store_stats counts chunks. */
+ * dml_prectx_stats counts calls as dml_store_stats counts chunks. At most three
+ * calls of one context may be outstanding (begun and not yet ended): a fourth
+ * _begin_ctx returns DML_E_INVALID_ARG instead of reusing a busy workspace. */
 typedef struct dml_prectx dml_prectx;
 int dml_prectx_create(const dml_desc* desc, int64_t first_key, int64_t rows, int32_t cols, int32_t device,
                       dml_prectx** out);

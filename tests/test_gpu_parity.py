@@ -2162,3 +2162,35 @@ def test_flat_kernel_widths_exact(oracle, vt, cols):
             assert o.push(h) == 0
     s.flush()
     assert kat.bits_equal(s.values(), o.data)
+
+
+def test_prectx_refuses_a_fourth_outstanding_call(oracle):
+    """A pre-reduce context's ring holds three workspaces: a fourth
+    _begin_ctx while three calls are begun and not ended is refused instead of
+    rewriting a workspace under its pieces; once one ends, the next call proceeds."""
+    from distml_amd import DataDesc, NativeError
+    from distml_amd.group import HipOps
+    rows, cols = 512, 64
+    fmt = DataDesc(1, 0, 1)
+    ops = HipOps()
+    ctx = ops.ctx_create(fmt, 0, rows, cols, 0)
+    push = torch.from_numpy(oracle.synth_dense_bucket(0, 1, 0, rows, rows, cols, 5, 1, 0)).cuda()
+    part = torch.zeros(rows * cols, dtype=torch.float32, device="cuda")
+    st = torch.cuda.current_stream().cuda_stream
+    torch.cuda.synchronize()
+    hs = [ops.begin_ctx(ctx, [push.data_ptr()], [push.numel()], st) for _ in range(3)]
+    with pytest.raises(NativeError):
+        ops.begin_ctx(ctx, [push.data_ptr()], [push.numel()], st)
+    for h in hs[:1]:
+        ops.piece(h, rows, rows, 0, rows, part.data_ptr(), st)
+        ops.verify(h)
+        ops.end(h)
+    h = ops.begin_ctx(ctx, [push.data_ptr()], [push.numel()], st)
+    for h2 in hs[1:] + [h]:
+        ops.piece(h2, rows, rows, 0, rows, part.data_ptr(), st)
+        ops.verify(h2)
+        ops.end(h2)
+    torch.cuda.synchronize()
+    want = oracle.synth_dense_bucket(0, 1, 0, rows, rows, cols, 5, 1, 0).reshape(rows, -1)[:, 4:].copy().view("<f4")
+    assert part.view(rows, cols).cpu().numpy().tobytes() == want.tobytes()
+    ops.ctx_destroy(ctx)
