@@ -426,7 +426,8 @@ def headline(ctx: Ctx, L, args, out_line: dict):
         timed_store = store
         algo_per_rank = W * BUCKET + 2 * SHARD
     else:
-        group = ShardGroup(fmt, ROWS, COLS, rank, world, device=ctx.local, pieces=args.pieces)
+        group = ShardGroup(fmt, ROWS, COLS, rank, world, device=ctx.local, pieces=args.pieces,
+                           emulate_world=args.emulate_rs)
         bufs = make_buckets(L, torch, fmt, W, ROWS) + make_buckets(L, torch, fmt, W, ROWS, value_seed=5000)
         sets = [([b.data_ptr() for b in bs], [b.numel() for b in bs]) for bs in (bufs[:W], bufs[W:])]
         st = torch.cuda.current_stream().cuda_stream
@@ -508,7 +509,9 @@ def headline(ctx: Ctx, L, args, out_line: dict):
         "config": {"workload": "config2: dense fp32 reduce, 32 device-resident pushes x 64 MiB "
                                "([int32 key][1024 x f32] x 16384) -> 16384x1024 fp32 model per GPU",
                    "pushes_per_gpu": W, "push_bytes": BUCKET, "model_rows": ROWS, "cols": COLS,
-                   "parallelism": ("single shard" if not sharded else f"linearSplit({world}) + RCCL reduce-scatter"),
+                   "parallelism": ("single shard" if not sharded else f"linearSplit({world}) + RCCL reduce-scatter"
+                                   + (f" (DIAGNOSTIC: owner-side footprint of {args.emulate_rs} ranks emulated, "
+                                      "results not valid)" if args.emulate_rs else "")),
                    "pushes": "16 ascending + 16 permuted per step; two bucket sets stepped alternately "
                              "(same key order per push position, different values)",
                    "algorithmic_bytes_per_step_per_gpu": algo_per_rank},
@@ -1173,6 +1176,9 @@ def main():
     ap.add_argument("--alloc-seed", type=int, default=0, help=argparse.SUPPRESS)
     ap.add_argument("--one-slab", action="store_true", help=argparse.SUPPRESS)
     ap.add_argument("--shuffle-only", choices=["", "asc", "perm"], default="", help=argparse.SUPPRESS)
+    ap.add_argument("--emulate-rs", type=int, default=0,
+                    help="diagnostic with --group at N = 1: the owner-side HBM footprint of an N-rank "
+                         "reduce-scatter + 1/N apply (results not valid)")
     ap.add_argument("--native-group", action="store_true",
                     help="also run the config-2 workload through dml_group at N = 1 (always at N > 1)")
     ap.add_argument("--group", action="store_true",

@@ -125,7 +125,7 @@ class HipOps:
 class ShardGroup:
     def __init__(self, fmt: DataDesc, total_rows: int, cols: int, rank: int, world: int,
                  device: Optional[int] = None, ops=None, store_factory=None, pieces: int = 1,
-                 reduce_scatter=None, exchange_only: bool = False):
+                 reduce_scatter=None, exchange_only: bool = False, emulate_world: int = 0):
         import torch
         import torch.distributed as dist
         self.torch, self.dist = torch, dist
@@ -155,6 +155,13 @@ class ShardGroup:
         # pre-reduce, and one launch per call has no per-piece tails (world 1, config 2:
         # 0.441 ms/step against 0.460 for P = 4 and 0.461 for P = 2)
         self.pieces = pieces
+        # diagnostic (bench.py --emulate-rs, world 1 only): replace the local shortcut by
+        # the HBM footprint an N-rank call has at its owner — a reduction on the comm
+        # stream that reads the whole partial and writes 1/N of it, then the apply of
+        # 1/N of the shard. The shard's values are then NOT the reduce's result.
+        if emulate_world > 1 and (world != 1 or self.shard.size() % emulate_world or pieces != 1):
+            raise ValueError("emulate_world needs world 1, pieces 1 and rows divisible by it")
+        self.emulate_world = emulate_world
         self._pending: list = []  # (pre-reduce handle, buffer set) not yet reduce-scattered / checked
         self._pctx = None         # speculative pre-reduce context (dml_prectx), created on first use
         self._xbufs: list = []    # exchange buffers the store may still read: (event, recv, send, push seq)
@@ -292,12 +299,20 @@ class ShardGroup:
                              partial[j * world * blk * cols:(j + 1) * world * blk * cols])
             if failed is not None:
                 raise failed
+            apply_elems = self.shard.size() * cols
+            if self.emulate_world > 1:
+                E = self.emulate_world
+                n = partial.numel() // E
+                recv = self._recvs[k]
+                with torch.cuda.stream(self.comm):
+                    torch.sum(partial.view(E, n), dim=0, out=recv[:n])
+                apply_elems = n
             self._rs_done[k].record(self.comm)
             if self._store_stream is not None:
                 self._store_stream.wait_event(self._rs_done[k])
             else:
                 self.comm.synchronize()
-            self.ops.apply(self.store, recv.data_ptr(), self.shard.size() * cols)
+            self.ops.apply(self.store, recv.data_ptr(), apply_elems)
             if self._store_stream is not None:
                 self._applied[k].record(self._store_stream)
         finally:
