@@ -299,20 +299,26 @@ class ShardGroup:
                              partial[j * world * blk * cols:(j + 1) * world * blk * cols])
             if failed is not None:
                 raise failed
-            apply_elems = self.shard.size() * cols
             if self.emulate_world > 1:
                 E = self.emulate_world
                 n = partial.numel() // E
                 recv = self._recvs[k]
                 with torch.cuda.stream(self.comm):
                     torch.sum(partial.view(E, n), dim=0, out=recv[:n])
-                apply_elems = n
+                self._rs_done[k].record(self.comm)
+                if not hasattr(self, "_emu_rows"):
+                    self._emu_rows = torch.zeros(n, dtype=partial.dtype, device=partial.device)
+                with torch.cuda.stream(self._store_stream):  # the 1/N owner apply's bytes
+                    self._store_stream.wait_event(self._rs_done[k])
+                    self._emu_rows.add_(recv[:n])
+                self._applied[k].record(self._store_stream)
+                return
             self._rs_done[k].record(self.comm)
             if self._store_stream is not None:
                 self._store_stream.wait_event(self._rs_done[k])
             else:
                 self.comm.synchronize()
-            self.ops.apply(self.store, recv.data_ptr(), apply_elems)
+            self.ops.apply(self.store, recv.data_ptr(), self.shard.size() * cols)
             if self._store_stream is not None:
                 self._applied[k].record(self._store_stream)
         finally:
