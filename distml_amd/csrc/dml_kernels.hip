@@ -530,6 +530,19 @@ __global__ __launch_bounds__(64 * WPB) void k_reduce(T* __restrict__ shard, int6
 }
 
 // ---------------------------------------------------------------------------
+// Blocks are dealt to the 8 XCDs round robin (block b on XCD b % 8), each XCD with
+// its own L2. xcd_block() renumbers them so that XCD x runs the x-th contiguous run
+// of block indices, in dispatch order: neighbouring blocks' data meets in one L2.
+// A bijection on [0, gridDim.x) for any grid size.
+#ifndef DML_AB_XCDF
+#define DML_AB_XCDF 0
+#endif
+__device__ inline int64_t xcd_block() {
+    const int64_t nbk = gridDim.x, b = blockIdx.x, per = (nbk + 7) / 8, x = b % 8, i = b / 8;
+    const int64_t full = nbk - (per - 1) * 8;  // XCDs 0..full-1 hold `per` blocks, the others per - 1
+    return x < full ? x * per + i : full * per + (x - full) * (per - 1) + i;
+}
+
 // k_reduce_rows: the plain-sum shapes (kAdd, kAddCheckI32, kPreReduce) with
 // RPW neighbouring rows per wave. One push at a time: the wave scalar-loads the
 // push's base / index and its RPW slots, issues RPW x CPW 16-B nt loads (16 for
@@ -551,7 +564,11 @@ __global__ __launch_bounds__(64 * WPB) void k_reduce_rows(T* __restrict__ shard,
     static_assert(MODE == kAdd || MODE == kAddCheckI32 || MODE == kPreReduce, "plain-sum modes only");
     const int lane = threadIdx.x & 63;
     const int wid = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-    const int64_t task = (int64_t)blockIdx.x * WPB + wid;
+    // DEPTH 3 (rows that are not whole lines, e.g. config 5's 4000-B rows): XCD-
+    // contiguous blocks, so the line two neighbouring rows share is written from one
+    // L2 (config 5 0.635 -> 0.653 of 8 TB/s, 3 rounds on one box)
+    const int64_t blk = DEPTH == 3 ? xcd_block() : (int64_t)blockIdx.x;
+    const int64_t task = blk * WPB + wid;
     const int64_t ntask = (rows + RPW - 1) / RPW * (int64_t)ngroups;
     if (task >= ntask) return;
     if (bt.prev && ctrl_abnormal(bt.prev)) return;  // predecessor needs the host first
@@ -958,7 +975,7 @@ __global__ __launch_bounds__(256) void k_reduce_flat(T* __restrict__ shard, int6
     __shared__ int32_t s_slot[4][RMAX * kMaxW];  // per wave: [row][push], -1 = no record / skipped row
     const int lane = threadIdx.x & 63;
     const int wid = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-    const int64_t t0 = ((int64_t)blockIdx.x * 4 + wid) * R;  // first task row of the wave
+    const int64_t t0 = ((DML_AB_XCDF ? xcd_block() : (int64_t)blockIdx.x) * 4 + wid) * R;  // first task row of the wave
     if (t0 >= rows) return;
     if (bt.prev && ctrl_abnormal(bt.prev)) return;  // predecessor needs the host first
     uint64_t cut = ctrl->cutoff;
@@ -1137,7 +1154,7 @@ __global__ __launch_bounds__(256) void k_ada_flat(float* __restrict__ shard, int
     __shared__ int32_t s_slot[4][RMAX * kMaxW];  // per wave: [row][push], -1 = no record / skipped row
     const int lane = threadIdx.x & 63;
     const int wid = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-    const int64_t t0 = ((int64_t)blockIdx.x * 4 + wid) * R;  // first row of the wave
+    const int64_t t0 = ((DML_AB_XCDF ? xcd_block() : (int64_t)blockIdx.x) * 4 + wid) * R;  // first row of the wave
     float cand_v = 0.f;
     uint64_t cand_p = kNoPos;
     bool cand_ok = false;

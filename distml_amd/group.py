@@ -159,7 +159,8 @@ class ShardGroup:
         # the HBM footprint an N-rank call has at its owner — a reduction on the comm
         # stream that reads the whole partial and writes 1/N of it, then the apply of
         # 1/N of the shard. The shard's values are then NOT the reduce's result.
-        if emulate_world > 1 and (world != 1 or self.shard.size() % emulate_world or pieces != 1):
+        # emulate_world -1: neither the reduction nor the apply (the pieces alone)
+        if emulate_world and (world != 1 or pieces != 1 or (emulate_world > 1 and self.shard.size() % emulate_world)):
             raise ValueError("emulate_world needs world 1, pieces 1 and rows divisible by it")
         self.emulate_world = emulate_world
         self._pending: list = []  # (pre-reduce handle, buffer set) not yet reduce-scattered / checked
@@ -299,6 +300,9 @@ class ShardGroup:
                              partial[j * world * blk * cols:(j + 1) * world * blk * cols])
             if failed is not None:
                 raise failed
+            if self.emulate_world < 0:
+                self._rs_done[k].record(self.comm)
+                return
             if self.emulate_world > 1:
                 E = self.emulate_world
                 n = partial.numel() // E
