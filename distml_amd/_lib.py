@@ -33,7 +33,8 @@ class dml_desc(C.Structure):
 class dml_store_counters(C.Structure):
     """Mirror of dml_store_counters (dml_store_stats)."""
     _fields_ = [("chunks", C.c_int64), ("spec_chunks", C.c_int64), ("spec_reruns", C.c_int64),
-                ("identity_pushes", C.c_int64), ("reused_pushes", C.c_int64), ("indexed_pushes", C.c_int64)]
+                ("identity_pushes", C.c_int64), ("reused_pushes", C.c_int64), ("indexed_pushes", C.c_int64),
+                ("sparse_big_chunks", C.c_int64), ("sparse_replays", C.c_int64)]
 
 
 # Every symbol include/distml_ps.h declares, with its ctypes signature.

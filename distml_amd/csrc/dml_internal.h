@@ -204,6 +204,9 @@ hipError_t launch_synth_sparse(uint8_t* out, int K, int vtype, int value_stride,
 constexpr int kSpTile = 4096;      // records per partition tile (256 threads x 16)
 constexpr int kSpLeafCap = 2048;   // records one leaf orders in LDS
 constexpr uint32_t kSpSkip = 0xFFFFFFFFu;  // sequence of a record at or past the cutoff (never applied)
+constexpr int kSpBigCap = 12288;   // records a big leaf orders in LDS (one-level partition)
+constexpr int kSpBigBins = 4096;   // big leaves per chunk, at most (the one-level pass's LDS histogram)
+constexpr int kSpSlices = 8;       // regions per big leaf: slice x holds the pushes p with p % 8 == x
 // Shape of one chunk's partition (host-computed, passed by value).
 struct SpPlan {
     int64_t tile_base[kMaxW + 1];  // first level-1 tile of push b (prefix of ceil(nrec / kSpTile))
@@ -221,6 +224,13 @@ struct SpPlan {
     // exact replay, which re-partitions with full sequence numbers)
     int compact;
     uint32_t seq_cut;              // records with sequence >= seq_cut are at / past the cutoff
+    // one-level partition (compact fp32, pushes balanced over the 8 slices): "big
+    // leaves" of 2^BL rows, one region of capS records per (big leaf, slice), filled
+    // by the slice's tiles (pushes p % 8 == x, run by the blocks of XCD x); the leaf
+    // kernel orders a big leaf's records in LDS, so there is no second pass
+    int big, BL;
+    int64_t nbig, capS, tiles_per_slice;
+    int64_t sbase[kMaxW];          // tiles of the earlier pushes of push b's slice
 };
 constexpr int kSpCompactRowBits = 26;  // SL + D2 limit of the compact word
 // Pinned status of a single-pass partition, read by the host before the leaf launch.
@@ -238,9 +248,15 @@ struct SpMeta {
 // Byte offsets of the partition buffers inside one workspace allocation.
 struct SpLayout {
     size_t meta, comp1, val1, comp2, val2, cnt1, off1, cnt2, off2, leafflag, bounds, scan_tmp, scan_tmp_bytes,
-        cur1, cur2, stat, total;
+        cur1, cur2, stat, big, curS, total;
 };
 SpPlan sparse_plan(const Batch& bt, int nb, int64_t rows);
+// The one-level partition where it applies (compact fp32 plan, >= 8 pushes balanced
+// over the slices, big leaves of 2 K - 8.7 K records on average): sets pl.big.
+void sparse_plan_big(SpPlan& pl, const Batch& bt, int64_t rows);
+hipError_t launch_sparse_partition_big(const Batch& bt, const SpPlan& pl, const SpLayout& l, uint8_t* ws,
+                                       int64_t stride, int K, int64_t first, int64_t rows, Ctrl* ctrl,
+                                       uint64_t tail_cut, SpStat* hstat, hipStream_t st);
 SpLayout sparse_layout(const SpPlan& pl, int vbytes);
 hipError_t launch_sparse_partition(int vtype, const Batch& bt, const SpPlan& pl, const SpLayout& l, uint8_t* ws,
                                    int64_t stride, int K, int64_t first, int64_t rows, Ctrl* ctrl,

@@ -332,10 +332,11 @@ constexpr bool kIntLeaf = sizeof(T) == 4 && T(0.5) == T(0);
 // value bits, ordered within a row by push.
 template <bool CMP>
 struct LeafRec {
-    uint64_t rowb0;     // CMP: first row of the leaf's level-1 bin
+    uint64_t rowb0;     // CMP: first row of the leaf's level-1 bin (or big leaf)
     uint32_t seq_cut;   // full records: sequences at / past it are never applied
-    __device__ uint64_t row(uint64_t c) const { return CMP ? rowb0 + (c >> 38) : c >> 32; }
-    __device__ uint64_t key(uint64_t c) const { return CMP ? c >> 32 : c; }  // add order within a row
+    uint64_t kmask = ~0ull;  // CMP: the (row, push) bits of c >> 32 (a big leaf keeps flags above them)
+    __device__ uint64_t row(uint64_t c) const { return CMP ? rowb0 + ((c >> 38) & (kmask >> 6)) : c >> 32; }
+    __device__ uint64_t key(uint64_t c) const { return CMP ? (c >> 32) & kmask : c; }  // add order within a row
     __device__ bool applied(uint64_t c) const { return CMP || (uint32_t)c < seq_cut; }
 };
 
@@ -740,11 +741,260 @@ __global__ __launch_bounds__(256) void k_sp_pack_flagged(const uint32_t* __restr
     }
 }
 
+// ---- one-level partition: big leaves sorted in LDS (no second pass) -------------
+// k_sp_l1_big: as k_sp_l1_fast, with up to kSpBigBins big leaves of 2^BL rows as its
+// bins (the LDS histogram holds them all) and one region per (big leaf, slice). The
+// grid is slice-major: block b runs on XCD b % 8 (the dispatcher deals blocks round
+// robin) and takes the (b / 8)-th tile of the pushes p with p % 8 == b % 8, so every
+// region is written from one XCD and the runs that tiles append to it meet in that
+// XCD's L2 (scripts/ubench_l1.hip: 3 815 bins x 8 slices 303 us against 440 us with
+// one region per bin written from every XCD, for 32 M random keys).
+__global__ __launch_bounds__(256) void k_sp_l1_big(const Batch bt, const SpPlan pl, int64_t stride, int K,
+                                                   int64_t first, int64_t rows, Ctrl* __restrict__ ctrl,
+                                                   uint64_t tail_cut, uint32_t* __restrict__ curS,
+                                                   uint64_t* __restrict__ comp, SpStat* __restrict__ stat) {
+    __shared__ uint32_t h[kSpBigBins];  // records per big leaf, then this tile's base in its region
+    const int tid = threadIdx.x;
+    if (blockIdx.x == 0 && tid == 0 && tail_cut != kNoPos) atomicMin(&ctrl->cutoff, (unsigned long long)tail_cut);
+    const int x = (int)(blockIdx.x % kSpSlices);
+    const int64_t ti = blockIdx.x / kSpSlices;
+    int b = -1;
+    int64_t tin = 0;
+    for (int p = x; p < pl.nb; p += kSpSlices) {  // <= 8 pushes per slice
+        const int64_t t = pl.tile_base[p + 1] - pl.tile_base[p];
+        if (ti < pl.sbase[p] + t) {
+            b = p;
+            tin = ti - pl.sbase[p];
+            break;
+        }
+    }
+    if (b < 0) return;  // uniform: past this slice's tiles
+    for (int j = tid; j < pl.nbig; j += 256) h[j] = 0u;
+    __syncthreads();
+    const int64_t r0 = tin * kSpTile + tid;
+    const int64_t n = bt.nrec[b];
+    const uint8_t* base_b = bt.base[b];
+    constexpr int kPer = kSpTile / 256;
+    int64_t key[kPer];
+    float u[kPer];
+#pragma unroll
+    for (int i = 0; i < kPer; ++i) {
+        const int64_t r = min(r0 + i * 256, n - 1);
+        key[i] = ld_key(base_b + r * stride, K);
+        u[i] = Elem<float>::load(base_b + r * stride + K);
+    }
+    uint64_t bad = kNoPos;
+    int64_t row[kPer];
+    uint32_t rank[kPer];
+#pragma unroll
+    for (int i = 0; i < kPer; ++i) {
+        const int64_t r = r0 + i * 256;
+        row[i] = -1;
+        if (r >= n) continue;
+        row[i] = row_index(key[i], first, rows);
+        if (row[i] < 0) {
+            bad = min(bad, pos_of((uint64_t)bt.bidx[b], (uint64_t)(r * stride)));
+            continue;
+        }
+        rank[i] = atomicAdd(&h[(uint32_t)(row[i] >> pl.BL)], 1u);
+    }
+    if (bad != kNoPos) atomicMin(&ctrl->cutoff, (unsigned long long)bad);
+    __syncthreads();
+    for (int j = tid; j < pl.nbig; j += 256) {
+        const uint32_t c = h[j];
+        if (!c) continue;
+        const uint32_t at = atomicAdd(&curS[(int64_t)x * pl.nbig + j], c);
+        if ((int64_t)at + c > pl.capS) stat->overflow = 1u;
+        h[j] = at;
+    }
+    __syncthreads();
+#pragma unroll
+    for (int i = 0; i < kPer; ++i) {
+        if (row[i] < 0) continue;
+        const int64_t B = row[i] >> pl.BL;
+        const int64_t q = (int64_t)h[B] + rank[i];
+        if (q >= pl.capS) continue;
+        comp[(B * kSpSlices + x) * pl.capS + q] = ((uint64_t)(row[i] - (B << pl.BL)) << 38) | ((uint64_t)b << 32) |
+                                                  (uint64_t)__float_as_uint(u[i]);
+    }
+}
+
+// k_sp_leaf_big: k_sp_leaf's ordered apply for one big leaf (up to kSpBigCap compact
+// records from its 8 slice regions): counting sort over kSpBigLines line buckets,
+// ownership, one RMW per touched row. One 16-wave block per CU (136 KB of LDS); a
+// record's own / repeated flags go into bits 62-63 of its LDS word (above the row
+// and push bits) instead of a separate array.
+constexpr int kSpBigThreads = 1024;
+constexpr int kSpBigLines = 2 * kSpBigThreads;
+__global__ __launch_bounds__(kSpBigThreads) void k_sp_leaf_big(float* __restrict__ shard,
+                                                               const uint32_t* __restrict__ curS, int64_t nbig,
+                                                               int64_t capS, const uint64_t* __restrict__ comp, int BL,
+                                                               int bshift, uint8_t* __restrict__ leafflag,
+                                                               Ctrl* __restrict__ ctrl, const Ctrl* __restrict__ prev) {
+    constexpr int kT = kSpBigThreads;
+    constexpr int kPer = kSpBigCap / kT;
+    __shared__ uint64_t sc[kSpBigCap];
+    __shared__ uint16_t perm[kSpBigCap];
+    __shared__ uint32_t bstart[kSpBigLines + 1];
+    __shared__ uint32_t cur[kSpBigLines];
+    __shared__ uint32_t wsum[kT / 64];
+    __shared__ int s_over;
+    if (prev && ctrl_abnormal(prev)) return;  // predecessor needs the host first
+    const int tid = threadIdx.x;
+    const int64_t B = blockIdx.x;
+    int64_t pre[kSpSlices + 1];
+    pre[0] = 0;
+#pragma unroll
+    for (int x = 0; x < kSpSlices; ++x) pre[x + 1] = pre[x] + min((int64_t)curS[(int64_t)x * nbig + B], capS);
+    const int n = (int)pre[kSpSlices];
+    if (n <= 0) return;
+    if (n > kSpBigCap) {  // skewed big leaf: exact replay on the host's request
+        if (tid == 0) {
+            leafflag[B] = 1;
+            atomicAnd(&ctrl->no_dup, 0u);
+        }
+        return;
+    }
+    const uint64_t row0 = (uint64_t)B << BL;
+    LeafRec<true> lr;
+    lr.rowb0 = row0;
+    lr.seq_cut = kSpSkip;
+    lr.kmask = ((uint64_t)1 << (BL + 6)) - 1;  // row within the big leaf | push
+    for (int i = tid; i < kSpBigLines; i += kT) cur[i] = 0;
+    if (tid == 0) s_over = 0;
+    uint64_t c[kPer];
+    float x0[kPer];
+    uint32_t bk[kPer];
+#pragma unroll
+    for (int k = 0; k < kPer; ++k) {
+        const int i = min(tid + k * kT, n - 1);
+        int x = 0;
+#pragma unroll
+        for (int y = 1; y < kSpSlices; ++y) x += i >= pre[y] ? 1 : 0;
+        c[k] = comp[(B * kSpSlices + x) * capS + (i - pre[x])];
+    }
+#pragma unroll
+    for (int k = 0; k < kPer; ++k) x0[k] = shard[lr.row(c[k])];  // in flight under the sort
+#pragma unroll
+    for (int k = 0; k < kPer; ++k) bk[k] = (uint32_t)((lr.row(c[k]) - row0) >> bshift);
+    __syncthreads();
+#pragma unroll
+    for (int k = 0; k < kPer; ++k) {
+        const int i = tid + k * kT;
+        if (i < n) {
+            sc[i] = c[k];
+            atomicAdd(&cur[bk[k]], 1u);
+        }
+    }
+    __syncthreads();
+    {  // exclusive scan of the bucket counts: thread t owns buckets 2t, 2t+1
+        const uint32_t a0 = cur[2 * tid], a1 = cur[2 * tid + 1];
+        uint32_t x = a0 + a1;
+        const int lane = tid & 63, wave = tid >> 6;
+#pragma unroll
+        for (int o = 1; o < 64; o <<= 1) {
+            const uint32_t y = __shfl_up(x, o);
+            if (lane >= o) x += y;
+        }
+        if (lane == 63) wsum[wave] = x;
+        __syncthreads();
+        uint32_t base = 0;
+        for (int w = 0; w < wave; ++w) base += wsum[w];
+        const uint32_t ex = base + x - (a0 + a1);
+        bstart[2 * tid] = ex;
+        bstart[2 * tid + 1] = ex + a0;
+        __syncthreads();
+        cur[2 * tid] = ex;
+        cur[2 * tid + 1] = ex + a0;
+        if (tid == 0) bstart[kSpBigLines] = (uint32_t)n;
+        __syncthreads();
+    }
+#pragma unroll
+    for (int k = 0; k < kPer; ++k) {
+        const int i = tid + k * kT;
+        if (i < n) perm[atomicAdd(&cur[bk[k]], 1u)] = (uint16_t)i;
+    }
+    __syncthreads();
+    // ownership, in address order: sorted position p = tid + k * kT
+    int ri[kPer];
+    uint32_t fl[kPer];  // bit 0 owns its row, bit 1 row repeated
+#pragma unroll
+    for (int k = 0; k < kPer; ++k) {
+        const int p = tid + k * kT;
+        fl[k] = 0;
+        ri[k] = 0;
+        if (p >= n) continue;
+        const int i = perm[p];
+        ri[k] = i;
+        const uint64_t ci = sc[i], row = lr.row(ci), ki = lr.key(ci);
+        const uint32_t b = (uint32_t)((row - row0) >> bshift);
+        const uint32_t bs = bstart[b], be = bstart[b + 1];
+        if (be - bs > (uint32_t)kSpBucketMax) s_over = 1;
+        bool first = true, dup = false;
+        for (uint32_t q = bs; q < be; ++q) {
+            const int j = perm[q];
+            const uint64_t cj = sc[j];
+            if (j != i && lr.row(cj) == row) {
+                const uint64_t kj = lr.key(cj);
+                dup = true;
+                first &= kj > ki;
+                if (kj == ki) s_over = 1;  // one push lists the row twice: the replay orders it
+            }
+        }
+        fl[k] = (first ? 1u : 0u) | (dup ? 2u : 0u);
+    }
+    __syncthreads();  // every ownership read of sc is done: the flags go above the key bits
+#pragma unroll
+    for (int k = 0; k < kPer; ++k)
+        if (tid + k * kT < n) sc[ri[k]] |= (uint64_t)fl[k] << 62;
+    __syncthreads();
+    if (s_over) {  // uniform
+        if (tid == 0) {
+            leafflag[B] = 1;
+            atomicAnd(&ctrl->no_dup, 0u);
+        }
+        return;
+    }
+#pragma unroll
+    for (int k = 0; k < kPer; ++k) {
+        const int i = tid + k * kT;
+        if (i >= n) continue;
+        const uint64_t ci = sc[i];
+        const uint32_t f = (uint32_t)(ci >> 62);
+        if (!(f & 1u)) continue;
+        const uint64_t row = lr.row(ci);
+        float xv = x0[k];
+        if (!(f & 2u)) {
+            xv = Elem<float>::add(xv, __uint_as_float((uint32_t)ci));
+        } else {
+            uint32_t rn = kSpSkip;
+            xv = leaf_chain<float, true>(xv, row, row0, bshift, bstart, perm, sc, (const float*)nullptr, lr, &rn);
+        }
+        shard[row] = xv;
+    }
+}
+
 // ---- host side ----------------------------------------------------------------
 static int ceil_log2(int64_t x) {
     int r = 0;
     while ((int64_t)1 << r < x) ++r;
     return r;
+}
+
+// The SL-dependent fields of a plan (leaf = row >> SL; two 256-way digits).
+static void plan_leaves(SpPlan& pl, int64_t rows, int SL) {
+    pl.SL = SL;
+    pl.nleaves = (rows + ((int64_t)1 << SL) - 1) >> SL;
+    pl.D2 = std::min(8, ceil_log2(pl.nleaves));
+    pl.nbins1 = (int)((pl.nleaves + ((int64_t)1 << pl.D2) - 1) >> pl.D2);
+    pl.max_tiles2 = (pl.nrec + kSpTile - 1) / kSpTile + pl.nbins1;
+    // single-pass layout: cap1 records per level-1 bin (twice the mean + one tile;
+    // config 3's lattice keys put up to 1.4x the mean into one bin, skewed keys
+    // overflow and take the counted partition), cap2 per leaf (twice the mean + 256,
+    // at most what the leaf kernel orders)
+    pl.cap1 = (pl.nrec / std::max(pl.nbins1, 1)) * 2 + kSpTile;
+    pl.cap2 = std::min<int64_t>(kSpLeafCap, 2 * (pl.nrec / std::max<int64_t>(pl.nleaves, 1)) + 256);
+    pl.tiles2_per_bin = (pl.cap1 + kSpTile - 1) / kSpTile;
 }
 
 SpPlan sparse_plan(const Batch& bt, int nb, int64_t rows) {
@@ -766,22 +1016,45 @@ SpPlan sparse_plan(const Batch& bt, int nb, int64_t rows) {
     int SL = 0;
     while (SL < 31 && (double)((int64_t)1 << (SL + 1)) <= span) ++SL;
     while (SL < 31 && ((rows + ((int64_t)1 << SL) - 1) >> SL) > 65536) ++SL;
-    pl.SL = SL;
-    pl.nleaves = (rows + ((int64_t)1 << SL) - 1) >> SL;
-    pl.D2 = std::min(8, ceil_log2(pl.nleaves));
-    pl.nbins1 = (int)((pl.nleaves + ((int64_t)1 << pl.D2) - 1) >> pl.D2);
-    pl.max_tiles2 = (nrec + kSpTile - 1) / kSpTile + pl.nbins1;
-    // single-pass layout: a bin holds twice its expected share + one tile (config
-    // 3's lattice keys put up to 1.4x the mean into one bin; skewed keys overflow
-    // and take the counted partition); a leaf holds what the leaf kernel can order.
-    // single-pass layout: cap1 records per level-1 bin (twice the mean + one tile),
-    // cap2 per leaf (twice the mean + 256, at most what the leaf kernel orders)
-    pl.cap1 = (nrec / std::max(pl.nbins1, 1)) * 2 + kSpTile;
-    pl.cap2 = std::min<int64_t>(kSpLeafCap, 2 * (nrec / std::max<int64_t>(pl.nleaves, 1)) + 256);
-    pl.tiles2_per_bin = (pl.cap1 + kSpTile - 1) / kSpTile;
+    plan_leaves(pl, rows, SL);
     pl.fast = 1;
     pl.seq_cut = kSpSkip;
     return pl;
+}
+
+// One-level partition: big leaves of 2^BL rows, as few as fit the
+// one-level pass's LDS histogram (<= kSpBigBins), holding 2 K - 8.7 K records on
+// average (kSpBigCap orders up to 12 288: config 3's lattice keys put 1.41x the
+// mean, 11 790, into its fullest big leaf). The 8 slices (pushes p % 8) must carry
+// near-equal shares, since slice x's tiles all run on one XCD.
+void sparse_plan_big(SpPlan& pl, const Batch& bt, int64_t rows) {
+    pl.big = 0;
+    if (!pl.compact || pl.nb < kSpSlices || pl.nrec <= 0) return;
+    int BL = 0;
+    while (BL < 24 && ((rows + ((int64_t)1 << BL) - 1) >> BL) > kSpBigBins) ++BL;
+    const int64_t nbig = (rows + ((int64_t)1 << BL) - 1) >> BL;
+    const int64_t mean = pl.nrec / nbig;
+    // the LDS word: value | push << 32 | row within the big leaf << 38 | flags << 62
+    if (BL > 24 || mean < 2048 || mean > 8704) return;
+    int64_t srec[kSpSlices] = {0}, stile[kSpSlices] = {0};
+    for (int b = 0; b < pl.nb; ++b) {
+        pl.sbase[b] = stile[b % kSpSlices];
+        stile[b % kSpSlices] += pl.tile_base[b + 1] - pl.tile_base[b];
+        srec[b % kSpSlices] += bt.nrec[b];
+    }
+    int64_t smax = 0, tmax = 0;
+    for (int x = 0; x < kSpSlices; ++x) {
+        smax = std::max(smax, srec[x]);
+        tmax = std::max(tmax, stile[x]);
+    }
+    if (smax * kSpSlices > pl.nrec * 5 / 4) return;  // unbalanced slices: one XCD would do most of the work
+    pl.BL = BL;
+    pl.nbig = nbig;
+    pl.tiles_per_slice = tmax;
+    // a region holds twice the slice's mean share of a big leaf + 512 (pushes spread
+    // their keys: config 3's regions peak at 1.1x the mean); overflow -> counted partition
+    pl.capS = 2 * (smax / nbig) + 512;
+    pl.big = 1;
 }
 
 uint32_t sparse_seq_cut(const SpPlan& pl, const Batch& bt, uint64_t cut, int64_t stride) {
@@ -820,6 +1093,10 @@ SpLayout sparse_layout(const SpPlan& pl, int vbytes) {
     l.off2 = take(cells2 * 4);
     l.leafflag = take((size_t)pl.nleaves);
     l.bounds = take(((size_t)pl.nleaves + 1) * 8);
+    if (pl.big) {
+        l.big = take((size_t)pl.nbig * kSpSlices * (size_t)pl.capS * 8);
+        l.curS = take((size_t)pl.nbig * kSpSlices * 4);
+    }
     size_t t1 = 0, t2 = 0;
     (void)hipcub::DeviceScan::ExclusiveSum(nullptr, t1, (uint32_t*)nullptr, (uint32_t*)nullptr, (int)cells1);
     (void)hipcub::DeviceScan::ExclusiveSum(nullptr, t2, (uint32_t*)nullptr, (uint32_t*)nullptr, (int)cells2);
@@ -929,6 +1206,21 @@ static hipError_t partition_fast_t(const Batch& bt, const SpPlan& pl, const SpLa
     return finish_fast(ws, l, ctrl, hstat, st);
 }
 
+hipError_t launch_sparse_partition_big(const Batch& bt, const SpPlan& pl, const SpLayout& l, uint8_t* ws,
+                                       int64_t stride, int K, int64_t first, int64_t rows, Ctrl* ctrl,
+                                       uint64_t tail_cut, SpStat* hstat, hipStream_t st) {
+    uint32_t* curS = (uint32_t*)(ws + l.curS);
+    SpStat* stat = (SpStat*)(ws + l.stat);
+    hipError_t e = hipMemsetAsync(ws + l.leafflag, 0, (size_t)pl.nbig, st);
+    if (e == hipSuccess) e = hipMemsetAsync(curS, 0, (size_t)pl.nbig * kSpSlices * 4, st);
+    if (e == hipSuccess) e = hipMemsetAsync(stat, 0, sizeof(SpStat), st);
+    if (e != hipSuccess) return e;
+    const dim3 g((unsigned)(pl.tiles_per_slice * kSpSlices));
+    hipLaunchKernelGGL(k_sp_l1_big, g, dim3(256), 0, st, bt, pl, stride, K, first, rows, ctrl, tail_cut, curS,
+                       (uint64_t*)(ws + l.big), stat);
+    return finish_fast(ws, l, ctrl, hstat, st);
+}
+
 hipError_t launch_sparse_partition_fast(int vtype, const Batch& bt, const SpPlan& pl, const SpLayout& l, uint8_t* ws,
                                         int64_t stride, int K, int64_t first, int64_t rows, Ctrl* ctrl,
                                         uint64_t tail_cut, SpStat* hstat, hipStream_t st) {
@@ -962,6 +1254,15 @@ constexpr unsigned leaf_lds_pad() {
 
 hipError_t launch_sparse_leaf(int vtype, void* shard, const SpPlan& pl, const SpLayout& l, uint8_t* ws, Ctrl* ctrl,
                               const Ctrl* prev, hipStream_t st, LaunchEv ev) {
+    if (pl.big) {
+        if (vtype != kF32) return hipErrorInvalidValue;
+        g_kernel_name = "dml::k_sp_leaf_big";
+        const int bshift = pl.BL > 11 ? pl.BL - 11 : 0;  // kSpBigLines = 2^11 line buckets
+        hipExtLaunchKernelGGL(k_sp_leaf_big, dim3((unsigned)pl.nbig), dim3(kSpBigThreads), 0, st, ev.start, ev.stop, 0,
+                              (float*)shard, (const uint32_t*)(ws + l.curS), pl.nbig, pl.capS,
+                              (const uint64_t*)(ws + l.big), pl.BL, bshift, ws + l.leafflag, ctrl, prev);
+        return hipGetLastError();
+    }
     if (pl.nleaves <= 0) return hipSuccess;
     const int64_t* bounds = (const int64_t*)(ws + l.bounds);
     const uint32_t* cnt2 = pl.fast ? (const uint32_t*)(ws + l.cur2) : nullptr;  // fixed-capacity layout
@@ -1007,6 +1308,10 @@ hipError_t sparse_replay(int vtype, void* shard, const SpPlan& pl_in, const SpLa
                          hipStream_t st) {
     hipError_t e = hipSuccess;
     SpPlan pl = pl_in;
+    if (pl.big) {  // the flags are per big leaf: re-partition with leaves of 2^BL rows
+        plan_leaves(pl, rows, pl.BL);
+        pl.big = 0;
+    }
     if (pl.compact) {
         // compact words order a row's adds by push only: re-partition the chunk with
         // full sequence numbers (counted, compact layout), keeping the leaf flags

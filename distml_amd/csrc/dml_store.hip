@@ -538,6 +538,8 @@ int launch_chunk(dml_store* s, Chunk& c, Workspace& W, const Ctrl* prev) {
             c.sp = sparse_plan(c.bt, c.nb, s->rows);
             // one 8-B word per fp32 record through the partition
             c.sp.compact = vt == kF32 && c.sp.SL + c.sp.D2 <= kSpCompactRowBits && c.tail_cut == kNoPos;
+            // big leaves sorted in LDS where they apply: no second partition pass (§4)
+            sparse_plan_big(c.sp, c.bt, s->rows);
             c.spl = sparse_layout(c.sp, s->V);
             if (W.sp_cap < c.spl.total) {
                 HIPCHK(hipStreamSynchronize(s->stream));  // W's previous chunk is retired; be safe
@@ -548,8 +550,12 @@ int launch_chunk(dml_store* s, Chunk& c, Workspace& W, const Ctrl* prev) {
                 W.sp_cap = c.spl.total;
             }
             if (!W.hsp) HIPCHK(hipHostMalloc((void**)&W.hsp, sizeof(SpStat), hipHostMallocDefault));
-            HIPCHK(launch_sparse_partition_fast(vt, c.bt, c.sp, c.spl, W.sp, s->stride, s->K, s->first, s->rows,
-                                                W.ctrl, c.tail_cut, W.hsp, is));
+            if (c.sp.big)
+                HIPCHK(launch_sparse_partition_big(c.bt, c.sp, c.spl, W.sp, s->stride, s->K, s->first, s->rows,
+                                                   W.ctrl, c.tail_cut, W.hsp, is));
+            else
+                HIPCHK(launch_sparse_partition_fast(vt, c.bt, c.sp, c.spl, W.sp, s->stride, s->K, s->first, s->rows,
+                                                    W.ctrl, c.tail_cut, W.hsp, is));
         }
     }
     HIPCHK(hipEventRecord(W.idx_done, is));
@@ -566,6 +572,7 @@ int launch_chunk(dml_store* s, Chunk& c, Workspace& W, const Ctrl* prev) {
             // counted partition, compact layout (still beside the running apply)
             c.sp.fast = 0;
             c.sp.compact = 0;
+            c.sp.big = 0;
             c.sp.seq_cut = kSpSkip;
             HIPCHK(launch_sparse_partition(vtype_of(s->desc), c.bt, c.sp, c.spl, W.sp, s->stride, s->K, s->first,
                                            s->rows, W.ctrl, c.tail_cut, is));
@@ -754,6 +761,7 @@ int retire_front(dml_store* s) {
     const bool abnormal = ctrl_abnormal(&ctl);  // the chunk queued behind it ran as a no-op
     W.clean = s->is_matrix && !abnormal && W.clears;
     s->st.chunks += 1;
+    if (!s->is_matrix && c.sp.big) s->st.sparse_big_chunks += 1;
     if (c.spec && ctl.spec_ok != 0u) {
         std::swap(s->data, s->data_alt);  // every identity record verified: the output is the shard
         s->st.spec_chunks += 1;
@@ -797,6 +805,7 @@ int retire_front(dml_store* s) {
     } else if (!s->is_matrix && ctl.no_dup == 0u) {
         // leaves too large for the LDS sort were skipped by the leaf kernel: apply them
         // exactly (an int32 replay may find an earlier negative counter)
+        s->st.sparse_replays += 1;
         HIPCHK(sparse_replay(vtype_of(s->desc), s->data, c.sp, c.spl, W.sp, c.bt, s->stride, s->K, s->first, s->rows,
                              W.ctrl, c.tail_cut, s->stream));
         HIPCHK(hipMemcpyAsync(&ctl.neg_pos, &W.ctrl->neg_pos, sizeof(ctl.neg_pos), hipMemcpyDeviceToHost,

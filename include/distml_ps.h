@@ -145,6 +145,8 @@ typedef struct dml_store_counters {
     int64_t identity_pushes;
     int64_t reused_pushes;
     int64_t indexed_pushes;
+    int64_t sparse_big_chunks;  /* array chunks applied through the one-level partition (big leaves) */
+    int64_t sparse_replays;     /* array chunks with leaves the exact replay applied */
 } dml_store_counters;
 int dml_store_stats(dml_store* s, dml_store_counters* out, int32_t reset);
 

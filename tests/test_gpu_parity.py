@@ -1862,6 +1862,71 @@ def test_sparse_single_pass_partition_exact(oracle, case):
     assert s.values().tobytes() == o.data.tobytes()
 
 
+@pytest.mark.parametrize("case", ["random", "lattice", "hot_big_leaf", "repeats", "push_repeat", "cutoff",
+                                  "unbalanced"])
+def test_sparse_big_leaves_exact(oracle, case):
+    """The one-level partition (big leaves of 2^BL rows sorted in LDS)
+    against the oracle, bit-exact (FloatArrayStore.java:110-122): a 4 M-row fp32 array
+    shard and 16 pushes of 2 M keys — 4 096 big leaves of 1 024 rows, ~8 K records
+    each, every row listed by ~8 pushes (owner chains in every bucket).
+    random — unique keys per push; lattice — the bench's config-3 key order
+    ((a r + c) mod dim per push); hot_big_leaf — every push adds 1 000 keys inside one
+    big leaf (over 12 288 records: that leaf takes the exact replay); repeats — pushes
+    drawn from half the rows (~10 adds per row); push_repeat — one push lists a key
+    twice (the replay re-partitions with full sequence numbers); cutoff — a key outside
+    the shard (the counted partition, sequence cut, error state); unbalanced — one push
+    twice the others' size lands in one slice (the two-level path)."""
+    from distml_amd import DataDesc, DistMLException, encode_array_push
+    rng = np.random.default_rng(7 + len(case))
+    first, rows = 11, 1 << 22
+    nb, per = 16, 1 << 21
+    fmt = DataDesc(0, 1, 1)  # FloatArrayStore, LONG keys
+    s, _ = mk_store(fmt, first, first + rows - 1)
+    o = oracle_store(oracle, fmt, first, first + rows - 1)
+    init = rng.standard_normal((rows, 1)).astype(np.float32)
+    s.load_values(init)
+    o.data[:] = init
+    pushes = []
+    for b in range(nb):
+        n = per * 12 if case == "unbalanced" and b == 0 else per
+        if case == "lattice":
+            a = (2 * b + 3) * 999_999_937 % rows | 1
+            keys = (a * np.arange(n, dtype=np.int64) + b * 12_345_701) % rows
+        elif case == "repeats":
+            keys = np.unique(rng.choice(rows // 2, size=n, replace=True))
+            rng.shuffle(keys)
+        else:
+            keys = rng.choice(rows, size=min(n, rows), replace=False)
+        keys = keys + first
+        if case == "hot_big_leaf":
+            keys[:1000] = first + 5 * 1024 + rng.choice(1024, size=1000, replace=False)
+            keys = np.concatenate([keys[:1000], np.setdiff1d(keys[1000:], keys[:1000])])
+        if case == "push_repeat" and b == 5:
+            keys[17] = keys[5]
+        vals = (rng.standard_normal(len(keys)) * 1e-2).astype(np.float32)
+        p = encode_array_push(keys, vals, 1, 1)
+        if case == "cutoff" and b == 9:
+            p = p[:12 * 9000] + encode_array_push([rows + first + 5], [1.0], 1, 1) + p[12 * 9000:]
+        pushes.append(p)
+    err = None
+    for p in pushes:
+        if o.push(p):
+            err = o.error()
+            break
+    s.stats(reset=True)
+    if err is None:
+        s.handlePushBatch(fmt, pushes)
+    else:
+        with pytest.raises(DistMLException) as ei:
+            s.handlePushBatch(fmt, pushes)
+        assert (ei.value.code, ei.value.key) == (err[0], err[1])
+    st = s.stats(reset=True)
+    assert s.values().tobytes() == o.data.tobytes()
+    big = case not in ("cutoff", "unbalanced")
+    assert st["sparse_big_chunks"] == (1 if big else 0), st
+    assert st["sparse_replays"] == (1 if case in ("hot_big_leaf", "push_repeat") else 0), st
+
+
 @pytest.mark.parametrize("cols", [200, 64])
 @pytest.mark.parametrize("W", [1, 2, 4])
 @pytest.mark.parametrize("case", ["plain", "large", "cutoff", "repeat"])
