@@ -54,7 +54,7 @@ import time
 ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
 # HIP's default hardware queues (4 per process), as the PS JVM runs: the store and
-# group paths measured the same at 4 and 8 (scripts/gpu_queues.sh).
+# group paths measured the same at 4 and 8 (round 3).
 
 METRIC = "device-resident gradient-bucket reduce GiB/s (dense fp32 + sparse scatter-add)"
 ROWS, COLS, W = 16384, 1024, 32
