@@ -753,7 +753,10 @@ __global__ __launch_bounds__(256) void k_sp_l1_big(const Batch bt, const SpPlan 
                                                    int64_t first, int64_t rows, Ctrl* __restrict__ ctrl,
                                                    uint64_t tail_cut, uint32_t* __restrict__ curS,
                                                    uint64_t* __restrict__ comp, SpStat* __restrict__ stat) {
-    __shared__ uint32_t h[kSpBigBins];  // records per big leaf, then this tile's base in its region
+    // records per big leaf, then this tile's base in its region: two 16-bit halves a
+    // word (counts <= kSpTile, bases < capS < 2^16), 16 KB, so one partition block
+    // fits beside two leaf blocks on a CU
+    __shared__ uint32_t h[kSpBigBins / 2];
     const int tid = threadIdx.x;
     if (blockIdx.x == 0 && tid == 0 && tail_cut != kNoPos) atomicMin(&ctrl->cutoff, (unsigned long long)tail_cut);
     const int x = (int)(blockIdx.x % kSpSlices);
@@ -769,7 +772,7 @@ __global__ __launch_bounds__(256) void k_sp_l1_big(const Batch bt, const SpPlan 
         }
     }
     if (b < 0) return;  // uniform: past this slice's tiles
-    for (int j = tid; j < pl.nbig; j += 256) h[j] = 0u;
+    for (int j = tid; j < (pl.nbig + 1) / 2; j += 256) h[j] = 0u;
     __syncthreads();
     const int64_t r0 = tin * kSpTile + tid;
     const int64_t n = bt.nrec[b];
@@ -796,23 +799,31 @@ __global__ __launch_bounds__(256) void k_sp_l1_big(const Batch bt, const SpPlan 
             bad = min(bad, pos_of((uint64_t)bt.bidx[b], (uint64_t)(r * stride)));
             continue;
         }
-        rank[i] = atomicAdd(&h[(uint32_t)(row[i] >> pl.BL)], 1u);
+        const uint32_t B = (uint32_t)(row[i] >> pl.BL), sh = 16u * (B & 1u);
+        rank[i] = (atomicAdd(&h[B >> 1], 1u << sh) >> sh) & 0xFFFFu;
     }
     if (bad != kNoPos) atomicMin(&ctrl->cutoff, (unsigned long long)bad);
     __syncthreads();
-    for (int j = tid; j < pl.nbig; j += 256) {
-        const uint32_t c = h[j];
-        if (!c) continue;
-        const uint32_t at = atomicAdd(&curS[(int64_t)x * pl.nbig + j], c);
-        if ((int64_t)at + c > pl.capS) stat->overflow = 1u;
-        h[j] = at;
+    for (int j = tid; j < (pl.nbig + 1) / 2; j += 256) {  // both halves of a word in one thread
+        const uint32_t w = h[j];
+        uint32_t o = 0;
+#pragma unroll
+        for (int e = 0; e < 2; ++e) {
+            const uint32_t c = (w >> (16 * e)) & 0xFFFFu;
+            const int64_t B = 2 * (int64_t)j + e;
+            if (!c || B >= pl.nbig) continue;
+            const uint32_t at = atomicAdd(&curS[(int64_t)x * pl.nbig + B], c);
+            if ((int64_t)at + c > pl.capS) stat->overflow = 1u;
+            o |= min(at, 0xFFFFu) << (16 * e);  // an overflowing base is not used (q >= capS)
+        }
+        h[j] = o;
     }
     __syncthreads();
 #pragma unroll
     for (int i = 0; i < kPer; ++i) {
         if (row[i] < 0) continue;
         const int64_t B = row[i] >> pl.BL;
-        const int64_t q = (int64_t)h[B] + rank[i];
+        const int64_t q = (int64_t)((h[B >> 1] >> (16 * (B & 1))) & 0xFFFFu) + rank[i];
         if (q >= pl.capS) continue;
         comp[(B * kSpSlices + x) * pl.capS + q] = ((uint64_t)(row[i] - (B << pl.BL)) << 38) | ((uint64_t)b << 32) |
                                                   (uint64_t)__float_as_uint(u[i]);
@@ -821,13 +832,13 @@ __global__ __launch_bounds__(256) void k_sp_l1_big(const Batch bt, const SpPlan 
 
 // k_sp_leaf_big: k_sp_leaf's ordered apply for one big leaf (up to kSpBigCap compact
 // records from its 8 slice regions): counting sort over kSpBigLines line buckets,
-// then each thread takes sorted positions p = tid + k * 1024 — its shard loads are
+// then each thread takes sorted positions p = tid + k * 512 — its shard loads are
 // issued in address order (a round of the block covers 1/12 of the big leaf's range,
 // which keeps the DRAM rows the chip touches at once few: loads in record order,
-// across the big leaf's 1 MB, ran the kernel 1.61 ms against 1.1 ms for the two-level
-// path's 64-KB leaves) and run under the ownership scan of the same positions. One
-// 16-wave block per CU (136 KB of LDS).
-constexpr int kSpBigThreads = 1024;
+// across a 1 MB big leaf, ran the kernel 1.61 ms against 1.36 ms in address order)
+// and run under the ownership scan of the same positions. 8-wave blocks of 68 KB of
+// LDS, two per CU (one 16-wave block of 12 K records per CU: 1.36 ms).
+constexpr int kSpBigThreads = 512;
 constexpr int kSpBigLines = 2 * kSpBigThreads;
 __global__ __launch_bounds__(kSpBigThreads) void k_sp_leaf_big(float* __restrict__ shard,
                                                                const uint32_t* __restrict__ curS, int64_t nbig,
@@ -1016,10 +1027,11 @@ SpPlan sparse_plan(const Batch& bt, int nb, int64_t rows) {
 }
 
 // One-level partition: big leaves of 2^BL rows, as few as fit the
-// one-level pass's LDS histogram (<= kSpBigBins), holding 2 K - 8.7 K records on
-// average (kSpBigCap orders up to 12 288: config 3's lattice keys put 1.41x the
-// mean, 11 790, into its fullest big leaf). The 8 slices (pushes p % 8) must carry
-// near-equal shares, since slice x's tiles all run on one XCD.
+// one-level pass's LDS histogram (<= kSpBigBins), holding 1 K - 4.35 K records on
+// average (kSpBigCap orders up to 6 144: config 3's lattice keys put 1.41x the
+// mean, 5 901 of 4 194, into its fullest big leaf of 2^17 rows; fuller ones take the
+// exact replay). The 8 slices (pushes p % 8) must carry near-equal shares, since
+// slice x's tiles all run on one XCD.
 void sparse_plan_big(SpPlan& pl, const Batch& bt, int64_t rows) {
     pl.big = 0;
     if (!pl.compact || pl.nb < kSpSlices || pl.nrec <= 0) return;
@@ -1027,8 +1039,8 @@ void sparse_plan_big(SpPlan& pl, const Batch& bt, int64_t rows) {
     while (BL < 24 && ((rows + ((int64_t)1 << BL) - 1) >> BL) > kSpBigBins) ++BL;
     const int64_t nbig = (rows + ((int64_t)1 << BL) - 1) >> BL;
     const int64_t mean = pl.nrec / nbig;
-    // the LDS word: value | push << 32 | row within the big leaf << 38 | flags << 62
-    if (BL > 24 || mean < 2048 || mean > 8704) return;
+    // the compact word: value | push << 32 | row within the big leaf << 38
+    if (BL > 24 || mean < kSpBigCap / 6 || mean > kSpBigCap * 17 / 24) return;
     int64_t srec[kSpSlices] = {0}, stile[kSpSlices] = {0};
     for (int b = 0; b < pl.nb; ++b) {
         pl.sbase[b] = stile[b % kSpSlices];
@@ -1047,6 +1059,7 @@ void sparse_plan_big(SpPlan& pl, const Batch& bt, int64_t rows) {
     // a region holds twice the slice's mean share of a big leaf + 512 (pushes spread
     // their keys: config 3's regions peak at 1.1x the mean); overflow -> counted partition
     pl.capS = 2 * (smax / nbig) + 512;
+    if (pl.capS >= 0xFFFF) return;  // the one-level pass keeps region bases in 16 bits
     pl.big = 1;
 }
 
@@ -1250,7 +1263,8 @@ hipError_t launch_sparse_leaf(int vtype, void* shard, const SpPlan& pl, const Sp
     if (pl.big) {
         if (vtype != kF32) return hipErrorInvalidValue;
         g_kernel_name = "dml::k_sp_leaf_big";
-        const int bshift = pl.BL > 11 ? pl.BL - 11 : 0;  // kSpBigLines = 2^11 line buckets
+        int bshift = 0;  // kSpBigLines line buckets over the big leaf's rows
+        while ((((int64_t)1 << pl.BL) >> bshift) > kSpBigLines) ++bshift;
         hipExtLaunchKernelGGL(k_sp_leaf_big, dim3((unsigned)pl.nbig), dim3(kSpBigThreads), 0, st, ev.start, ev.stop, 0,
                               (float*)shard, (const uint32_t*)(ws + l.curS), pl.nbig, pl.capS,
                               (const uint64_t*)(ws + l.big), pl.BL, bshift, ws + l.leafflag, ctrl, prev);
