@@ -924,16 +924,23 @@ __global__ __launch_bounds__(kSpBigThreads) void k_sp_leaf_big(float* __restrict
     __syncthreads();
     // sorted positions p = tid + k * kT: the shard loads first (address order), then
     // the ownership scan of the same positions while they are in flight
+    // slot k takes the sorted twelfth (k + rot) % kPer: with rot = B % kPer, the blocks'
+    // concurrent rounds do not all sit at the same offset of their big leaves (-0.5 %,
+    // 3 rounds on one box)
+    const int rot = (int)(B % kPer);
     uint64_t cs[kPer];
     float x0[kPer];
 #pragma unroll
-    for (int k = 0; k < kPer; ++k) cs[k] = sc[perm[min(tid + k * kT, n - 1)]];
+    for (int k = 0; k < kPer; ++k) {
+        const int kk = k + rot >= kPer ? k + rot - kPer : k + rot;
+        cs[k] = sc[perm[min(tid + kk * kT, n - 1)]];
+    }
 #pragma unroll
     for (int k = 0; k < kPer; ++k) x0[k] = shard[lr.row(cs[k])];
     uint32_t fl = 0;  // bit 2k: owns its row, bit 2k+1: row repeated
 #pragma unroll
     for (int k = 0; k < kPer; ++k) {
-        const int p = tid + k * kT;
+        const int p = tid + (k + rot >= kPer ? k + rot - kPer : k + rot) * kT;
         if (p >= n) continue;
         const int i = perm[p];
         const uint64_t ci = cs[k], row = lr.row(ci), ki = lr.key(ci);
@@ -1032,9 +1039,12 @@ SpPlan sparse_plan(const Batch& bt, int nb, int64_t rows) {
 // mean, 5 901 of 4 194, into its fullest big leaf of 2^17 rows; fuller ones take the
 // exact replay). The 8 slices (pushes p % 8) must carry near-equal shares, since
 // slice x's tiles all run on one XCD.
+#ifndef DML_AB_NOBIG
+#define DML_AB_NOBIG 0
+#endif
 void sparse_plan_big(SpPlan& pl, const Batch& bt, int64_t rows) {
     pl.big = 0;
-    if (!pl.compact || pl.nb < kSpSlices || pl.nrec <= 0) return;
+    if (DML_AB_NOBIG || !pl.compact || pl.nb < kSpSlices || pl.nrec <= 0) return;
     int BL = 0;
     while (BL < 24 && ((rows + ((int64_t)1 << BL) - 1) >> BL) > kSpBigBins) ++BL;
     const int64_t nbig = (rows + ((int64_t)1 << BL) - 1) >> BL;
