@@ -428,6 +428,8 @@ def headline(ctx: Ctx, L, args, out_line: dict):
     else:
         group = ShardGroup(fmt, ROWS, COLS, rank, world, device=ctx.local, pieces=args.pieces,
                            emulate_world=args.emulate_rs)
+        if args.index_normal_prio:  # diagnostic: the next call's index chain at normal priority
+            group.istream = torch.cuda.Stream(device=torch.device("cuda", ctx.local))
         bufs = make_buckets(L, torch, fmt, W, ROWS) + make_buckets(L, torch, fmt, W, ROWS, value_seed=5000)
         sets = [([b.data_ptr() for b in bs], [b.numel() for b in bs]) for bs in (bufs[:W], bufs[W:])]
         st = torch.cuda.current_stream().cuda_stream
@@ -1179,6 +1181,7 @@ def main():
     ap.add_argument("--emulate-rs", type=int, default=0,
                     help="diagnostic with --group at N = 1: the owner-side HBM footprint of an N-rank "
                          "reduce-scatter + 1/N apply (results not valid)")
+    ap.add_argument("--index-normal-prio", action="store_true", help=argparse.SUPPRESS)
     ap.add_argument("--native-group", action="store_true",
                     help="also run the config-2 workload through dml_group at N = 1 (always at N > 1)")
     ap.add_argument("--group", action="store_true",

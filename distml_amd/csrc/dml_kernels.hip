@@ -62,26 +62,38 @@ __device__ inline u32x4 pack(const T* v) {
 // Rows listed twice by one push are flagged (rowflag[row] = 1): atomicExch sees
 // the earlier record; the reduce skips those rows and the host replays just
 // them through the exact layered path.
-__global__ __launch_bounds__(256) void k_index(const Batch bt, int64_t stride, int K, int64_t first, int64_t rows,
-                                               int32_t* __restrict__ slot, uint32_t* __restrict__ rowflag,
-                                               Ctrl* __restrict__ ctrl, uint64_t tail_cut) {
-    const int b = blockIdx.y;
-    const int64_t r = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (r == 0 && b == 0 && tail_cut != kNoPos) atomicMin(&ctrl->cutoff, (unsigned long long)tail_cut);
-    if (r >= bt.nrec[b]) return;
-    // identity push: the reduce verifies its keys (spec), or k_ident_full did (ident_ok)
-    if ((bt.spec || bt.ident_ok) && ((ctrl->ident >> b) & 1ull)) return;
-    const int64_t off = r * stride;
-    const int64_t key = ld_key(bt.base[b] + off, K);
-    const int64_t idx = row_index(key, first, rows);
-    if (idx < 0) {
-        atomicMin(&ctrl->cutoff, (unsigned long long)pos_of((uint64_t)bt.bidx[b], (uint64_t)off));
-        return;
-    }
-    const int32_t old = atomicExch(&slot[idx * slot_stride((int)gridDim.y) + ctrl_col(ctrl, b)], (int32_t)r);
-    if (old != -1 && !bt.keeps) {
-        rowflag[idx] = 1u;
-        ctrl->no_dup = 0u;  // benign race: every writer stores the same value
+// A bounded grid walks the (push, 256-record chunk) tasks: the launch dispatches at
+// most kIndexBlocks blocks even when every push skips (identity / reused pushes of a
+// speculative chunk), instead of one block per chunk of every push — 8 192 waves for
+// config 2, which at the sharded path's high stream priority took dispatch slots from
+// the running pre-reduce (its pieces 352-369 us against 331-347 us with the index at
+// normal priority).
+constexpr int kIndexBlocks = 512;
+__global__ __launch_bounds__(256) void k_index(const Batch bt, int nb, int64_t nchunk, int64_t stride, int K,
+                                               int64_t first, int64_t rows, int32_t* __restrict__ slot,
+                                               uint32_t* __restrict__ rowflag, Ctrl* __restrict__ ctrl,
+                                               uint64_t tail_cut) {
+    if (blockIdx.x == 0 && threadIdx.x == 0 && tail_cut != kNoPos)
+        atomicMin(&ctrl->cutoff, (unsigned long long)tail_cut);
+    const uint64_t ident = (bt.spec || bt.ident_ok) ? ctrl->ident : 0ull;
+    for (int64_t t = blockIdx.x; t < (int64_t)nb * nchunk; t += gridDim.x) {
+        const int b = (int)(t / nchunk);
+        // identity push: the reduce verifies its keys (spec), or k_ident_full did (ident_ok)
+        if ((ident >> b) & 1ull) continue;  // uniform
+        const int64_t r = (t - (int64_t)b * nchunk) * 256 + threadIdx.x;
+        if (r >= bt.nrec[b]) continue;
+        const int64_t off = r * stride;
+        const int64_t key = ld_key(bt.base[b] + off, K);
+        const int64_t idx = row_index(key, first, rows);
+        if (idx < 0) {
+            atomicMin(&ctrl->cutoff, (unsigned long long)pos_of((uint64_t)bt.bidx[b], (uint64_t)off));
+            continue;
+        }
+        const int32_t old = atomicExch(&slot[idx * slot_stride(nb) + ctrl_col(ctrl, b)], (int32_t)r);
+        if (old != -1 && !bt.keeps) {
+            rowflag[idx] = 1u;
+            ctrl->no_dup = 0u;  // benign race: every writer stores the same value
+        }
     }
 }
 
@@ -193,8 +205,10 @@ hipError_t launch_ident_full(const Batch& bt, int nb, int64_t max_nrec, int64_t 
 hipError_t launch_index(const Batch& bt, int nb, int64_t max_nrec, int64_t stride, int K, int64_t first,
                         int64_t rows, int32_t* slot, uint32_t* rowflag, Ctrl* ctrl, uint64_t tail_cut, hipStream_t st) {
     if (nb <= 0) return hipSuccess;
-    dim3 grid((unsigned)std::max<int64_t>(1, (max_nrec + 255) / 256), (unsigned)nb);
-    hipLaunchKernelGGL(k_index, grid, dim3(256), 0, st, bt, stride, K, first, rows, slot, rowflag, ctrl, tail_cut);
+    const int64_t nchunk = std::max<int64_t>(1, (max_nrec + 255) / 256);
+    const unsigned grid = (unsigned)std::min<int64_t>(kIndexBlocks, nchunk * nb);
+    hipLaunchKernelGGL(k_index, dim3(grid), dim3(256), 0, st, bt, nb, nchunk, stride, K, first, rows, slot, rowflag,
+                       ctrl, tail_cut);
     return hipGetLastError();
 }
 
