@@ -153,28 +153,33 @@ hipError_t launch_ident_check(const Batch& bt, int nb, int64_t stride, int K, in
     return hipGetLastError();
 }
 
-// k_assign_cols (one thread): the pushes k_ident_check neither verified as identity
-// nor matched to a kept column are indexed; each keeps its own column when no
-// matched push reads it, the others take the lowest free columns. A chunk of nb
-// pushes has slot_stride(nb) >= nb columns and at most nb of them are taken, so
-// every push gets one.
+// k_assign_cols (one wave, lane b = push b): the pushes k_ident_check neither
+// verified as identity nor matched to a kept column are indexed; each keeps its own
+// column when no matched push reads it, the others take the lowest free columns in
+// push order. A chunk of nb pushes has slot_stride(nb) >= nb columns and at most nb
+// of them are taken, so every push gets one. (One thread walking the pushes took
+// 32-45 us on the next call's index chain beside a running reduce: a chain of
+// dependent byte loads; here one load per lane.)
 __global__ __launch_bounds__(64) void k_assign_cols(Ctrl* __restrict__ ctrl, int nb) {
-    if (threadIdx.x != 0) return;
+    const int b = threadIdx.x;
     const unsigned long long id = ctrl->ident;
-    uint64_t used = 0, need = 0;
-    for (int b = 0; b < nb; ++b)
-        if (((id >> b) & 1ull) && ctrl->col[b] != 0xFFu) used |= 1ull << ctrl->col[b];
-    for (int b = 0; b < nb; ++b) {
-        if ((id >> b) & 1ull) continue;
-        if ((used >> b) & 1ull) need |= 1ull << b;
-        else used |= 1ull << b;  // column b (Ctrl::col stays 0xFF)
-    }
-    while (need) {
-        const int b = (int)__builtin_ctzll(need);
-        need &= need - 1;
-        const int c = (int)__builtin_ctzll(~used);
-        used |= 1ull << c;
-        ctrl->col[b] = (unsigned char)c;
+    const bool live = b < nb;
+    const bool matched = live && ((id >> b) & 1ull);
+    const unsigned col = live ? ctrl->col[b] : 0xFFu;
+    uint64_t used = (matched && col != 0xFFu) ? 1ull << col : 0ull;  // columns matched pushes read
+#pragma unroll
+    for (int m = 32; m > 0; m >>= 1) used |= (uint64_t)__shfl_xor((unsigned long long)used, m);
+    const bool indexed = live && !matched;
+    const bool need = indexed && ((used >> b) & 1ull);  // its own column is read by a matched push
+    const uint64_t keep = __ballot(indexed && !need);   // pushes that keep their own column
+    const uint64_t needs = __ballot(need);
+    used |= keep;
+    if (need) {
+        // the k-th pushes needing a column (in push order) takes the k-th lowest free one
+        int k = __popcll(needs & ((1ull << b) - 1ull));
+        uint64_t freec = ~used;
+        while (k-- > 0) freec &= freec - 1;
+        ctrl->col[b] = (unsigned char)__builtin_ctzll(freec);
     }
 }
 hipError_t launch_assign_cols(Ctrl* ctrl, int nb, hipStream_t st) {
