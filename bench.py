@@ -553,6 +553,29 @@ def headline(ctx: Ctx, L, args, out_line: dict):
     torch.cuda.empty_cache()
 
 
+def guarded_leg(ctx: Ctx, line: dict, out, key: str, fn, seconds: float):
+    """A secondary leg that must not cost the line: if it raises, or has not returned
+    after `seconds` (a collective that never completes), rank 0 prints the line so
+    far with the leg's error and every rank exits (os._exit: no exec)."""
+    import threading
+
+    def bail(msg: str):
+        if ctx.rank == 0:
+            print(json.dumps(dict(line, **{key: {"error": msg}})), file=out, flush=True)
+        os._exit(0)
+
+    t = threading.Timer(seconds, bail, args=(f"did not finish within {seconds:.0f} s",))
+    t.daemon = True
+    t.start()
+    try:
+        return fn()
+    except Exception as e:  # noqa: BLE001 — reported in the line, not raised
+        t.cancel()
+        bail(repr(e)[:400])
+    finally:
+        t.cancel()
+
+
 def leg_native_group(ctx: Ctx, L, args) -> dict:
     """The config-2 workload through the native shard group (dml_group_*, the RCCL
     communicator libdistml_ps creates itself; what the JNI's GpuShardGroup binds):
@@ -1261,7 +1284,8 @@ def main():
     if "4a" in legs:
         line["config4_ada"] = leg_config4_ada(ctx, L, args)
     if (world > 1 and not args.rehearse_gloo) or args.native_group:
-        line["native_group"] = leg_native_group(ctx, L, args)
+        line["native_group"] = guarded_leg(ctx, line, out, "native_group", lambda: leg_native_group(ctx, L, args),
+                                           seconds=180.0)
     if world == 1 and not args.group and args.sparse_steps > 0:
         line["sparse"] = sparse_leg(ctx, L, args.sparse_steps, cpu=not args.no_cpu)
     if rank == 0 and world == 1 and not args.no_cpu and not args.group:

@@ -58,3 +58,31 @@ def test_hbm_footprint_check():
     # the config-4 leg at N = 8: 16 pushes of the full model per rank + the sharded path's buffers
     s4 = bench.store_bytes(1_250_000, 200, 4, spec=True) + bench.group_bytes(8, 10_000_000, 200, 4)
     assert 16 * 10_000_000 * 804 + s4 < 0.97 * bench.HBM_BYTES
+
+
+@pytest.mark.parametrize("mode", ["raise", "hang", "ok"])
+def test_guarded_leg_keeps_the_line(mode):
+    """bench.guarded_leg: a secondary leg (the native group at N > 1) that raises or
+    never returns costs only itself — rank 0 prints the line so far with the leg's
+    error and the rank exits 0; a leg that returns is reported as is."""
+    code = f"""
+import json, sys, time
+sys.path.insert(0, {ROOT!r})
+import bench
+class Ctx: rank = 0
+def leg():
+    if {mode!r} == "raise": raise RuntimeError("boom")
+    if {mode!r} == "hang": time.sleep(30)
+    return {{"value": 1.0}}
+line = {{"metric": "m", "value": 5.0}}
+line["native_group"] = bench.guarded_leg(Ctx(), line, sys.stdout, "native_group", leg, seconds=1.0)
+print(json.dumps(line), flush=True)
+"""
+    r = subprocess.run([sys.executable, "-c", code], capture_output=True, text=True, timeout=60)
+    assert r.returncode == 0, r.stderr[-2000:]
+    d = json.loads([ln for ln in r.stdout.splitlines() if ln.startswith("{")][-1])
+    assert d["value"] == 5.0
+    if mode == "ok":
+        assert d["native_group"] == {"value": 1.0}
+    else:
+        assert "error" in d["native_group"] and ("boom" in d["native_group"]["error"] or "within" in d["native_group"]["error"])
