@@ -217,6 +217,17 @@ def test_mock_jvm_store_on_gpu(oracle):
         _, exc = jvm.call("nativeGroupPush", g, jvm.longs([t.data_ptr() for t in pair]),
                           jvm.longs([t.numel() for t in pair]), 0)
         assert exc is None
+    # pushLocal (mode 3) right behind the full-range calls: applied after them, in order
+    p = encode_matrix_push(rng.permutation(rows)[:rows // 2], rng.integers(0, 3, size=(rows // 2, cols)).astype(np.int32),
+                           0, 0)
+    assert og.push(p) == 0
+    dl = torch.frombuffer(bytearray(p), dtype=torch.uint8).cuda()
+    torch.cuda.synchronize()
+    _, exc = jvm.call("nativeGroupPush", g, jvm.longs([dl.data_ptr()]), jvm.longs([dl.numel()]), 3)
+    assert exc is None
+    # an unknown mode is refused with a Java exception (DML_E_INVALID_ARG)
+    _, exc = jvm.call("nativeGroupPush", g, jvm.longs([dl.data_ptr()]), jvm.longs([dl.numel()]), 9)
+    assert exc is not None
     _, exc = jvm.call("nativeGroupFlush", g)
     assert exc is None
     st, exc = jvm.call("nativeGroupStore", g)
