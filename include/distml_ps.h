@@ -383,7 +383,10 @@ int dml_group_push_exchange(dml_group* g, const void* const* dev_bufs, const int
  * one ncclReduceScatter of both, the owner's
  * dml_store_apply_adagrad_moments_device. xGMI bytes per rank: (world-1)/world
  * x 2 x the model, whatever n is (the exchange path moves n pushes). Within
- * 1e-6, not bit-exact; errors surface at the next call or the flush. */
+ * 1e-6, not bit-exact; errors surface at the next call or the flush. Known
+ * divergences: a maxDelta tie goes to the first element in row-major order (the
+ * reference's: the first in push / record order, FloatMatrixStoreAdaGrad.java:273-277),
+ * and with NaN / Inf gradients alpha keeps its value. */
 int dml_group_push_moments(dml_group* g, const void* const* dev_bufs, const int64_t* lens, int32_t n);
 /* Pushes the client already split to this shard (SparseMatrix.java:46-60): the
  * store's exact ordered device push (dml_store_push_batch_device), queued after
