@@ -16,6 +16,8 @@ Cases (generators shared with tests/test_gpu_group.py):
             sum) on the rank's own rows: exact only if the store applies them in order
   fault     int32 full-range calls; rank 0's second finished call fails its verdict
             (fault injection): it raises there, every rank finishes every call
+  jni       int32 full-range calls and a pushLocal through the JNI shim's GpuShardGroup
+            entry points (integration/jni/dml_jni.cc on the mock JNIEnv of tests/jni_mock)
 Writes out/<case>_<rank>.npz and prints one JSON line.
 """
 import argparse
@@ -135,6 +137,39 @@ def main():
             errors.append(["flush", type(e).__name__, str(e)[:200]])
         res["data"] = g.store.values()
         res["stats"] = np.array([g.prereduce_stats().get(k, 0) for k in ("spec_chunks", "spec_reruns")])
+    elif a.case == "jni":
+        # the same full-range calls driven through the JNI shim's GpuShardGroup entry points
+        # (integration/jni/dml_jni.cc linked with the in-process mock JNIEnv), int32, then
+        # a pushLocal of this rank's own rows; the shard comes back through nativeWriteAll
+        from test_jni_shim import MockJVM
+        jvm = MockJVM()
+        rows, cols = a.rows, a.cols
+        uid_arr = jvm.bytes_(uid)
+        g, exc = jvm.call("nativeGroupCreate", uid_arr, world, rank, a.device, 1, 0, 0, 0, 1, 0, rows, cols, a.pieces)
+        assert exc is None and g, exc
+        from distml_amd import KeyRange
+        shard = KeyRange(0, rows - 1).linearSplit(world)[rank]
+        st, exc = jvm.call("nativeGroupStore", g)
+        init = G._init(0, rows, cols)[shard.firstKey:shard.lastKey + 1]
+        jvm.call("nativeReadAll", st, jvm.bytes_(init.astype(">i4").tobytes()))
+        for call in range(G.CALLS):
+            bufs = G._buckets(pyoracle, 0, rank, a.pushes, rows, cols, call)
+            ptrs = [H.put(b) for b in bufs]
+            _, exc = jvm.call("nativeGroupPush", g, jvm.longs(ptrs), jvm.longs([b.nbytes for b in bufs]), 0)
+            if exc:
+                errors.append([call, exc[0], exc[1][:200]])
+        from distml_amd import encode_matrix_push
+        keys = np.arange(shard.firstKey, shard.lastKey + 1)
+        lp = np.frombuffer(encode_matrix_push(keys, np.full((len(keys), cols), rank + 1, np.int32), 0, 0),
+                           np.uint8).copy()
+        _, exc = jvm.call("nativeGroupPush", g, jvm.longs([H.put(lp)]), jvm.longs([lp.nbytes]), 3)
+        assert exc is None, exc
+        _, exc = jvm.call("nativeGroupFlush", g)
+        assert exc is None, exc
+        wa, _ = jvm.call("nativeWriteAll", st)
+        res["data"] = np.frombuffer(jvm.read(wa), ">i4").astype(np.int32)
+        jvm.call("nativeGroupDestroy", g)
+        g = None
     elif a.case in ("exchange", "moments"):
         vt = 1 if a.case == "moments" else a.vt
         fmt = DataDesc(1, 0, vt, False, True, vt == 1)
@@ -154,7 +189,8 @@ def main():
             res["md"] = np.array(g.store.maxDelta(), np.float64)
     else:
         raise SystemExit(f"unknown case {a.case}")
-    g.close()
+    if g is not None:
+        g.close()
     H.free()
     np.savez(os.path.join(a.out, f"{a.case}_{rank}.npz"), **res)
     calls = None

@@ -179,3 +179,20 @@ def test_native_group_rccl_all_devices(tmp_path, oracle):
             G.check_full_range(got, o, init, all_b, rows, cols)
     run_ranks(tmp_path, world, "exchange", double=False, vt=1)
     G.check_exchange(tmp_path, oracle, world, 1, lambda n, r: np.load(tmp_path / f"exchange_{r}.npz")[n])
+
+
+@pytest.mark.parametrize("world", [2, 3])
+def test_native_group_through_jni(tmp_path, oracle, world):
+    """The JNI's multi-GPU binding itself at world 2-3: GpuShardGroup's entry points in
+    integration/jni/dml_jni.cc (nativeGroupCreate / nativeGroupPush mode 0 and 3 /
+    nativeGroupFlush / nativeGroupStore) on the mock JNIEnv, in torch-free ranks over
+    the RCCL stand-in; int32 full-range calls then a pushLocal of each rank's rows,
+    every shard read back through nativeWriteAll (big-endian), exact."""
+    rows, cols, W = 1000, 64, 3
+    outs = run_ranks(tmp_path, world, "jni", rows=rows, cols=cols, pushes=W)
+    assert all(not d["errors"] for d in outs), outs
+    from distml_amd.datadesc import KeyRange
+    o, _, _ = full_expected(oracle, 0, world, rows, cols, W, G.CALLS)
+    for r, sh in enumerate(KeyRange(0, rows - 1).linearSplit(world)):
+        got = np.load(tmp_path / f"jni_{r}.npz")["data"].reshape(-1, cols)
+        assert np.array_equal(got, o.data[sh.firstKey:sh.lastKey + 1] + (r + 1)), r
