@@ -16,7 +16,6 @@ Checks as tests/test_gpu_group.py: fp32 within the reduce-scatter bound of
 DESIGN.md §2 (check_full_range), int32 and the exchange path bit-exact, the
 two-moment path within 1e-6 (kat.moments_within).
 """
-import ctypes as C
 import json
 import os
 import subprocess
@@ -37,10 +36,12 @@ pytestmark = pytest.mark.gpu
 def run_ranks(tmp_path, world, case, double=True, **kw):
     """Start `world` workers, wait for all, return their JSON lines (rank order)."""
     uid = tmp_path / f"uid_{case}"
-    if double:  # the stand-in's id names its shared-memory segment (no GPU needed)
-        buf = (C.c_uint8 * 128)()
-        assert C.CDLL(DOUBLE).ncclGetUniqueId(buf) == 0
-        uid.write_bytes(bytes(buf))
+    if double:
+        # the stand-in's id names its shared-memory segment (rccl_double.cc's format);
+        # written here without loading the stand-in, whose HIP runtime (/opt/rocm) must
+        # not join torch's in this process
+        name = ("dml-rccl-double:/dmlrccl_" + os.urandom(12).hex()).encode()
+        uid.write_bytes(name + b"\0" * (128 - len(name)))
     args = [f"--{k.replace('_', '-')}={v}" for k, v in kw.items()]
     procs = []
     for r in range(world):
