@@ -918,8 +918,8 @@ __global__ __launch_bounds__(kSpBigThreads) void k_sp_leaf_big(float* __restrict
     }
 #pragma unroll
     for (int k = 0; k < kPer; ++k) {
-        const int i = tid + k * kT;
-        if (i < n) perm[atomicAdd(&cur[(uint32_t)((lr.row(c[k]) - row0) >> bshift)], 1u)] = (uint16_t)i;
+        const int i = tid + k * kT;  // the word from LDS: c[] is dead by now (fewer live VGPRs)
+        if (i < n) perm[atomicAdd(&cur[(uint32_t)((lr.row(sc[i]) - row0) >> bshift)], 1u)] = (uint16_t)i;
     }
     __syncthreads();
     // sorted positions p = tid + k * kT: the shard loads first (address order), then
@@ -928,22 +928,21 @@ __global__ __launch_bounds__(kSpBigThreads) void k_sp_leaf_big(float* __restrict
     // concurrent rounds do not all sit at the same offset of their big leaves (-0.5 %,
     // 3 rounds on one box)
     const int rot = (int)(B % kPer);
-    uint64_t cs[kPer];
+    // only the shard values stay in registers; the words are re-read from LDS where
+    // needed (109 -> fewer VGPRs, so a partition block fits beside two leaf blocks)
     float x0[kPer];
 #pragma unroll
     for (int k = 0; k < kPer; ++k) {
         const int kk = k + rot >= kPer ? k + rot - kPer : k + rot;
-        cs[k] = sc[perm[min(tid + kk * kT, n - 1)]];
+        x0[k] = shard[lr.row(sc[perm[min(tid + kk * kT, n - 1)]])];
     }
-#pragma unroll
-    for (int k = 0; k < kPer; ++k) x0[k] = shard[lr.row(cs[k])];
     uint32_t fl = 0;  // bit 2k: owns its row, bit 2k+1: row repeated
 #pragma unroll
     for (int k = 0; k < kPer; ++k) {
         const int p = tid + (k + rot >= kPer ? k + rot - kPer : k + rot) * kT;
         if (p >= n) continue;
         const int i = perm[p];
-        const uint64_t ci = cs[k], row = lr.row(ci), ki = lr.key(ci);
+        const uint64_t ci = sc[i], row = lr.row(ci), ki = lr.key(ci);
         const uint32_t b = (uint32_t)((row - row0) >> bshift);
         const uint32_t bs = bstart[b], be = bstart[b + 1];
         if (be - bs > (uint32_t)kSpBucketMax) s_over = 1;
@@ -972,7 +971,7 @@ __global__ __launch_bounds__(kSpBigThreads) void k_sp_leaf_big(float* __restrict
     for (int k = 0; k < kPer; ++k) {
         const uint32_t f = fl >> (2 * k);
         if (!(f & 1u)) continue;  // not an owner (or past n)
-        const uint64_t ci = cs[k];
+        const uint64_t ci = sc[perm[tid + (k + rot >= kPer ? k + rot - kPer : k + rot) * kT]];
         const uint64_t row = lr.row(ci);
         float xv = x0[k];
         if (!(f & 2u)) {
