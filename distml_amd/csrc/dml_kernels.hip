@@ -732,10 +732,13 @@ __global__ __launch_bounds__(64 * WPB) void k_reduce_rows(T* __restrict__ shard,
         // int32 rollback (rare) rebuilds the table with a second index. Only when this
         // wave is its rows' one reader (rows wider than CPW chunks have several). A
         // speculative chunk keeps its table: its full-range columns are permutations
-        // the next chunk in this workspace may reuse (Batch::kept_cols).
+        // the next chunk in this workspace may reuse (Batch::kept_cols). Entries read
+        // as -1 are left alone: a row no push lists costs no write (config 5: 11 % of
+        // the shard's rows, one 128-B slot line each).
 #pragma unroll
         for (int r = 0; r < RPW; ++r)
-            if ((live >> r & 1u) && lane < nb) slot[row[r] * slot_stride(nb) + lcol] = -1;
+            if ((live >> r & 1u) && lane < nb && (lane_ident || vslot[r] >= 0))
+                slot[row[r] * slot_stride(nb) + lcol] = -1;
     }
     const uint64_t vbase = lane < nb ? (uint64_t)bt.base[lane] : 0ull;
     // Speculative chunks verify identity records through lane 63 of the wave's last
@@ -1042,7 +1045,7 @@ __global__ __launch_bounds__(256) void k_reduce_flat(T* __restrict__ shard, int6
                 const int cb = ctrl_col(ctrl, b);
                 v = slot[mr * ss + cb];
                 // a speculative chunk keeps its table (Batch::kept_cols, see k_reduce_rows)
-                if (!bt.spec) slot[mr * ss + cb] = -1;
+                if (!bt.spec && v >= 0) slot[mr * ss + cb] = -1;
             }
         }
         ls[rl * kMaxW + b] = v;
@@ -1205,7 +1208,7 @@ __global__ __launch_bounds__(256) void k_ada_flat(float* __restrict__ shard, int
                         v = r < bt.nrec[b] ? (int32_t)r : -1;  // record = row; the index skipped it
                     } else {
                         v = slot[r * ss + b];
-                        slot[r * ss + b] = -1;
+                        if (v >= 0) slot[r * ss + b] = -1;
                     }
                 }
                 ls[rl * kMaxW + b] = v;
@@ -2112,7 +2115,7 @@ __global__ __launch_bounds__(256) void k_moments_flat(int64_t ntask, int32_t col
                     v = mr < bt.nrec[b] ? (int32_t)mr : -1;
                 } else {
                     v = slot[mr * ss + b];
-                    slot[mr * ss + b] = -1;
+                    if (v >= 0) slot[mr * ss + b] = -1;
                 }
             }
             ls[rl * kMaxW + b] = v;
