@@ -85,6 +85,36 @@ __global__ void k_read(const float4* p, int64_t n, float* out) {
     if (s == 1234.5f) *out = s;
 }
 
+// Dense sweep: one block per region of RF floats. The region is read whole
+// (coalesced 16-B loads) into LDS, the region's updates (a run of the globally
+// sorted keys) are added there, and the region is written back whole (WB 0) or
+// only its touched 32-B sectors (WB 1). Streams the 4 GB array instead of
+// random 64-B reads: does HBM serve it faster than the random RMW?
+template <int RF, int WB>
+__global__ __launch_bounds__(256) void k_sweep(float* a, const uint32_t* run, const uint32_t* keys, const float* v) {
+    __shared__ float4 reg[RF / 4];
+    __shared__ uint8_t tsec[RF / 8];
+    const int64_t base = (int64_t)blockIdx.x * RF;
+    const float4* src = (const float4*)(a + base);
+    for (int j = threadIdx.x; j < RF / 4; j += 256) reg[j] = src[j];
+    for (int j = threadIdx.x; j < RF / 8; j += 256) tsec[j] = 0;
+    __syncthreads();
+    float* rf = (float*)reg;
+    for (uint32_t r = run[blockIdx.x] + threadIdx.x; r < run[blockIdx.x + 1]; r += 256) {
+        const uint32_t e = keys[r] - (uint32_t)base;
+        atomicAdd(&rf[e], v[r]);
+        if (WB) tsec[e / 8] = 1;
+    }
+    __syncthreads();
+    float4* dst = (float4*)(a + base);
+    if (WB == 0) {
+        for (int j = threadIdx.x; j < RF / 4; j += 256) dst[j] = reg[j];
+    } else {
+        for (int j = threadIdx.x; j < RF / 4; j += 256)
+            if (tsec[j / 2]) dst[j] = reg[j];
+    }
+}
+
 static uint64_t sm(uint64_t x) {
     x += 0x9e3779b97f4a7c15ull;
     x = (x ^ (x >> 30)) * 0xbf58476d1ce4e5b9ull;
@@ -178,6 +208,27 @@ int main() {
         CK(hipFree(du));
         CK(hipFree(dr));
     };
+    auto sweep_case = [&](auto tagr, auto tagw, const char* name) {
+        constexpr int RF = decltype(tagr)::value, WB = decltype(tagw)::value;
+        const int64_t nreg = rows / RF;  // 1e9 is a multiple of 8192 x 5^k? checked below
+        if (nreg * RF != rows) { printf("  skip %s: rows %% %d\n", name, RF); return; }
+        std::vector<uint32_t> hr(nreg + 1);
+        int64_t r = 0;
+        for (int64_t g = 0; g < nreg; ++g) {
+            hr[g] = (uint32_t)r;
+            while (r < N && hg[r] < (uint64_t)(g + 1) * RF) ++r;
+        }
+        hr[nreg] = (uint32_t)N;
+        uint32_t* dr;
+        CK(hipMalloc(&dr, hr.size() * 4));
+        CK(hipMemcpy(dr, hr.data(), hr.size() * 4, hipMemcpyHostToDevice));
+        timeit(name, [&] { k_sweep<RF, WB><<<(unsigned)nreg, 256>>>(a, dr, dg, dv); });
+        CK(hipFree(dr));
+    };
+    sweep_case(std::integral_constant<int, 8000>{}, std::integral_constant<int, 0>{}, "sweep 32 KB regions, write all");
+    sweep_case(std::integral_constant<int, 8000>{}, std::integral_constant<int, 1>{}, "sweep 32 KB regions, write touched 32 B");
+    sweep_case(std::integral_constant<int, 16000>{}, std::integral_constant<int, 1>{}, "sweep 64 KB regions, write touched 32 B");
+    sweep_case(std::integral_constant<int, 4000>{}, std::integral_constant<int, 1>{}, "sweep 16 KB regions, write touched 32 B");
     unit_case(std::integral_constant<int, 8>{}, "unit RMW 32 B, globally sorted");
     unit_case(std::integral_constant<int, 16>{}, "unit RMW 64 B, globally sorted");
     unit_case(std::integral_constant<int, 32>{}, "unit RMW 128 B, globally sorted");
