@@ -730,6 +730,22 @@ def sparse_leg(ctx: Ctx, L, steps: int, cpu: bool):
         tr = out["roofline"].get("traffic")
         if tr:  # the effective (counted-bytes) rate beside the algorithmic one
             out["roofline"]["effective_GBps"] = round(tr / k_s / 1e9, 1)
+        # the random-RMW floor of the same 32e6 updates on this box (dml_diag_rmw_floor):
+        # sorted globally, one plain read-modify-write each, no partition — the leaf's best
+        # case; measured into the shard after the timed steps (its values are not used again)
+        keys = torch.cat([b.view(-1, 12)[:, :8].contiguous().view(torch.int64).view(-1) for b in bufs])
+        idx = torch.sort(keys).values.to(torch.int32)
+        del keys
+        ones = torch.ones(idx.numel(), dtype=torch.float32, device="cuda")
+        ms = C.c_float()
+        best = None
+        for _ in range(3):
+            assert L.dml_diag_rmw_floor(C.c_void_p(store.device_ptr()), C.c_void_p(idx.data_ptr()),
+                                        C.c_void_p(ones.data_ptr()), idx.numel(), C.c_void_p(st), C.byref(ms)) == 0
+            best = ms.value if best is None else min(best, ms.value)
+        del idx, ones
+        out["roofline"]["measured_rmw_floor_us"] = round(best * 1e3, 1)
+        out["roofline"]["frac_of_measured_floor"] = round(best * 1e-3 / k_s, 3)
     store.close()
     del bufs
     torch.cuda.empty_cache()

@@ -2001,6 +2001,26 @@ __global__ __launch_bounds__(256) void k_stream(uint8_t* __restrict__ dst, const
         if (fold == 0x9E3779B9u) *(uint32_t*)dst = fold;
 }
 
+// Random-RMW floor (diagnostic): one plain 4-B read-modify-write per update over a
+// globally sorted index list — the best case of config 3's scatter-add (every update
+// in address order, no partition), against which the leaf kernel is judged.
+// Repeated indices race: the array's values are not meaningful afterwards.
+__global__ __launch_bounds__(256) void k_rmw_floor(float* __restrict__ a, const uint32_t* __restrict__ idx,
+                                                   const float* __restrict__ v, int64_t n) {
+    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i < n) {
+        const uint32_t k = idx[i];
+        a[k] = a[k] + v[i];
+    }
+}
+
+hipError_t launch_rmw_floor(float* a, const uint32_t* idx, const float* v, int64_t n, hipStream_t st, LaunchEv ev) {
+    if (n <= 0) return hipSuccess;
+    hipExtLaunchKernelGGL(k_rmw_floor, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, st, ev.start, ev.stop, 0, a,
+                          idx, v, n);
+    return hipGetLastError();
+}
+
 hipError_t launch_stream(bool copy, void* dst, const void* src, int64_t n16, hipStream_t st, LaunchEv ev) {
     if (n16 <= 0) return hipSuccess;
     const int64_t want = (n16 + 1023) / 1024;  // one 256-thread block per 4 wave steps

@@ -2360,6 +2360,25 @@ int dml_diag_stream(int32_t copy, void* dev_dst, const void* dev_src, int64_t by
     return DML_OK;
 }
 
+int dml_diag_rmw_floor(float* dev_array, const uint32_t* dev_index, const float* dev_values, int64_t n, void* stream,
+                       float* ms) {
+    if (!dev_array || n < 0 || (n > 0 && (!dev_index || !dev_values)) || n >= ((int64_t)1 << 40))
+        return set_err(DML_E_INVALID_ARG, "bad rmw floor arguments");
+    hipStream_t st = (hipStream_t)stream;
+    hipEvent_t e0 = nullptr, e1 = nullptr;
+    HIPCHK(hipEventCreate(&e0));
+    hipError_t e = hipEventCreate(&e1);
+    if (e == hipSuccess) e = launch_rmw_floor(dev_array, dev_index, dev_values, n, st, LaunchEv{e0, e1});
+    if (e == hipSuccess) e = hipEventSynchronize(e1);
+    float t = 0.f;
+    if (e == hipSuccess) e = hipEventElapsedTime(&t, e0, e1);
+    (void)hipEventDestroy(e0);
+    if (e1) (void)hipEventDestroy(e1);
+    if (e != hipSuccess) return set_err(DML_E_HIP, hipGetErrorString(e));
+    if (ms) *ms = t;
+    return DML_OK;
+}
+
 int dml_store_rand(dml_store* s, uint64_t seed) {
     if (int rc = check_store(s)) return rc;
     std::lock_guard<std::mutex> lk(s->mu);

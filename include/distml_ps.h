@@ -415,6 +415,14 @@ int dml_synth_fill_store(dml_store* s, uint64_t seed);
  * `stream`, *ms = kernel time. bench.py reports the reduce's fraction of these
  * measured HBM ceilings. */
 int dml_diag_stream(int32_t copy, void* dev_dst, const void* dev_src, int64_t bytes, void* stream, float* ms);
+/* Random-RMW floor (diagnostic): dev_array[dev_index[i]] += dev_values[i] for i < n,
+ * one plain 4-B read-modify-write per update, in the given (sorted) order, timed on
+ * `stream`, *ms = kernel time. Every index must lie inside dev_array; repeated
+ * indices race, so the array's values are not meaningful afterwards (scratch only).
+ * bench.py's config-3 leg times the leaf apply against it: the same updates sorted
+ * globally, with no partition, are the best case of the random scatter-add. */
+int dml_diag_rmw_floor(float* dev_array, const uint32_t* dev_index, const float* dev_values, int64_t n, void* stream,
+                       float* ms);
 
 /* --- misc --------------------------------------------------------------- */
 const char* dml_last_error(void);   /* thread-local message for the last failure */
