@@ -204,8 +204,8 @@ hipError_t launch_synth_sparse(uint8_t* out, int K, int vtype, int value_stride,
 constexpr int kSpTile = 4096;      // records per partition tile (256 threads x 16)
 constexpr int kSpLeafCap = 2048;   // records one leaf orders in LDS
 constexpr uint32_t kSpSkip = 0xFFFFFFFFu;  // sequence of a record at or past the cutoff (never applied)
-constexpr int kSpBigCap = 6144;    // records a big leaf orders in LDS (one-level partition)
-constexpr int kSpBigBins = 8192;   // big leaves per chunk, at most (the one-level pass's LDS histogram)
+constexpr int kSpBigCap = 4096;    // records a big leaf orders in LDS (one-level partition)
+constexpr int kSpBigBins = 16384;  // big leaves per chunk, at most (the one-level pass's LDS histogram)
 constexpr int kSpSlices = 8;       // regions per big leaf: slice x holds the pushes p with p % 8 == x
 // Shape of one chunk's partition (host-computed, passed by value).
 struct SpPlan {

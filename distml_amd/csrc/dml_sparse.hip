@@ -754,7 +754,7 @@ __global__ __launch_bounds__(256) void k_sp_l1_big(const Batch bt, const SpPlan 
                                                    uint64_t tail_cut, uint32_t* __restrict__ curS,
                                                    uint64_t* __restrict__ comp, SpStat* __restrict__ stat) {
     // records per big leaf, then this tile's base in its region: two 16-bit halves a
-    // word (counts <= kSpTile, bases < capS < 2^16), 16 KB, so one partition block
+    // word (counts <= kSpTile, bases < capS < 2^16), 32 KB, so one partition block
     // fits beside two leaf blocks on a CU
     __shared__ uint32_t h[kSpBigBins / 2];
     const int tid = threadIdx.x;
@@ -833,11 +833,14 @@ __global__ __launch_bounds__(256) void k_sp_l1_big(const Batch bt, const SpPlan 
 // k_sp_leaf_big: k_sp_leaf's ordered apply for one big leaf (up to kSpBigCap compact
 // records from its 8 slice regions): counting sort over kSpBigLines line buckets,
 // then each thread takes sorted positions p = tid + k * 512 — its shard loads are
-// issued in address order (a round of the block covers 1/12 of the big leaf's range,
+// issued in address order (a round of the block covers 1/8 of the big leaf's range,
 // which keeps the DRAM rows the chip touches at once few: loads in record order,
 // across a 1 MB big leaf, ran the kernel 1.61 ms against 1.36 ms in address order)
-// and run under the ownership scan of the same positions. 8-wave blocks of 68 KB of
-// LDS, two per CU (one 16-wave block of 12 K records per CU: 1.36 ms).
+// and run under the ownership scan of the same positions. 8-wave blocks of 48 KB of
+// LDS, up to three per CU. Big leaves of 2^16 rows (<= 4 096 records) run config 3's
+// step 1.32-1.33 ms against 1.39 ms for 2^17 rows (<= 6 144 records, 68 KB, two per
+// CU) and 1.40 ms for 2^15 (<= 2 048: the partition's 64 KB histogram), 3 rounds on
+// one box; one 16-wave block of 12 K records per CU ran 1.36 ms.
 constexpr int kSpBigThreads = 512;
 constexpr int kSpBigLines = 2 * kSpBigThreads;
 __global__ __launch_bounds__(kSpBigThreads) void k_sp_leaf_big(float* __restrict__ shard,
@@ -1033,9 +1036,9 @@ SpPlan sparse_plan(const Batch& bt, int nb, int64_t rows) {
 }
 
 // One-level partition: big leaves of 2^BL rows, as few as fit the
-// one-level pass's LDS histogram (<= kSpBigBins), holding 1 K - 4.35 K records on
-// average (kSpBigCap orders up to 6 144: config 3's lattice keys put 1.41x the
-// mean, 5 901 of 4 194, into its fullest big leaf of 2^17 rows; fuller ones take the
+// one-level pass's LDS histogram (<= kSpBigBins), holding 0.68 K - 2.9 K records on
+// average (kSpBigCap orders up to 4 096: config 3's lattice keys put 1.41x the
+// mean, 2 959 of 2 097, into its fullest big leaf of 2^16 rows; fuller ones take the
 // exact replay). The 8 slices (pushes p % 8) must carry near-equal shares, since
 // slice x's tiles all run on one XCD.
 #ifndef DML_AB_NOBIG

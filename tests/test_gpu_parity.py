@@ -1867,11 +1867,11 @@ def test_sparse_single_pass_partition_exact(oracle, case):
 def test_sparse_big_leaves_exact(oracle, case):
     """The one-level partition (big leaves of 2^BL rows sorted in LDS)
     against the oracle, bit-exact (FloatArrayStore.java:110-122): a 4 M-row fp32 array
-    shard and 16 pushes of 2 M keys — 4 096 big leaves of 1 024 rows, ~8 K records
-    each, every row listed by ~8 pushes (owner chains in every bucket).
+    shard and 16 pushes of 2 M keys — every row listed by ~8 pushes (owner chains in
+    every bucket), big leaves as the planner sizes them for kSpBigBins / kSpBigCap.
     random — unique keys per push; lattice — the bench's config-3 key order
     ((a r + c) mod dim per push); hot_big_leaf — every push adds 1 000 keys inside one
-    big leaf (over 12 288 records: that leaf takes the exact replay); repeats — pushes
+    big leaf, over 32 pushes (past kSpBigCap: that leaf takes the exact replay); repeats — pushes
     drawn from half the rows (~10 adds per row); push_repeat — one push lists a key
     twice (the replay re-partitions with full sequence numbers); cutoff — a key outside
     the shard (the counted partition, sequence cut, error state); unbalanced — one push
@@ -1879,7 +1879,9 @@ def test_sparse_big_leaves_exact(oracle, case):
     from distml_amd import DataDesc, DistMLException, encode_array_push
     rng = np.random.default_rng(7 + len(case))
     first, rows = 11, 1 << 22
-    nb, per = 16, 1 << 21
+    # hot_big_leaf: 32 pushes of 1 M keys (same 32 M records), so one push per row
+    # still overfills a big leaf whatever its size (a leaf holds <= pushes x rows)
+    nb, per = (32, 1 << 20) if case == "hot_big_leaf" else (16, 1 << 21)
     fmt = DataDesc(0, 1, 1)  # FloatArrayStore, LONG keys
     s, _ = mk_store(fmt, first, first + rows - 1)
     o = oracle_store(oracle, fmt, first, first + rows - 1)
