@@ -2007,8 +2007,7 @@ __global__ __launch_bounds__(256) void k_stream(uint8_t* __restrict__ dst, const
 // Repeated indices race: the array's values are not meaningful afterwards.
 __global__ __launch_bounds__(256) void k_rmw_floor(float* __restrict__ a, const uint32_t* __restrict__ idx,
                                                    const float* __restrict__ v, int64_t n) {
-    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (i < n) {
+    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
         const uint32_t k = idx[i];
         a[k] = a[k] + v[i];
     }
@@ -2016,8 +2015,9 @@ __global__ __launch_bounds__(256) void k_rmw_floor(float* __restrict__ a, const 
 
 hipError_t launch_rmw_floor(float* a, const uint32_t* idx, const float* v, int64_t n, hipStream_t st, LaunchEv ev) {
     if (n <= 0) return hipSuccess;
-    hipExtLaunchKernelGGL(k_rmw_floor, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, st, ev.start, ev.stop, 0, a,
-                          idx, v, n);
+    // one update per thread up to 2^28 updates (config 3: 32e6), grid-stride beyond
+    const unsigned grid = (unsigned)std::min<int64_t>((n + 255) / 256, (int64_t)1 << 20);
+    hipExtLaunchKernelGGL(k_rmw_floor, dim3(grid), dim3(256), 0, st, ev.start, ev.stop, 0, a, idx, v, n);
     return hipGetLastError();
 }
 

@@ -2362,7 +2362,7 @@ int dml_diag_stream(int32_t copy, void* dev_dst, const void* dev_src, int64_t by
 
 int dml_diag_rmw_floor(float* dev_array, const uint32_t* dev_index, const float* dev_values, int64_t n, void* stream,
                        float* ms) {
-    if (!dev_array || n < 0 || (n > 0 && (!dev_index || !dev_values)) || n >= ((int64_t)1 << 40))
+    if (!dev_array || n < 0 || (n > 0 && (!dev_index || !dev_values)))
         return set_err(DML_E_INVALID_ARG, "bad rmw floor arguments");
     hipStream_t st = (hipStream_t)stream;
     hipEvent_t e0 = nullptr, e1 = nullptr;
