@@ -1306,6 +1306,10 @@ def main():
         line["sparse"] = sparse_leg(ctx, L, args.sparse_steps, cpu=not args.no_cpu)
     if rank == 0 and world == 1 and not args.no_cpu and not args.group:
         line["cpu_baseline"] = cpu_baseline()
+    if args.rehearse_gloo and world > 1:
+        # diagnostic only: the collectives ran over gloo through host memory with every
+        # rank on one GPU, so the timing says nothing about xGMI / RCCL
+        line["rehearsal"] = f"gloo collectives, {world} ranks sharing cuda:0 (schedule check, not a measurement)"
     if rank == 0:
         print(json.dumps(line), file=out, flush=True)
     if dist.is_initialized():
