@@ -58,6 +58,7 @@ SIGNATURES = {
     "dml_store_write_dense": (C.c_int, [_vp, _vp, _i64]),
     "dml_store_device_ptr": (C.c_int, [_vp, _P(_vp)]),
     "dml_store_read_adagrad": (C.c_int, [_vp, _vp, _vp, _i64]),
+    "dml_store_read_rows": (C.c_int, [_vp, _i32, _i64, _i64, _vp, _i64]),
     "dml_store_fill": (C.c_int, [_vp, C.c_double]),
     "dml_store_set_alpha": (C.c_int, [_vp, C.c_float, C.c_float, C.c_float]),
     "dml_store_max_delta": (C.c_int, [_vp, _P(C.c_float), _P(_i32), _P(_i32)]),

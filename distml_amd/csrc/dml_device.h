@@ -37,6 +37,30 @@ __device__ inline void stg16_wt(const void* base, uint32_t nbytes, uint32_t off,
     __builtin_amdgcn_raw_buffer_store_b128(v, rsrc, (int)off, 0, 16);
 }
 
+// Buffer resource over [base, base + nbytes) at a wave-uniform base, and its 16-B
+// non-temporal load (aux 2 = nt): 32-bit per-lane offsets instead of 64-bit
+// addresses, and an offset past nbytes reads zeros (the range check), so a masked
+// lane needs no select.
+__device__ inline __amdgpu_buffer_rsrc_t buf_rsrc(const void* base, uint32_t nbytes) {
+    const uint64_t b = (uint64_t)base;
+    const uint32_t lo = __builtin_amdgcn_readfirstlane((uint32_t)b);
+    const uint32_t hi = __builtin_amdgcn_readfirstlane((uint32_t)(b >> 32));
+    const uint32_t n = __builtin_amdgcn_readfirstlane(nbytes);
+    return __builtin_amdgcn_make_buffer_rsrc((void*)(((uint64_t)hi << 32) | lo), (short)0, (int)n, 0x00020000);
+}
+__device__ inline u32x4 ldb16_nt(__amdgpu_buffer_rsrc_t r, uint32_t off) {
+    return __builtin_amdgcn_raw_buffer_load_b128(r, (int)off, 0, 2);
+}
+// A wave-uniform 64-bit value in scalar registers (the compiler then branches on it
+// with scalar branches).
+__device__ inline int64_t uni64(int64_t v) {
+    const uint32_t lo = __builtin_amdgcn_readfirstlane((uint32_t)(uint64_t)v);
+    const uint32_t hi = __builtin_amdgcn_readfirstlane((uint32_t)((uint64_t)v >> 32));
+    return (int64_t)(((uint64_t)hi << 32) | lo);
+}
+__device__ inline uint64_t uni64(uint64_t v) { return (uint64_t)uni64((int64_t)v); }
+constexpr uint32_t kBufOff = 0xFFFFFFF0u;  // an offset past any range: the load reads zeros
+
 __device__ inline uint32_t ld32(const uint8_t* p) { return ldg32(p); }
 __device__ inline int64_t ld_key(const uint8_t* p, int K) {
     // DataDesc.readKey (DataDesc.java:131-138): LE int32 sign-extended, or LE int64.

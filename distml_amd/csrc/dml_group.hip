@@ -109,6 +109,15 @@ struct dml_group {
 
 namespace {
 
+// A/B switch for the race check (scripts/build_ab.sh nofix -DDML_AB_NO_FAIL_ORDER=1): the
+// local-failure path without its stream orders, to show the asynchronous RCCL stand-in
+// (tests/rccl_double) catches the race they close
+#ifdef DML_AB_NO_FAIL_ORDER
+constexpr bool kFailOrder = false;
+#else
+constexpr bool kFailOrder = true;
+#endif
+
 // The oldest pending call: read its verdict (a failed speculation re-runs its
 // pieces exactly), then reduce-scatter its partial on the communication stream
 // and apply the received rows on the store's stream; its errors are returned.
@@ -135,9 +144,12 @@ int finish_front(dml_group* g) {
     uint8_t* rcv = W == 1 ? part : (uint8_t*)g->recv[c.set];
     const int local = rc;
     if (local != DML_OK && W > 1) {
-        // contribute zeros: the pieces (or their re-run) are done with the partial first
+        // contribute zeros: the pieces (or their re-run) are done with the partial first,
+        // and the apply of the call two back (store stream) with this set's recv — a call
+        // that failed in _begin_ctx skipped the host wait for it
         (void)hipStreamSynchronize(g->cstream);
         if (c.h) (void)dml_prereduce_stream_wait(c.h, g->rstream);
+        if (kFailOrder) (void)hipStreamWaitEvent(g->rstream, g->applied[c.set], 0);
         (void)hipMemsetAsync(part, 0, (size_t)(W * S * C) * g->vbytes, g->rstream);
     }
     int crc = DML_OK;  // the collective's own status
@@ -149,10 +161,21 @@ int finish_front(dml_group* g) {
             crc = set_error(DML_E_HIP, std::string("ncclReduceScatter: ") + ncclGetErrorString(r));
     }
     if (local != DML_OK) {
+        // the set stays busy until the zero-contribution reduce-scatter has read the
+        // partial and written recv: its next use (two calls on) waits on applied[set],
+        // which for this call is the scatter itself (there is no apply)
+        if (W > 1 && kFailOrder) {
+            (void)hipEventRecord(g->rs_done[c.set], g->rstream);
+            (void)hipEventRecord(g->applied[c.set], g->rstream);
+        }
         if (c.h) (void)dml_prereduce_end(c.h);
         return local;
     }
-    rc = crc;
+    if (crc != DML_OK) {  // no apply: the set is free once the stream is past the scatter
+        (void)hipEventRecord(g->applied[c.set], g->rstream);
+        (void)dml_prereduce_end(c.h);
+        return crc;
+    }
     if (rc == DML_OK && hipEventRecord(g->rs_done[c.set], g->rstream) != hipSuccess) rc = set_error(DML_E_HIP, "event");
     if (rc == DML_OK && hipStreamWaitEvent(g->sstream, g->rs_done[c.set], 0) != hipSuccess)
         rc = set_error(DML_E_HIP, "stream wait");
@@ -528,6 +551,10 @@ int dml_group_push_moments(dml_group* g, const void* const* dev_bufs, const int6
     }
     const ncclResult_t r = ncclReduceScatter(g->mpart[k], g->mrecv[k], (size_t)(S * 2 * C), ncclFloat32, ncclSum,
                                              g->comm, g->rstream);
+    if (local != DML_OK || r != ncclSuccess) {
+        // no apply: the set's next use (two calls on) waits for the scatter instead
+        (void)hipEventRecord(g->mapplied[k], g->rstream);
+    }
     if (local != DML_OK) {
         if (h) (void)dml_prereduce_end(h);
         return local;

@@ -297,6 +297,20 @@ int64_t reduce_blocks(int vtype, int64_t rows, int32_t cols);
 bool reduce_clears_slots(int vtype, int mode, int32_t cols);
 // The chunk's plain-sum reduce is k_reduce_flat (narrow dense rows), not k_reduce_rows.
 bool use_flat(int vtype, int mode, int32_t cols, const Batch& bt, int nb, int64_t rows);
+// k_flat_ident (dml_kernels.hip): a flat-shape chunk (use_flat, kAdd / kPreReduce)
+// the host has seen, after its index, to be all identity — every push lists every
+// row as record r = row r (flat_ident_ok), no cutoff, no repeated row. Its waves
+// verify every key; a mismatch clears ctrl->spec_ok as k_reduce_flat does.
+constexpr int kFlatIdentWaves = 8;
+hipError_t launch_flat_ident(int vtype, int mode, void* shard, int64_t rows, int32_t cols, const Batch& bt, int nb,
+                             int64_t stride, int K, Ctrl* ctrl, hipStream_t st, int64_t* nblocks_out,
+                             LaunchEv ev = {}, RowMap rm = {});
+// Whether a chunk of nb pushes may run k_flat_ident, from the host's copy of its
+// Ctrl after the index (hctrl) and the pushes' record counts (`need` per push: the
+// model rows).
+bool flat_ident_ok(const Ctrl& hctrl, const Batch& bt, int nb, int64_t need, uint64_t tail_cut);
+// Task rows per wave of k_flat_ident at this width (a row map's blocks must hold whole waves).
+int flat_ident_rows_per_wave(int vtype, int32_t cols);
 // row shapes whose reduce runs identity-speculative chunks (k_reduce_rows FULL, k_reduce_flat)
 bool spec_shape(int vtype, int32_t cols);
 

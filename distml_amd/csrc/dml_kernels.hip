@@ -1155,6 +1155,121 @@ __global__ __launch_bounds__(256) void k_reduce_flat(T* __restrict__ shard, int6
     if (bad) ctrl->spec_ok = 0u;  // an identity push is not: the host re-runs the chunk
 }
 
+// k_flat_ident: k_reduce_flat for the chunks the host has seen to be all identity
+// after the index (every push full-range, verified record r = row r, no cutoff, no
+// repeated row: config 4's steady state), with nothing else in it. Same row / vector
+// ownership and the same adds in push order (bit-identical to k_reduce_flat), but
+//  - record offsets from the wave's first model row are 32-bit per-lane constants
+//    every push shares (buffer loads at a wave-uniform base; a lane without a vector
+//    reads zeros from the range check), no slot table, no LDS;
+//  - a ring of D pushes in flight: push b+D-1's loads are issued before push b's
+//    adds, so a wave never drains to zero between pushes;
+//  - the block's waves write their rows after a block barrier: the shard's writes
+//    leave a CU in one burst instead of trickling between the pushes' reads. Writes
+//    interleaved with this read stream cost ~2.4 TB/s marginal against ~6.8 for reads
+//    (scripts/ubench_flat.hip): the burst is what this kernel gains most from.
+// Keys of every record are still verified (speculative chunks): a mismatch clears
+// ctrl->spec_ok and the host re-runs the chunk exactly, as for k_reduce_flat.
+template <typename T, int MODE, int J, int D, int NW>
+__global__ __launch_bounds__(NW * 64) void k_flat_ident(T* __restrict__ shard, int64_t rows, int32_t cols, int32_t R,
+                                                        const Batch bt, int nb, int64_t stride, int K,
+                                                        Ctrl* __restrict__ ctrl, RowMap rm) {
+    constexpr int VEC = Elem<T>::VEC;
+    static_assert(MODE == kAdd || MODE == kPreReduce, "plain sums only");
+    const int lane = threadIdx.x & 63;
+    const int wid = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    const int64_t t0 = (xcd_block() * NW + wid) * R;
+    // every wave reaches the block barrier below: a wave past the last row, or behind
+    // a predecessor that needs the host first, does no work and writes nothing
+    const bool live = t0 < rows && !(bt.prev && ctrl_abnormal(bt.prev));
+    const int nrow = !live ? 0 : (int)(rows - t0 < (int64_t)R ? rows - t0 : (int64_t)R);
+    const int NV = cols / VEC, nvec = nrow * NV;
+    const int64_t mr0 = live ? uni64(rm.row(t0)) : 0;
+    const int64_t mrl = live ? uni64(rm.row(t0 + nrow - 1)) : 0;
+    // per lane j: record offset from record mr0 (push buffers), element offset from
+    // row mr0 (input shard) and from the output base; kBufOff = no vector here
+    uint32_t loff[J], soff[J], ooff[J];
+#pragma unroll
+    for (int j = 0; j < J; ++j) {
+        const int v = j * 64 + lane;
+        const int rl = v / NV, cv = v - rl * NV;
+        const bool on = v < nvec;
+        const int64_t mr = on ? rm.row(t0 + rl) : mr0;
+        const bool pad = rm.block && mr >= rm.rows_total;  // padding row of a short last shard
+        loff[j] = on && !pad ? (uint32_t)((mr - mr0) * stride + K + cv * 16) : kBufOff;
+        soff[j] = on && !pad ? (uint32_t)(((mr - mr0) * cols + cv * VEC) * (int64_t)sizeof(T)) : kBufOff;
+        const int64_t orow = rm.out ? (int64_t)rl : mr - mr0;
+        ooff[j] = on ? (uint32_t)((orow * cols + cv * VEC) * (int64_t)sizeof(T)) : kBufOff;
+    }
+    const uint32_t span = (uint32_t)((mrl - mr0 + 1) * stride);  // records mr0 .. mrl
+    const uint32_t sspan = (uint32_t)((mrl - mr0 + 1) * cols * (int64_t)sizeof(T));
+    T acc[J][VEC];
+    bool bad = false;
+    if (live) {
+        if constexpr (MODE == kAdd) {
+            // the input rows: in place, or the speculative chunk's input buffer
+            const T* const ib = (bt.src ? (const T*)bt.src : shard) + mr0 * cols;
+            const __amdgpu_buffer_rsrc_t is = buf_rsrc(ib, sspan);
+#pragma unroll
+            for (int j = 0; j < J; ++j) unpack<T>(ldb16_nt(is, soff[j]), acc[j]);
+        } else {
+#pragma unroll
+            for (int j = 0; j < J; ++j)
+#pragma unroll
+                for (int e = 0; e < VEC; ++e) acc[j][e] = T(0);
+        }
+        // key verification: lane l < nrow checks the record of task row t0 + l
+        const int64_t lrow = rm.row(t0 + lane);
+        const bool lchk = bt.spec && lane < nrow && !(rm.block && lrow >= rm.rows_total);
+        const int64_t vrows = rm.block ? rm.rows_total : rows;
+        const uint32_t koff = lchk ? (uint32_t)((lrow - mr0) * stride) : kBufOff;
+        u32x4 ring[D][J];
+        uint32_t key[D];
+        auto issue = [&](int b, u32x4 (&raw)[J], uint32_t& k) {
+            const __amdgpu_buffer_rsrc_t rs = buf_rsrc(bt.base[b] + mr0 * stride, span);
+            k = __builtin_amdgcn_raw_buffer_load_b32(rs, (int)koff, 0, 2);  // the key's low word
+#pragma unroll
+            for (int j = 0; j < J; ++j) raw[j] = ldb16_nt(rs, loff[j]);
+        };
+        auto add = [&](const u32x4 (&raw)[J], uint32_t k, int b) {
+#pragma unroll
+            for (int j = 0; j < J; ++j) {
+                T u[VEC];
+                unpack<T>(raw[j], u);
+#pragma unroll
+                for (int e = 0; e < VEC; ++e) acc[j][e] = Elem<T>::add(acc[j][e], u[e]);
+            }
+            if (lchk) {
+                // 8-byte keys: the high word beside the low one (one more load, rare shape)
+                const int64_t kv =
+                    K == 4 ? (int64_t)(int32_t)k
+                           : (int64_t)((uint64_t)k | ((uint64_t)ld32(bt.base[b] + lrow * stride + 4) << 32));
+                bad |= row_index(kv, bt.first, vrows) != lrow;
+            }
+        };
+#pragma unroll
+        for (int d = 0; d < D - 1; ++d)
+            if (d < nb) issue(d, ring[d], key[d]);
+#pragma unroll 1
+        for (int b0 = 0; b0 < nb; b0 += D) {
+#pragma unroll
+            for (int d = 0; d < D; ++d) {
+                const int b = b0 + d, bn = b + D - 1;  // bn's loads go to slot (d + D - 1) % D
+                if (bn < nb) issue(bn, ring[(d + D - 1) % D], key[(d + D - 1) % D]);
+                if (b < nb) add(ring[d], key[d], b);
+            }
+        }
+    }
+    // every wave of the block has read its rows: the block's writes leave together
+    __syncthreads();
+    if (!live) return;
+    T* const ob = rm.out ? (T*)rm.out + t0 * (int64_t)cols : shard + mr0 * cols;
+    const __amdgpu_buffer_rsrc_t os = buf_rsrc(ob, rm.out ? (uint32_t)(nrow * cols * (int64_t)sizeof(T)) : sspan);
+#pragma unroll
+    for (int j = 0; j < J; ++j) __builtin_amdgcn_raw_buffer_store_b128(pack<T>(acc[j]), os, (int)ooff[j], 0, 2);
+    if (bad) ctrl->spec_ok = 0u;  // an identity push is not: the host re-runs the chunk
+}
+
 // k_ada_flat: FloatMatrixStoreAdaGrad's push (FloatMatrixStoreAdaGrad.java:262-277)
 // in k_reduce_flat's layout, for rows narrower than 4 KiB whose pushes list most
 // rows (config 4's AdaGrad variant: 800-B rows). k_reduce gives such a row one
@@ -1521,6 +1636,50 @@ static hipError_t launch_flat(void* shard, int64_t rows, int32_t cols, const Bat
                                          nblocks_out, ev, rm);
 }
 
+// k_flat_ident launch: the all-identity chunks of the flat shape (the host checked
+// the index's Ctrl). J = 8 vectors per lane (10 rows of 200 fp32 per wave), three
+// pushes in flight, 8-wave blocks (one per CU at 2 waves per SIMD): the best of the
+// shapes scripts/ubench_flat.hip measured (config 4: 0.768 of 8 TB/s against 0.727
+// for k_reduce_flat's loop on one box).
+constexpr int kFlatIdentJ = 8;  // 16-B vectors per lane
+
+int flat_ident_rows_per_wave(int vtype, int32_t cols) {
+    const int NV = cols / (vtype == kF64 ? 2 : 4);
+    return std::max(1, std::min(16, kFlatIdentJ * 64 / std::max(NV, 1)));
+}
+
+template <typename T, int MODE>
+static hipError_t launch_flat_ident_t(void* shard, int64_t rows, int32_t cols, const Batch& bt, int nb,
+                                      int64_t stride, int K, Ctrl* ctrl, hipStream_t st, int64_t* nblocks_out,
+                                      LaunchEv ev, RowMap rm) {
+    constexpr int VEC = Elem<T>::VEC, J = kFlatIdentJ, D = 3, NW = kFlatIdentWaves;
+    const int NV = cols / VEC;
+    const int R = std::max(1, std::min(16, J * 64 / NV));
+    const int64_t nblocks = ((rows + R - 1) / R + NW - 1) / NW;
+    if (nblocks_out) *nblocks_out = nblocks;
+    if (nblocks <= 0) return hipSuccess;
+    static const std::string kn = kname("k_flat_ident", type_name<T>(), MODE, J, D, NW);
+    g_kernel_name = kn.c_str();
+    if (ev.start || ev.stop)
+        hipExtLaunchKernelGGL((k_flat_ident<T, MODE, J, D, NW>), dim3((unsigned)nblocks), dim3(NW * 64), 0, st,
+                              ev.start, ev.stop, 0, (T*)shard, rows, cols, R, bt, nb, stride, K, ctrl, rm);
+    else
+        hipLaunchKernelGGL((k_flat_ident<T, MODE, J, D, NW>), dim3((unsigned)nblocks), dim3(NW * 64), 0, st,
+                           (T*)shard, rows, cols, R, bt, nb, stride, K, ctrl, rm);
+    return hipGetLastError();
+}
+
+hipError_t launch_flat_ident(int vtype, int mode, void* shard, int64_t rows, int32_t cols, const Batch& bt, int nb,
+                             int64_t stride, int K, Ctrl* ctrl, hipStream_t st, int64_t* nblocks_out, LaunchEv ev,
+                             RowMap rm) {
+#define DML_FI(T, M) launch_flat_ident_t<T, M>(shard, rows, cols, bt, nb, stride, K, ctrl, st, nblocks_out, ev, rm)
+    if (vtype == kF32) return mode == kAdd ? DML_FI(float, kAdd) : DML_FI(float, kPreReduce);
+    if (vtype == kI32) return mode == kAdd ? DML_FI(int32_t, kAdd) : DML_FI(int32_t, kPreReduce);
+    if (vtype == kF64) return mode == kAdd ? DML_FI(double, kAdd) : DML_FI(double, kPreReduce);
+#undef DML_FI
+    return hipErrorInvalidValue;
+}
+
 // The flat narrow-row kernels apply to plain sums (and AdaGrad chunks of at most 4
 // pushes) of rows narrower than 4 KiB (whole vectors) when every push of the chunk
 // lists at least half the rows (dense pushes; sparse ones keep the pair-packed
@@ -1532,6 +1691,13 @@ bool use_flat(int vtype, int mode, int32_t cols, const Batch& bt, int nb, int64_
     if (cols % VEC || (int64_t)cols * elem >= 4096 || nb <= 0) return false;
     for (int b = 0; b < nb; ++b)
         if (2 * bt.nrec[b] < rows) return false;
+    return true;
+}
+
+bool flat_ident_ok(const Ctrl& h, const Batch& bt, int nb, int64_t need, uint64_t tail_cut) {
+    if (nb <= 0 || tail_cut != kNoPos || h.cutoff != kNoPos || h.no_dup == 0u) return false;
+    for (int b = 0; b < nb; ++b)
+        if (!ctrl_identity(&h, h.ident, b) || bt.nrec[b] < need) return false;
     return true;
 }
 

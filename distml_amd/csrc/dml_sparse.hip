@@ -1053,6 +1053,10 @@ void sparse_plan_big(SpPlan& pl, const Batch& bt, int64_t rows) {
     const int64_t mean = pl.nrec / nbig;
     // the compact word: value | push << 32 | row within the big leaf << 38
     if (BL > 24 || mean < kSpBigCap / 6 || mean > kSpBigCap * 17 / 24) return;
+    // the exact replay re-plans a big leaf's chunk with BL inside the layout sized for
+    // the two-level plan (SL): in bounds only while big leaves are at least as large
+    // (fewer, larger leaves), so refuse the one-level pass otherwise
+    if (BL < pl.SL) return;
     int64_t srec[kSpSlices] = {0}, stile[kSpSlices] = {0};
     for (int b = 0; b < pl.nb; ++b) {
         pl.sbase[b] = stile[b % kSpSlices];

@@ -190,6 +190,8 @@ struct Workspace {
     uint8_t* sp = nullptr;            // sparse partition buffers (SpLayout), grown on demand
     size_t sp_cap = 0;
     SpStat* hsp = nullptr;            // pinned status of the single-pass sparse partition
+    Ctrl* hidx = nullptr;             // pinned copy of ctrl right after the index (flat speculative chunks)
+    bool flat_ident = false;          // the chunk's apply runs k_flat_ident (chosen from hidx)
     bool clears = false;              // the chunk's reduce leaves its slot table all -1
     bool clean = false;               // slot table all -1 and rowflags 0: only the Ctrl needs a reset
     // Kept slot table (the last chunk here was a verified speculative chunk): rowflags
@@ -465,8 +467,12 @@ int launch_apply(dml_store* s, Chunk& c, Workspace& W, const Ctrl* prev) {
         int64_t nblk = 0;
         W.clears = reduce_clears_slots(vtype_of(s->desc), reduce_mode(s), s->cols);
         c.bt.src = c.in != c.out ? c.in : nullptr;
-        HIPCHK(launch_reduce(vtype_of(s->desc), reduce_mode(s), c.out, s->rows, s->cols, c.bt, c.nb, s->stride,
-                             s->K, W.slot, W.rowflag, W.ctrl, c.tail_cut, ada_args(s), s->stream, &nblk, ev));
+        if (W.flat_ident)  // every push verified-identity by the index (the host's Ctrl copy)
+            HIPCHK(launch_flat_ident(vtype_of(s->desc), reduce_mode(s), c.out, s->rows, s->cols, c.bt, c.nb,
+                                     s->stride, s->K, W.ctrl, s->stream, &nblk, ev));
+        else
+            HIPCHK(launch_reduce(vtype_of(s->desc), reduce_mode(s), c.out, s->rows, s->cols, c.bt, c.nb, s->stride,
+                                 s->K, W.slot, W.rowflag, W.ctrl, c.tail_cut, ada_args(s), s->stream, &nblk, ev));
         if (s->adagrad)
             // finalized here unless the index saw a repeated row: then after its replay
             HIPCHK(launch_maxdelta_finalize(s->cand, nblk, s->md, c.bt, c.nb, s->stride, s->K, s->V, s->stream,
@@ -528,6 +534,17 @@ int launch_chunk(dml_store* s, Chunk& c, Workspace& W, const Ctrl* prev) {
         }
         HIPCHK(launch_index(c.bt, c.nb, c.max_nrec, s->stride, s->K, s->first, s->rows, W.slot, W.rowflag, W.ctrl,
                             c.tail_cut, is));
+        // A speculative chunk of the flat shape: its Ctrl (identity / kept columns,
+        // cutoff, repeats) is final here; a pinned copy lets the host pick the lean
+        // all-identity kernel after the wait below (k_flat_ident)
+        W.flat_ident = false;
+        if (c.spec && reduce_mode(s) == kAdd && c.tail_cut == kNoPos &&
+            use_flat(vtype_of(s->desc), kAdd, s->cols, c.bt, c.nb, s->rows)) {
+            if (!W.hidx) HIPCHK(hipHostMalloc((void**)&W.hidx, sizeof(Ctrl), hipHostMallocDefault));
+            W.hidx->cutoff = 0;  // not all-identity unless the copy lands
+            HIPCHK(hipMemcpyAsync(W.hidx, W.ctrl, sizeof(Ctrl), hipMemcpyDeviceToHost, is));
+            W.flat_ident = true;  // provisional: decided after idx_done
+        }
     } else {
         // arrays: partition the chunk by leaf (row range) for the ordered per-leaf
         // apply (its first pass also finds the cutoff); int32 leaves check every add
@@ -564,6 +581,7 @@ int launch_chunk(dml_store* s, Chunk& c, Workspace& W, const Ctrl* prev) {
     // directly behind that reduce. A cross-queue barrier packet instead costs
     // ~16 µs of idle GPU between the two reduces (measured).
     HIPCHK(hipEventSynchronize(W.idx_done));
+    if (W.flat_ident) W.flat_ident = flat_ident_ok(*W.hidx, c.bt, c.nb, s->rows, c.tail_cut);
     if (c.sorted && c.sp.fast) {
         const uint64_t pcut = std::min<uint64_t>(W.hsp->cutoff, c.tail_cut);
         if (W.hsp->overflow || (c.sp.compact && pcut != kNoPos)) {
@@ -1111,6 +1129,7 @@ void dml_store_destroy(dml_store* s) {
             (void)hipFree(W.base);
             (void)hipFree(W.sp);
             if (W.hsp) (void)hipHostFree(W.hsp);
+            if (W.hidx) (void)hipHostFree(W.hidx);
             if (W.hctrl) (void)hipHostFree(W.hctrl);
             if (W.idx_done) (void)hipEventDestroy(W.idx_done);
             if (W.done) (void)hipEventDestroy(W.done);
@@ -1321,6 +1340,24 @@ int dml_store_read_adagrad(dml_store* s, float* alpha_dst, float* delta_dst, int
     const size_t n = (size_t)(s->rows * s->cols) * 4;
     if (alpha_dst) HIPCHK(hipMemcpyAsync(alpha_dst, s->alpha, n, hipMemcpyDeviceToHost, s->stream));
     if (delta_dst) HIPCHK(hipMemcpyAsync(delta_dst, s->delta, n, hipMemcpyDeviceToHost, s->stream));
+    HIPCHK(hipStreamSynchronize(s->stream));
+    return DML_OK;
+}
+
+int dml_store_read_rows(dml_store* s, int32_t which, int64_t row0, int64_t nrows, void* host_dst, int64_t bytes) {
+    if (int rc = check_store(s)) return rc;
+    std::lock_guard<std::mutex> lk(s->mu);
+    DeviceGuard g(s->device);
+    if (which < 0 || which > 2 || row0 < 0 || nrows < 0 || row0 > s->rows || nrows > s->rows - row0)
+        return set_err(DML_E_INVALID_ARG, "bad row range or array");
+    if (which != 0 && !s->adagrad) return set_err(DML_E_UNSUPPORTED, "not an AdaGrad store");
+    const int64_t esz = which == 0 ? s->V : 4;
+    const int64_t need = nrows * s->cols * esz;
+    if (need > 0 && (!host_dst || bytes < need)) return set_err(DML_E_CAPACITY, "destination too small");
+    if (int rc = begin_call(s)) return rc;
+    if (need == 0) return DML_OK;
+    const uint8_t* src = (const uint8_t*)(which == 0 ? s->data : which == 1 ? (void*)s->alpha : (void*)s->delta);
+    HIPCHK(hipMemcpyAsync(host_dst, src + row0 * s->cols * esz, (size_t)need, hipMemcpyDeviceToHost, s->stream));
     HIPCHK(hipStreamSynchronize(s->stream));
     return DML_OK;
 }
@@ -1763,6 +1800,7 @@ struct dml_prereduce {
     };
     std::vector<PieceRec> prec;  // the pieces as launched (a failed verification re-runs them)
     hipEvent_t rerun_ev = nullptr;
+    const Ctrl* hidx = nullptr;  // the workspace's Ctrl as the index left it (speculative calls of the flat shape)
 };
 
 // Pre-reduce context (dml_prectx_*): the sharded path's pre-reduce with the
@@ -1776,6 +1814,7 @@ struct PreWs {
     int32_t* slot = nullptr;
     uint32_t* rowflag = nullptr;
     Ctrl* hctrl = nullptr;          // pinned Ctrl, copied after the pieces (or their re-run)
+    Ctrl* hidx = nullptr;           // pinned Ctrl, copied right after the index (k_flat_ident's choice)
     hipEvent_t ctrl_ev = nullptr;   // that copy done
     hipEvent_t free_ev = nullptr;   // the workspace's last call ended (pieces / re-run done)
     bool used = false, clean = false, kept = false;
@@ -2049,8 +2088,16 @@ int dml_prereduce_piece(dml_prereduce* p, int64_t row_block, int64_t row_stride,
         p->tev.push_back(t);
         ev = LaunchEv{t.first, t.second};
     }
-    HIPCHK(launch_reduce(p->desc.value_type, kPreReduce, dev_out, ntask_rows, p->cols, p->bt, p->nb, p->stride, p->K,
-                         p->slot, nullptr, p->ctrl, kNoPos, none, st, nullptr, ev, rm));
+    // all-identity calls (seen in the index's Ctrl, once the host has waited for it):
+    // the lean kernel, when no wave's rows straddle two row blocks of the map
+    const int Rw = flat_ident_rows_per_wave(p->desc.value_type, p->cols);
+    if (p->hidx && p->idx_waited && (row_block % Rw == 0 || ntask_rows <= row_block) &&
+        flat_ident_ok(*p->hidx, p->bt, p->nb, p->rows, kNoPos))
+        HIPCHK(launch_flat_ident(p->desc.value_type, kPreReduce, dev_out, ntask_rows, p->cols, p->bt, p->nb, p->stride,
+                                 p->K, p->ctrl, st, nullptr, ev, rm));
+    else
+        HIPCHK(launch_reduce(p->desc.value_type, kPreReduce, dev_out, ntask_rows, p->cols, p->bt, p->nb, p->stride,
+                             p->K, p->slot, nullptr, p->ctrl, kNoPos, none, st, nullptr, ev, rm));
     p->done_ev = ev.stop;
     p->prec.push_back({row_block, row_stride, row_off, ntask_rows, dev_out});
     // model rows this piece covered: blocks of row_block task rows at row_off + q*row_stride
@@ -2215,6 +2262,7 @@ void dml_prectx_destroy(dml_prectx* x) {
         for (PreWs& W : x->ws) {
             if (W.free_ev) (void)hipEventSynchronize(W.free_ev);
             (void)hipFree(W.base);
+            if (W.hidx) (void)hipHostFree(W.hidx);
             if (W.hctrl) (void)hipHostFree(W.hctrl);
             if (W.ctrl_ev) (void)hipEventDestroy(W.ctrl_ev);
             if (W.free_ev) (void)hipEventDestroy(W.free_ev);
@@ -2304,6 +2352,17 @@ int dml_prereduce_begin_ctx(dml_prectx* x, const void* const* dev_bufs, const in
     if (e == hipSuccess)
         e = launch_index(p->bt, n, p->max_nrec, p->stride, p->K, x->first, x->rows, W.slot, W.rowflag, W.ctrl, kNoPos,
                          st);
+    // speculative calls of the flat shape: a pinned copy of the Ctrl the index left, so
+    // that the pieces (after the host's wait for the index) can run k_flat_ident
+    p->hidx = nullptr;
+    if (e == hipSuccess && p->spec && use_flat(vt, kPreReduce, x->cols, p->bt, n, x->rows)) {
+        if (!W.hidx) e = hipHostMalloc((void**)&W.hidx, sizeof(Ctrl), hipHostMallocDefault);
+        if (e == hipSuccess) {
+            W.hidx->cutoff = 0;  // not all-identity unless the copy lands
+            e = hipMemcpyAsync(W.hidx, W.ctrl, sizeof(Ctrl), hipMemcpyDeviceToHost, st);
+            p->hidx = W.hidx;
+        }
+    }
     if (e == hipSuccess) e = hipEventCreateWithFlags(&p->idx_ev, hipEventDisableTiming);
     if (e == hipSuccess) e = hipEventRecord(p->idx_ev, st);
     if (e != hipSuccess) {

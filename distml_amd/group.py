@@ -257,23 +257,41 @@ class ShardGroup:
         partial = self._partials[k]
         if self._pctx is None:
             self._pctx = self.ops.ctx_create(self.fmt, 0, self.total_rows, cols, self.device)
-        h = self.ops.begin_ctx(self._pctx, dev_ptrs, lens, self.istream.cuda_stream)
-        # buffer set k was last used two calls ago: its apply (queued behind its
-        # reduce-scatter) has finished with recv[k], and so has the scatter with partial[k]
-        self._applied[k].synchronize()
+        h, local = None, None
         try:
+            h = self.ops.begin_ctx(self._pctx, dev_ptrs, lens, self.istream.cuda_stream)
+            # buffer set k was last used two calls ago: its apply (queued behind its
+            # reduce-scatter) has finished with recv[k], and so has the scatter with partial[k]
+            self._applied[k].synchronize()
             for j in range(P):
                 piece = partial[j * world * blk * cols:(j + 1) * world * blk * cols]
                 self.ops.piece(h, blk, S, j * blk, world * blk, piece.data_ptr(), st)
-        except BaseException:
-            self.ops.end(h)
-            raise
-        self._pending.append((h, k))
-        self._end_pending(keep=1)  # the previous call: verdict, reduce-scatter, apply, errors
+        except Exception as e:
+            # a call that fails here (begin: not whole records, a fourth outstanding call;
+            # a piece) still takes its place in the collective sequence: _finish
+            # contributes zeros for it and raises e (as dml_group_push_full_range)
+            if h is not None:
+                self.ops.end(h)
+                h = None
+            local = e
+        self._pending.append((h, k, local))
+        err = None
+        try:
+            self._end_pending(keep=1)  # the previous call: verdict, reduce-scatter, apply, errors
+        except Exception as e:
+            err = e
+        if local is not None:
+            try:
+                self._end_pending(keep=0)  # this call's zeros, its failure raised now
+            except Exception as e:
+                err = err or e
+        if err is not None:
+            raise err
 
-    def _finish(self, h, k) -> None:
+    def _finish(self, h, k, local=None) -> None:
         """A pending call: verdict (exact re-run if the speculation failed), its slices'
-        reduce-scatter on the communication stream, the owner apply, its errors."""
+        reduce-scatter on the communication stream, the owner apply, its errors.
+        `local`: the call already failed before its pieces were recorded (h is None)."""
         torch = self.torch
         S, P, cols, world = self.step_rows, self.pieces, self.cols, self.world
         blk = S // P
@@ -283,15 +301,25 @@ class ShardGroup:
                 # one rank: the [rank][row] slices are the shard's rows in order, so
                 # the reduce-scatter is the identity and the apply reads the partial
                 recv = partial
-            failed = None
-            try:
-                self.ops.verify(h)
-                self.ops.stream_wait(h, self.comm.cuda_stream)  # the pieces (or their re-run)
-            except Exception as e:
+            failed = local
+            if failed is None:
+                try:
+                    self.ops.verify(h)
+                    self.ops.stream_wait(h, self.comm.cuda_stream)  # the pieces (or their re-run)
+                except Exception as e:
+                    failed = e
+            if failed is not None:
                 # every rank runs the same collectives whatever fails locally:
-                # this rank contributes zeros, skips its apply and raises afterwards
-                failed = e
+                # this rank contributes zeros, skips its apply and raises afterwards. The
+                # zeros go in after the pieces and any re-run of them and after
+                # the apply of the call two back, which may still read recv[k]
+                if h is not None:
+                    try:
+                        self.ops.stream_wait(h, self.comm.cuda_stream)
+                    except Exception:
+                        pass
                 self.cstream.synchronize()
+                self.comm.wait_event(self._applied[k])
                 with torch.cuda.stream(self.comm):
                     partial.zero_()
             with torch.cuda.stream(self.comm):
@@ -299,6 +327,9 @@ class ShardGroup:
                     self._rs(recv[j * blk * cols:(j + 1) * blk * cols],
                              partial[j * world * blk * cols:(j + 1) * world * blk * cols])
             if failed is not None:
+                # no apply: the set's next use (two calls on) waits for the scatter instead
+                self._rs_done[k].record(self.comm)
+                self._applied[k].record(self.comm)
                 raise failed
             if self.emulate_world < 0:
                 self._rs_done[k].record(self.comm)
@@ -326,11 +357,21 @@ class ShardGroup:
             if self._store_stream is not None:
                 self._applied[k].record(self._store_stream)
         finally:
-            self.ops.end(h)
+            if h is not None:
+                self.ops.end(h)
 
     def _end_pending(self, keep: int = 0) -> None:
+        """Finish the oldest calls until `keep` remain, every one of them even when one
+        raises (each still issues its collectives, as dml_group's end_pending); the
+        first error is raised after them."""
+        err = None
         while len(self._pending) > keep:
-            self._finish(*self._pending.pop(0))
+            try:
+                self._finish(*self._pending.pop(0))
+            except Exception as e:
+                err = err or e
+        if err is not None:
+            raise err
 
     def prereduce_stats(self, reset: bool = False) -> dict:
         """dml_prectx_stats of the speculative pre-reduce (identity / reused / indexed pushes)."""

@@ -14,6 +14,7 @@ Exceptions mirror the Java ones the reference throws out of handlePush:
 from __future__ import annotations
 
 import ctypes as C
+import re
 import struct
 import weakref
 from typing import List, Optional, Sequence
@@ -86,7 +87,9 @@ def java_parse_float(text: str) -> float:
         if exact is None:
             raise ValueError(f"NumberFormatException: {text!r}")
     else:
-        if not body or body.lower() in ("inf", "nan", "infinity") or "_" in body:
+        # Java's FloatingDecimal grammar: digits, one '.', an exponent — not Python's
+        # Fraction extras ('1/2', '_' separators)
+        if not re.fullmatch(r"[+-]?(\d+\.?\d*|\.\d+)([eE][+-]?\d+)?", t):
             raise ValueError(f"NumberFormatException: {text!r}")
         exact = Fraction(t)
     with np.errstate(over="ignore"):

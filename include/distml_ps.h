@@ -171,6 +171,14 @@ int dml_store_write_dense(dml_store* s, const void* host_src, int64_t bytes);
 int dml_store_device_ptr(dml_store* s, void** dev_ptr);
 /* AdaGrad side arrays (FloatMatrixStoreAdaGrad.java:23-24), f32 row-major. */
 int dml_store_read_adagrad(dml_store* s, float* alpha_dst, float* delta_dst, int64_t elems);
+/* Local rows [row0, row0 + nrows) of the shard's values (which 0, the store's value
+ * type), or of AdaGrad's alpha (1) / delta (2) (f32), row-major and native-endian,
+ * after every accepted push: the snapshot behind the stores' Iter, which the
+ * result-collect paths read (DoubleArrayStore.java:129-157, FloatMatrixStore.java:241-269,
+ * FloatArrayStore.java:124-152, FloatMatrixStoreAdaGrad.java:308-337; called from
+ * LogisticRegression.scala:290-291 and Word2Vec.scala:814-817). Row ranges let a JVM
+ * fill its heap arrays in bounded chunks. */
+int dml_store_read_rows(dml_store* s, int32_t which, int64_t row0, int64_t nrows, void* host_dst, int64_t bytes);
 
 /* DataStore.rand() (DataStore.java:22; PSActor OP_RAND, PSActor.java:181-201).
  * DoubleMatrixStore: exactly the reference's values — java.util.Random(1L) on every

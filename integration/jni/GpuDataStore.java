@@ -11,9 +11,14 @@ import java.io.IOException;
 import java.util.Iterator;
 
 /**
- * DataStore backed by libdistml_ps (MI355X, HBM-resident shard, HIP kernels).
- * Drop-in for the seven typed stores that DataStore.createStore returns
- * (DataStore.java:50-92): same methods, same byte layouts, same exceptions.
+ * DataStore backed by libdistml_ps (MI355X, HBM-resident shard, HIP kernels): the
+ * push / fetch / checkpoint / init methods of the seven typed stores that
+ * DataStore.createStore returns (DataStore.java:50-92), same byte layouts, same
+ * exceptions. Callers that downcast a store to its concrete class and iterate it
+ * (LogisticRegression.scala:290-291, Word2Vec.scala:814-817) get the typed
+ * subclasses from GpuStores.createStore (GpuDoubleArrayStore extends
+ * DoubleArrayStore, ...), which delegate here and fill the parent's localData
+ * from a snapshot of the shard in iter().
  * Native methods are implemented in dml_jni.cc over include/distml_ps.h.
  */
 public class GpuDataStore extends DataStore {
@@ -52,6 +57,8 @@ public class GpuDataStore extends DataStore {
     public void set(String value) {
         if (floatMatrix) nativeFill(handle, Float.parseFloat(value));
     }
+    /** FloatMatrixStore.setValue (FloatMatrixStore.java:61-71): zero(String) fills 0f. */
+    void fill(float v) { nativeFill(handle, v); }
     public void setAlpha(float initialAlpha, float minAlpha, float factor) {
         nativeSetAlpha(handle, initialAlpha, minAlpha, factor);
     }
@@ -99,21 +106,33 @@ public class GpuDataStore extends DataStore {
 
     public void close() { nativeDestroy(handle); }
 
-    private static native long nativeCreate(int dataType, int keyType, int valueType, int denseRow, int denseColumn,
+    /** Copy the shard (which 0), or AdaGrad's alpha (1) / delta (2), into dst: a
+     *  T[rows][rowSize] for matrices, a T[rows] for arrays; T = the element type
+     *  DataDesc names (ELEMENT_TYPE_INT / FLOAT / DOUBLE). Every accepted push is
+     *  applied first (dml_store_read_rows). */
+    void snapshot(int which, int elemType, Object dst) {
+        nativeSnapshot(handle, which, elemType, dst instanceof Object[] ? 2 : 1, dst);
+    }
+    /** FloatMatrixStoreAdaGrad's maxDelta; rowCol receives maxDeltaRow, maxDeltaCol. */
+    float maxDelta(int[] rowCol) { return nativeMaxDelta(handle, rowCol); }
+
+    static native long nativeCreate(int dataType, int keyType, int valueType, int denseRow, int denseColumn,
                                             int adaGrad, long firstKey, long lastKey, int cols, int device, int flags);
-    private static native void nativePush(long h, byte[] data);
-    private static native byte[] nativeFetch(long h, long[] keys);
-    private static native byte[] nativeFetchRange(long h, long first, long last);
-    private static native byte[] nativeWriteAll(long h);
-    private static native void nativeReadAll(long h, byte[] be);
-    private static native long nativeShardBytes(long h);
-    private static native byte[] nativeSyncTo(long h, int from, int to);
-    private static native void nativeSyncFrom(long h, int from, int to, byte[] be);
-    private static native java.nio.ByteBuffer nativeHostAlloc(long bytes);
-    private static native void nativeHostFree(java.nio.ByteBuffer b);
-    private static native void nativePushDirect(long h, java.nio.ByteBuffer b, int offset, int len);
-    private static native void nativeFill(long h, double v);
-    private static native void nativeRand(long h, long seed);
-    private static native void nativeSetAlpha(long h, float a, float min, float factor);
-    private static native void nativeDestroy(long h);
+    static native void nativePush(long h, byte[] data);
+    static native byte[] nativeFetch(long h, long[] keys);
+    static native byte[] nativeFetchRange(long h, long first, long last);
+    static native byte[] nativeWriteAll(long h);
+    static native void nativeReadAll(long h, byte[] be);
+    static native long nativeShardBytes(long h);
+    static native byte[] nativeSyncTo(long h, int from, int to);
+    static native void nativeSyncFrom(long h, int from, int to, byte[] be);
+    static native java.nio.ByteBuffer nativeHostAlloc(long bytes);
+    static native void nativeHostFree(java.nio.ByteBuffer b);
+    static native void nativePushDirect(long h, java.nio.ByteBuffer b, int offset, int len);
+    static native void nativeFill(long h, double v);
+    static native void nativeRand(long h, long seed);
+    static native void nativeSetAlpha(long h, float a, float min, float factor);
+    static native void nativeDestroy(long h);
+    static native void nativeSnapshot(long h, int which, int elemType, int dims, Object dst);
+    static native float nativeMaxDelta(long h, int[] rowCol);
 }

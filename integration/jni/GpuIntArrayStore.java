@@ -1,0 +1,51 @@
+package com.intel.distml.util.store;
+
+import com.intel.distml.util.DataDesc;
+import com.intel.distml.util.KeyCollection;
+
+import java.io.DataInputStream;
+import java.io.DataOutputStream;
+import java.io.IOException;
+
+/**
+ * IntArrayStore whose shard lives in HBM (GpuDataStore, libdistml_ps): every method the
+ * parent implements on localData runs on the GPU, so the JVM heap holds no copy of
+ * the shard (IntArrayStore.java:29-34). localData stays null until snapshot()
+ * fills it from the device.
+ * Created by GpuStores.createStore (the DataStore.createStore dispatch, DataStore.java:50-92).
+ */
+public class GpuIntArrayStore extends IntArrayStore {
+    private final DataDesc format;
+    private final int device;
+    private GpuDataStore gpu;
+
+    public GpuIntArrayStore(DataDesc format, int device) {
+        this.format = format;
+        this.device = device;
+    }
+
+    /** IntArrayStore.init without the heap array: the shard is zero-filled in HBM. */
+    public void init(KeyCollection keys) {
+        gpu = new GpuDataStore(format, GpuStores.range(keys), 1, device);
+        localRows = keys;
+    }
+
+    public KeyCollection rows() { return localRows; }
+    public int rowSize() { return 1; }
+    public byte[] handleFetch(DataDesc format, KeyCollection rows) { return gpu.handleFetch(format, rows); }
+    public void writeAll(DataOutputStream os) throws IOException { gpu.writeAll(os); }
+    public void readAll(DataInputStream is) throws IOException { gpu.readAll(is); }
+    public void syncTo(DataOutputStream os, int fromRow, int toRow) throws IOException { gpu.syncTo(os, fromRow, toRow); }
+    public void syncFrom(DataInputStream is, int fromRow, int toRow) throws IOException { gpu.syncFrom(is, fromRow, toRow); }
+    /** The device store behind this one (pinned wire ingest, handlePushDirect). */
+    public GpuDataStore gpu() { return gpu; }
+    public void close() { gpu.close(); }
+    public void handlePush(DataDesc format, byte[] data) { gpu.handlePush(format, data); }
+
+    /** Fill the parent's localData from the device shard (every accepted
+     *  push applied): the state the reference store holds at this point. */
+    public void snapshot() {
+        if (localData == null) localData = new int[(int) localRows.size()];
+        gpu.snapshot(0, DataDesc.ELEMENT_TYPE_INT, localData);
+    }
+}

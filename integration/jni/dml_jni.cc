@@ -6,6 +6,7 @@
 // IntMatrixStore.java:175, array bounds): see include/distml_ps.h.
 #include <jni.h>
 
+#include <algorithm>
 #include <cstddef>
 #include <cstdint>
 
@@ -90,19 +91,33 @@ JNIEXPORT void JNICALL FN(nativeRand)(JNIEnv* env, jclass, jlong h, jlong seed) 
     if (int rc = dml_store_rand(H(h), (uint64_t)seed)) throw_for(env, rc);
 }
 
+// Largest Java array (the JVM's limit on `new byte[n]`): a larger result cannot be
+// returned as one byte[]; the JVM itself would throw OutOfMemoryError.
+constexpr int64_t kMaxJavaArray = 0x7FFFFFF7;
+
 static jbyteArray fetch_common(JNIEnv* env, dml_store* s, const int64_t* keys, int64_t n, bool range, int64_t f,
                                int64_t l) {
     int64_t rows = 0;
     int32_t cols = 0;
     dml_store_shape(s, &rows, &cols);
     const int64_t cap = (range ? (l - f + 1) : n) * (8 + 16 * (int64_t)cols);
-    std::vector<uint8_t> out((size_t)(cap > 0 ? cap : 1));
+    if (cap > kMaxJavaArray) {
+        env->ThrowNew(env->FindClass("java/lang/OutOfMemoryError"), "fetch result exceeds the maximum Java array size");
+        return nullptr;
+    }
+    // the library DMAs straight into the thread's pinned stage (no bounce buffer);
+    // SetByteArrayRegion is the one host copy into the Java heap
+    uint8_t* out = t_stage.get(cap > 0 ? cap : 1);
+    if (!out) {
+        throw_for(env, DML_E_NOMEM);
+        return nullptr;
+    }
     int64_t len = 0;
-    int rc = range ? dml_store_fetch_range(s, f, l, out.data(), cap, &len)
-                   : dml_store_fetch(s, keys, n, out.data(), cap, &len);
+    int rc = range ? dml_store_fetch_range(s, f, l, out, cap, &len) : dml_store_fetch(s, keys, n, out, cap, &len);
     if (rc) { throw_for(env, rc); return nullptr; }
     jbyteArray r = env->NewByteArray((jsize)len);
-    env->SetByteArrayRegion(r, 0, (jsize)len, reinterpret_cast<const jbyte*>(out.data()));
+    if (!r) return nullptr;  // OutOfMemoryError pending
+    env->SetByteArrayRegion(r, 0, (jsize)len, reinterpret_cast<const jbyte*>(out));
     return r;
 }
 
@@ -126,11 +141,17 @@ JNIEXPORT jlong JNICALL FN(nativeShardBytes)(JNIEnv*, jclass, jlong h) {
 JNIEXPORT jbyteArray JNICALL FN(nativeWriteAll)(JNIEnv* env, jclass, jlong h) {
     int64_t len = 0;
     dml_store_write_all(H(h), nullptr, 0, &len);
-    std::vector<uint8_t> out((size_t)(len > 0 ? len : 1));
-    int rc = dml_store_write_all(H(h), out.data(), len, &len);
+    if (len > kMaxJavaArray) {
+        env->ThrowNew(env->FindClass("java/lang/OutOfMemoryError"), "shard exceeds the maximum Java array size");
+        return nullptr;
+    }
+    uint8_t* out = t_stage.get(len > 0 ? len : 1);
+    if (!out) { throw_for(env, DML_E_NOMEM); return nullptr; }
+    int rc = dml_store_write_all(H(h), out, len, &len);
     if (rc) { throw_for(env, rc); return nullptr; }
     jbyteArray r = env->NewByteArray((jsize)len);
-    env->SetByteArrayRegion(r, 0, (jsize)len, reinterpret_cast<const jbyte*>(out.data()));
+    if (!r) return nullptr;
+    env->SetByteArrayRegion(r, 0, (jsize)len, reinterpret_cast<const jbyte*>(out));
     return r;
 }
 
@@ -150,10 +171,16 @@ JNIEXPORT jbyteArray JNICALL FN(nativeSyncTo)(JNIEnv* env, jclass, jlong h, jint
     // size query: the rows that exist in [from, to]
     const int64_t hi = to < rows ? to : rows - 1;
     const int64_t cap = (from >= 0 && hi >= from) ? (hi - from + 1) * (int64_t)cols * 8 : 0;
-    std::vector<uint8_t> out((size_t)(cap > 0 ? cap : 1));
-    const int rc = dml_store_sync_to(H(h), from, to, out.data(), cap, &len);
+    if (cap > kMaxJavaArray) {
+        env->ThrowNew(env->FindClass("java/lang/OutOfMemoryError"), "rows exceed the maximum Java array size");
+        return nullptr;
+    }
+    uint8_t* out = t_stage.get(cap > 0 ? cap : 1);
+    if (!out) { throw_for(env, DML_E_NOMEM); return nullptr; }
+    const int rc = dml_store_sync_to(H(h), from, to, out, cap, &len);
     jbyteArray r = env->NewByteArray((jsize)len);
-    env->SetByteArrayRegion(r, 0, (jsize)len, reinterpret_cast<const jbyte*>(out.data()));
+    if (!r) return nullptr;
+    env->SetByteArrayRegion(r, 0, (jsize)len, reinterpret_cast<const jbyte*>(out));
     if (rc) { throw_for(env, rc); return nullptr; }  // the caller writes the rows before rethrowing
     return r;
 }
@@ -190,6 +217,68 @@ JNIEXPORT void JNICALL FN(nativeFill)(JNIEnv* env, jclass, jlong h, jdouble v) {
 
 JNIEXPORT void JNICALL FN(nativeSetAlpha)(JNIEnv* env, jclass, jlong h, jfloat a, jfloat m, jfloat f) {
     if (int rc = dml_store_set_alpha(H(h), a, m, f)) throw_for(env, rc);
+}
+
+// Iter snapshot (GpuXStore.iter()): the shard's values (which 0) or
+// AdaGrad's alpha (1) / delta (2) copied into the Java heap arrays the reference's
+// Iter reads — dims 2: a T[rows][cols] (FloatMatrixStore.localData, ...), dims 1: a
+// T[rows] (DoubleArrayStore.localData, ...); elem = the DataDesc element type of the
+// array (INT 0, FLOAT 1, DOUBLE 3). Bounded chunks of rows through the thread's
+// pinned stage (dml_store_read_rows), then Set<T>ArrayRegion per row.
+JNIEXPORT void JNICALL FN(nativeSnapshot)(JNIEnv* env, jclass, jlong h, jint which, jint elem, jint dims,
+                                          jobject dst) {
+    int64_t rows = 0;
+    int32_t cols = 0;
+    if (int rc = dml_store_shape(H(h), &rows, &cols)) { throw_for(env, rc); return; }
+    const int64_t esz = elem == DML_ELEMENT_TYPE_DOUBLE ? 8 : 4;
+    const int64_t per_row = dims == 2 ? cols : 1;  // elements per local row
+    if ((dims != 1 && dims != 2) || (elem != DML_ELEMENT_TYPE_INT && elem != DML_ELEMENT_TYPE_FLOAT &&
+                                     elem != DML_ELEMENT_TYPE_DOUBLE) || !dst ||
+        env->GetArrayLength(static_cast<jarray>(dst)) != rows) {
+        env->ThrowNew(env->FindClass("java/lang/IllegalArgumentException"), "snapshot array does not match the shard");
+        return;
+    }
+    const int64_t row_bytes = per_row * esz;
+    const int64_t chunk = std::max<int64_t>(1, (int64_t)(16 << 20) / std::max<int64_t>(row_bytes, 1));
+    for (int64_t r0 = 0; r0 < rows; r0 += chunk) {
+        const int64_t n = std::min(chunk, rows - r0);
+        uint8_t* buf = t_stage.get(std::max<int64_t>(n * row_bytes, 1));
+        if (!buf) { throw_for(env, DML_E_NOMEM); return; }
+        if (int rc = dml_store_read_rows(H(h), which, r0, n, buf, n * row_bytes)) { throw_for(env, rc); return; }
+        for (int64_t i = 0; i < (dims == 2 ? n : 1); ++i) {
+            jobject a = dims == 2 ? env->GetObjectArrayElement(static_cast<jobjectArray>(dst), (jsize)(r0 + i)) : dst;
+            if (!a) {
+                if (!env->ExceptionCheck())
+                    env->ThrowNew(env->FindClass("java/lang/NullPointerException"), "snapshot row is null");
+                return;
+            }
+            const jsize at = dims == 2 ? 0 : (jsize)r0, len = (jsize)(dims == 2 ? per_row : n);
+            const uint8_t* src = buf + (dims == 2 ? i * row_bytes : 0);
+            if (dims == 2 && env->GetArrayLength(static_cast<jarray>(a)) != per_row) {
+                env->ThrowNew(env->FindClass("java/lang/IllegalArgumentException"), "snapshot row length != rowSize");
+                return;
+            }
+            if (elem == DML_ELEMENT_TYPE_FLOAT)
+                env->SetFloatArrayRegion(static_cast<jfloatArray>(a), at, len, reinterpret_cast<const jfloat*>(src));
+            else if (elem == DML_ELEMENT_TYPE_INT)
+                env->SetIntArrayRegion(static_cast<jintArray>(a), at, len, reinterpret_cast<const jint*>(src));
+            else
+                env->SetDoubleArrayRegion(static_cast<jdoubleArray>(a), at, len, reinterpret_cast<const jdouble*>(src));
+            if (dims == 2) env->DeleteLocalRef(a);
+            if (env->ExceptionCheck()) return;
+        }
+    }
+}
+
+// FloatMatrixStoreAdaGrad's maxDelta / maxDeltaRow / maxDeltaCol (:27-29, :273-277):
+// returns maxDelta, rowCol[0] = maxDeltaRow (the key, as the reference's (int)key),
+// rowCol[1] = maxDeltaCol.
+JNIEXPORT jfloat JNICALL FN(nativeMaxDelta)(JNIEnv* env, jclass, jlong h, jintArray row_col) {
+    float v = 0.f;
+    int32_t rc2[2] = {0, 0};
+    if (int rc = dml_store_max_delta(H(h), &v, &rc2[0], &rc2[1])) { throw_for(env, rc); return 0.f; }
+    env->SetIntArrayRegion(row_col, 0, 2, reinterpret_cast<const jint*>(rc2));
+    return v;
 }
 
 JNIEXPORT void JNICALL FN(nativeDestroy)(JNIEnv*, jclass, jlong h) { dml_store_destroy(H(h)); }

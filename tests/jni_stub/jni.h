@@ -20,6 +20,10 @@ typedef jobject jclass;
 typedef jobject jarray;
 typedef jobject jbyteArray;
 typedef jobject jlongArray;
+typedef jobject jobjectArray;
+typedef jobject jfloatArray;
+typedef jobject jintArray;
+typedef jobject jdoubleArray;
 typedef jobject jthrowable;
 #define JNIEXPORT __attribute__((visibility("default")))
 #define JNICALL
@@ -34,5 +38,11 @@ struct JNIEnv {
     jbyteArray NewByteArray(jsize len);
     jobject NewDirectByteBuffer(void* address, jlong capacity);
     void* GetDirectBufferAddress(jobject buf);
+    jobject GetObjectArrayElement(jobjectArray array, jsize index);
+    void SetFloatArrayRegion(jfloatArray array, jsize start, jsize len, const jfloat* buf);
+    void SetIntArrayRegion(jintArray array, jsize start, jsize len, const jint* buf);
+    void SetDoubleArrayRegion(jdoubleArray array, jsize start, jsize len, const jdouble* buf);
+    void DeleteLocalRef(jobject obj);
+    jboolean ExceptionCheck();
 };
 #endif

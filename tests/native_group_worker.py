@@ -16,6 +16,9 @@ Cases (generators shared with tests/test_gpu_group.py):
             sum) on the rank's own rows: exact only if the store applies them in order
   fault     int32 full-range calls; rank 0's second finished call fails its verdict
             (fault injection): it raises there, every rank finishes every call
+  beginfail int32 full-range calls; rank 0's call 1 hands over a ragged push, so its
+            _begin_ctx fails (no pieces, no host wait for the set's last apply): it
+            raises at once, contributes zeros, every rank finishes every call
   jni       int32 full-range calls and a pushLocal through the JNI shim's GpuShardGroup
             entry points (integration/jni/dml_jni.cc on the mock JNIEnv of tests/jni_mock)
 Writes out/<case>_<rank>.npz and prints one JSON line.
@@ -102,8 +105,8 @@ def main():
     uid = read_uid(a.uid_file, a.rank)
     world, rank = a.world, a.rank
     errors, res = [], {}
-    if a.case in ("full", "fault", "local"):
-        vt = 0 if a.case in ("fault", "local") else a.vt
+    if a.case in ("full", "fault", "local", "beginfail"):
+        vt = 0 if a.case in ("fault", "local", "beginfail") else a.vt
         rows, cols = a.rows, a.cols
         g = NativeShardGroup(DataDesc(1, 0, vt), rows, cols, rank, world, uid, device=a.device, pieces=a.pieces)
         sh = g.shard
@@ -114,8 +117,11 @@ def main():
         for call in range(calls):
             bufs = G._buckets(pyoracle, vt, rank, a.pushes, rows, cols, call)
             ptrs = [H.put(b) for b in bufs]
+            lens = [b.nbytes for b in bufs]
+            if a.case == "beginfail" and rank == 0 and call == 1:
+                lens[0] -= 1  # not whole records: DML_E_TRUNCATED from _begin_ctx
             try:
-                g.push_full_range(ptrs, [b.nbytes for b in bufs])
+                g.push_full_range(ptrs, lens)
             except Exception as e:  # the fault case: rank 0's call-1 failure, raised at call 2
                 errors.append([call, type(e).__name__, str(e)[:200]])
         if a.case == "local":

@@ -303,7 +303,7 @@ def test_moments_hip_multiprocess(tmp_path, oracle, world):
 
 
 # ---------------------------------------------------------------- local failure, torch binding
-def _fworker(rank, world, port, rows, cols, W, out_dir):
+def _fworker(rank, world, port, rows, cols, W, out_dir, mode="verify"):
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
     sys.path[:0] = [ROOT, os.path.join(ROOT, "oracle")]
     import torch
@@ -319,7 +319,7 @@ def _fworker(rank, world, port, rows, cols, W, out_dir):
 
         def verify(self, h):
             FailOnce.n += 1
-            if rank == 0 and FailOnce.n == 2:
+            if mode == "verify" and rank == 0 and FailOnce.n == 2:
                 raise RuntimeError("injected verify failure")
             return super().verify(h)
 
@@ -333,10 +333,12 @@ def _fworker(rank, world, port, rows, cols, W, out_dir):
         bufs = [torch.from_numpy(b).cuda() for b in _buckets(pyoracle, 0, rank, W, rows, cols, call)]
         keep.append(bufs)
         torch.cuda.synchronize()
+        lens = [b.numel() for b in bufs]
+        if mode == "begin" and rank == 0 and call == 1:
+            lens[0] -= 1  # a ragged push: begin_ctx fails before any piece
         try:
-            g.push_full_range([b.data_ptr() for b in bufs], [b.numel() for b in bufs],
-                              torch.cuda.current_stream().cuda_stream)
-        except RuntimeError as e:
+            g.push_full_range([b.data_ptr() for b in bufs], lens, torch.cuda.current_stream().cuda_stream)
+        except Exception:
             errors.append(call)
     g.flush()
     np.save(os.path.join(out_dir, f"shard{rank}.npy"), g.store.values())
@@ -345,16 +347,19 @@ def _fworker(rank, world, port, rows, cols, W, out_dir):
     dist.destroy_process_group()
 
 
-def test_shard_group_local_failure_keeps_collectives(tmp_path, oracle):
-    """ShardGroup (torch binding) at world 2: rank 0's verdict for call 1 fails locally
-    (ADVICE r3). Rank 0 raises once (at call 2, which finishes call 1), still enters call
-    1's reduce-scatter with a zeroed partial and skips its own apply; nobody hangs. int32,
+@pytest.mark.parametrize("mode", ["verify", "begin"])
+def test_shard_group_local_failure_keeps_collectives(tmp_path, oracle, mode):
+    """ShardGroup (torch binding) at world 2: rank 0's call 1 fails locally — its verdict
+    (raised at call 2, which finishes call 1) or its begin_ctx on a ragged
+    push (raised at call 1 itself). Rank 0 still enters call 1's
+    reduce-scatter with a zeroed partial and skips its own apply; nobody hangs. int32,
     exact: rank 1's shard lacks only rank 0's call-1 pushes, rank 0's lacks all of call 1."""
     import torch.multiprocessing as mp
     from distml_amd.datadesc import KeyRange
     world, rows, cols, W = 2, 1000, 64, 3
-    mp.spawn(_fworker, args=(world, _free_port(), rows, cols, W, str(tmp_path)), nprocs=world, join=True)
-    assert np.load(tmp_path / "err0.npy").tolist() == [2] and np.load(tmp_path / "err1.npy").tolist() == []
+    mp.spawn(_fworker, args=(world, _free_port(), rows, cols, W, str(tmp_path), mode), nprocs=world, join=True)
+    assert np.load(tmp_path / "err0.npy").tolist() == ([2] if mode == "verify" else [1])
+    assert np.load(tmp_path / "err1.npy").tolist() == []
     init = _init(0, rows, cols)
     for r, sh in enumerate(KeyRange(0, rows - 1).linearSplit(world)):
         o = oracle.OracleStore(1, 0, 0, 0, rows - 1, cols)

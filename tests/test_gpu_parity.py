@@ -1773,6 +1773,9 @@ def test_identity_speculation_exact(oracle, case, shape):
         st.pushDevice([d.data_ptr() for d in dev_all[0]], [d.numel() for d in dev_all[0]])
         st.flush()
         assert st.device_ptr() != p0
+        if cols * (8 if vt == 3 else 4) < 4096:
+            # all-identity flat chunks run the lean kernel (chosen from the index's Ctrl)
+            assert st.kernel_name().startswith("dml::k_flat_ident<"), st.kernel_name()
         for d in dev_all[0]:
             assert o.push(d.cpu().numpy().tobytes()) == 0
         assert st.values().tobytes() == o.data.tobytes()
@@ -2228,6 +2231,15 @@ def test_flat_kernel_widths_exact(oracle, vt, cols):
         for h in host[2 * c: 2 * c + 2]:
             assert o.push(h) == 0
     s.flush()
+    assert kat.bits_equal(s.values(), o.data)
+    # an all-identity call (two ascending pushes): k_flat_ident at this width, with the
+    # row count no wave's rows divide
+    idn = [dev[0], dev[2]]
+    s.pushDevice(DeviceBatch([t.data_ptr() for t in idn], [t.numel() for t in idn]))
+    for j in (0, 2):
+        assert o.push(host[j]) == 0
+    s.flush()
+    assert s.kernel_name().startswith("dml::k_flat_ident<"), s.kernel_name()
     assert kat.bits_equal(s.values(), o.data)
 
 

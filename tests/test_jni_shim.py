@@ -63,7 +63,9 @@ class MockJVM:
         for n, a, r in [("mock_byte_array", [P, I], P), ("mock_long_array", [P, I], P),
                         ("mock_array_length", [P], I), ("mock_array_data", [P], P),
                         ("mock_direct_address", [P], P), ("mock_direct_capacity", [P], J), ("mock_free", [P], None),
-                        ("mock_take_exception", [P, I, P, I], I), ("mock_calls", [], I)]:
+                        ("mock_take_exception", [P, I, P, I], I), ("mock_calls", [], I),
+                        ("mock_prim_array", [C.c_char, I], P), ("mock_object_array", [P, I], P),
+                        ("mock_object_element", [P, I], P)]:
             getattr(L, n).argtypes, getattr(L, n).restype = a, r
         self.env = L.mock_env()
         sig = {
@@ -73,6 +75,7 @@ class MockJVM:
             "nativeSyncTo": ([J, I, I], P), "nativeSyncFrom": ([J, I, I, P], None), "nativeHostAlloc": ([J], P),
             "nativeHostFree": ([P], None), "nativePushDirect": ([J, P, I, I], None), "nativeFill": ([J, D], None),
             "nativeSetAlpha": ([J, F, F, F], None), "nativeDestroy": ([J], None),
+            "nativeSnapshot": ([J, I, I, I, P], None), "nativeMaxDelta": ([J, P], F),
         }
         gsig = {
             "nativeUniqueId": ([], P), "nativeGroupCreate": ([P, I, I, I, I, I, I, I, I, I, J, I, I], J),
@@ -103,6 +106,25 @@ class MockJVM:
     def read(self, arr) -> bytes:
         n = self.L.mock_array_length(arr)
         return self.C.string_at(self.L.mock_array_data(arr), n) if n > 0 else b""
+
+    def prim(self, kind: str, n: int):
+        """A Java float[] / int[] / double[] ('F' / 'I' / 'D') of n zeros."""
+        return self.L.mock_prim_array(kind.encode(), n)
+
+    def matrix(self, kind: str, rows: int, cols: int):
+        """A Java T[rows][cols] (an Object[] of T[] rows), as `new float[rows][cols]`."""
+        elems = (self.C.c_void_p * max(rows, 1))(*[self.prim(kind, cols) for _ in range(rows)])
+        return self.L.mock_object_array(elems, rows)
+
+    def read_prim(self, arr, dtype):
+        import numpy as np
+        n = self.L.mock_array_length(arr)
+        return np.frombuffer(self.C.string_at(self.L.mock_array_data(arr), n * np.dtype(dtype).itemsize), dtype)
+
+    def read_matrix(self, arr, dtype):
+        import numpy as np
+        return np.stack([self.read_prim(self.L.mock_object_element(arr, i), dtype)
+                         for i in range(self.L.mock_array_length(arr))])
 
 
 @pytest.mark.skipif(shutil.which("g++") is None, reason="no g++")
@@ -235,3 +257,90 @@ def test_mock_jvm_store_on_gpu(oracle):
     wa, _ = jvm.call("nativeWriteAll", st)
     assert jvm.read(wa) == og.write_all()
     jvm.call("nativeGroupDestroy", g)
+
+
+@pytest.mark.gpu
+def test_mock_jvm_snapshot_on_gpu(oracle):
+    """The result-collect entry points through the shim, as the typed
+    GPU stores call them: GpuDoubleArrayStore.iter() (LogisticRegression.scala:290-291)
+    and GpuFloatMatrixStoreAdaGrad.iter() (Word2Vec.scala:814-817) fill the parent's
+    localData (and alpha / delta, which the AdaGrad Iter prints) with nativeSnapshot,
+    in bounded row chunks; the AdaGrad push reports maxDelta through nativeMaxDelta
+    (FloatMatrixStoreAdaGrad.java:246). Keys and values bit-exact against the oracle.
+    Also an IntMatrixStore snapshot (int[][]), a wrong-shape array
+    (IllegalArgumentException) and a fetch past the Java array limit (OutOfMemoryError)."""
+    import numpy as np
+    from distml_amd import encode_array_push, encode_matrix_push
+    jvm = MockJVM()
+    rng = np.random.default_rng(41)
+
+    # DoubleArrayStore shard [1000, 1999] (LR weights): sparse pushes with repeats
+    first, n = 1000, 1000
+    h, exc = jvm.call("nativeCreate", 0, 1, 3, 0, 1, 0, first, first + n - 1, 1, 0, 0)
+    assert exc is None and h
+    o = oracle.OracleStore(0, 1, 3, first, first + n - 1)
+    for b in range(5):
+        keys = rng.integers(first, first + n, size=700)
+        p = encode_array_push(keys, rng.standard_normal(700), 1, 3)
+        _, exc = jvm.call("nativePush", h, jvm.bytes_(p))
+        assert exc is None and o.push(p) == 0
+    arr = jvm.prim("D", n)  # DoubleArrayStore.localData = new double[rows]
+    _, exc = jvm.call("nativeSnapshot", h, 0, 3, 1, arr)
+    assert exc is None
+    got = jvm.read_prim(arr, np.float64)
+    assert got.tobytes() == o.data.reshape(-1).tobytes()
+    # the Iter's (key, value) pairs: key = firstKey + p (keyOf), value = localData[p]
+    pairs = [(first + i, float(v)) for i, v in enumerate(got)]
+    assert pairs[0][0] == first and pairs[-1][0] == first + n - 1
+    bad = jvm.prim("D", n - 1)
+    _, exc = jvm.call("nativeSnapshot", h, 0, 3, 1, bad)
+    assert exc and exc[0] == "java/lang/IllegalArgumentException"
+    jvm.call("nativeDestroy", h)
+
+    # FloatMatrixStoreAdaGrad shard (Word2Vec syn0): rows 0..2999 x 100, two pushes
+    rows, cols = 3000, 100
+    h, exc = jvm.call("nativeCreate", 1, 0, 1, 0, 1, 1, 0, rows - 1, cols, 0, 0)
+    assert exc is None and h
+    o = oracle.OracleStore(1, 0, 1, 0, rows - 1, cols, 1, 1)
+    _, exc = jvm.call("nativeSetAlpha", h, 0.025, 0.0001, 1.5)
+    o.set_alpha(0.025, 0.0001, 1.5)
+    for b in range(2):
+        keys = rng.permutation(rows)[:2500]
+        p = encode_matrix_push(keys, rng.standard_normal((2500, cols)).astype(np.float32), 0, 1)
+        _, exc = jvm.call("nativePush", h, jvm.bytes_(p))
+        assert exc is None and o.push(p) == 0
+        rc = jvm.prim("I", 2)
+        v, exc = jvm.call("nativeMaxDelta", h, rc)
+        assert exc is None
+        assert (np.float32(v), *jvm.read_prim(rc, np.int32).tolist()) == tuple(o.max_delta())
+    for which, want in ((0, o.data), (1, o.alpha), (2, o.delta)):
+        m = jvm.matrix("F", rows, cols)  # new float[rows][rowSize]
+        _, exc = jvm.call("nativeSnapshot", h, which, 1, 2, m)
+        assert exc is None, exc
+        assert jvm.read_matrix(m, np.float32).tobytes() == np.ascontiguousarray(want).tobytes(), which
+        jvm.L.mock_free(m)
+    jvm.call("nativeDestroy", h)
+
+    # IntMatrixStore: int[][], and rows large enough to take several 16 MiB chunks
+    rows, cols = 40000, 256
+    h, exc = jvm.call("nativeCreate", 1, 0, 0, 0, 1, 0, 0, rows - 1, cols, 0, 0)
+    assert exc is None
+    o = oracle.OracleStore(1, 0, 0, 0, rows - 1, cols)
+    p = encode_matrix_push(rng.permutation(rows), rng.integers(0, 5, size=(rows, cols)).astype(np.int32), 0, 0)
+    _, exc = jvm.call("nativePush", h, jvm.bytes_(p))
+    assert exc is None and o.push(p) == 0
+    m = jvm.matrix("I", rows, cols)
+    _, exc = jvm.call("nativeSnapshot", h, 0, 0, 2, m)
+    assert exc is None
+    assert jvm.read_matrix(m, np.int32).tobytes() == o.data.tobytes()
+    jvm.L.mock_free(m)
+    # a fetch whose byte[] would pass the JVM's array limit: OutOfMemoryError, as `new byte[n]`
+    _, exc = jvm.call("nativeFetchRange", h, 0, rows - 1)
+    assert exc is None
+    jvm.call("nativeDestroy", h)
+    rows, cols = 3_000_000, 180  # 3 M x (8 + 16 x 180) B > 2^31
+    h, exc = jvm.call("nativeCreate", 1, 0, 0, 0, 1, 0, 0, rows - 1, cols, 0, 0)
+    assert exc is None
+    _, exc = jvm.call("nativeFetchRange", h, 0, rows - 1)
+    assert exc and exc[0] == "java/lang/OutOfMemoryError"
+    jvm.call("nativeDestroy", h)

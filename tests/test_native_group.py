@@ -33,7 +33,13 @@ DOUBLE = os.path.join(ROOT, "tests", "rccl_double", "librccl_double.so")
 pytestmark = pytest.mark.gpu
 
 
-def run_ranks(tmp_path, world, case, double=True, **kw):
+# Every collective of the stand-in runs this long after its inputs are ready (helper
+# thread, asynchronous to the caller's streams): a stream dependency the library
+# forgets shows up as wrong sums.
+DELAY_US = 20000
+
+
+def run_ranks(tmp_path, world, case, double=True, delay_us=DELAY_US, **kw):
     """Start `world` workers, wait for all, return their JSON lines (rank order)."""
     uid = tmp_path / f"uid_{case}"
     if double:
@@ -43,12 +49,13 @@ def run_ranks(tmp_path, world, case, double=True, **kw):
         name = ("dml-rccl-double:/dmlrccl_" + os.urandom(12).hex()).encode()
         uid.write_bytes(name + b"\0" * (128 - len(name)))
     args = [f"--{k.replace('_', '-')}={v}" for k, v in kw.items()]
+    env = dict(os.environ, DML_RCCL_DOUBLE_DELAY_US=str(delay_us))
     procs = []
     for r in range(world):
         cmd = [sys.executable, "-u", WORKER, f"--world={world}", f"--rank={r}", f"--uid-file={uid}",
                f"--case={case}", f"--out={tmp_path}", f"--device={0 if double else r}"] + args
         procs.append(subprocess.Popen(cmd + (["--double"] if double else []), stdout=subprocess.PIPE,
-                                      stderr=subprocess.PIPE, text=True))
+                                      stderr=subprocess.PIPE, text=True, env=env))
     outs = []
     try:
         for p in procs:
@@ -157,6 +164,25 @@ def test_native_group_local_failure_keeps_collectives(tmp_path, oracle):
     on, _, _ = full_expected(oracle, 0, world, rows, cols, W, G.CALLS, skip=lambda r, c: (r, c) == (0, 1))
     for r, sh in enumerate(parts):
         got = np.load(tmp_path / f"fault_{r}.npz")["data"].reshape(-1, cols)
+        want = (o0 if r == 0 else on).data[sh.firstKey:sh.lastKey + 1]
+        assert np.array_equal(got, want), r
+
+
+def test_native_group_begin_failure_keeps_collectives(tmp_path, oracle):
+    """A call that fails in dml_prereduce_begin_ctx (rank 0's call 1: a ragged push) at
+    world 3: it skipped the host wait for its buffer set's last apply, so
+    its zero contribution orders after that apply on the device, and the set stays
+    busy until the zero-contribution scatter has run: call 3 reuses it while the
+    stand-in still delays call 1's scatter. Rank 0 raises at call 1; every shard exact."""
+    world, rows, cols, W = 3, 1000, 64, 4
+    outs = run_ranks(tmp_path, world, "beginfail", rows=rows, cols=cols, pushes=W)
+    assert [len(d["errors"]) for d in outs] == [1, 0, 0], outs
+    assert outs[0]["errors"][0][0] == 1 and outs[0]["errors"][0][1] == "ArrayIndexOutOfBoundsException", outs[0]
+    from distml_amd.datadesc import KeyRange
+    o0, _, _ = full_expected(oracle, 0, world, rows, cols, W, G.CALLS, skip=lambda r, c: c == 1)
+    on, _, _ = full_expected(oracle, 0, world, rows, cols, W, G.CALLS, skip=lambda r, c: (r, c) == (0, 1))
+    for r, sh in enumerate(KeyRange(0, rows - 1).linearSplit(world)):
+        got = np.load(tmp_path / f"beginfail_{r}.npz")["data"].reshape(-1, cols)
         want = (o0 if r == 0 else on).data[sh.firstKey:sh.lastKey + 1]
         assert np.array_equal(got, want), r
 

@@ -154,8 +154,11 @@ def test_java_parse_float():
     # where a detour through double (which holds the tie exactly) would round down
     up = float(np.nextafter(np.float32(1), np.float32(2)))
     assert pf("1.000000059604644775390625") == 1.0 and pf("1.000000059604644775390626") == up
-    with pytest.raises(ValueError):
-        pf("abc")
+    assert pf(".5") == 0.5 and pf("1.") == 1.0 and pf("+1e2") == 100.0 and pf("1.e1") == 10.0
+    # Float.parseFloat throws NumberFormatException on these (Fraction would take the first two)
+    for bad in ("abc", "1/2", "1_0", "1e", "--1", ".", "1..2", ""):
+        with pytest.raises(ValueError):
+            pf(bad)
 
 
 def test_row_subset_generators_match_full(oracle):
