@@ -261,13 +261,18 @@ def _sparse_perm(b, dim):
 
 
 # ---------------------------------------------------------------- config 2
-SLAB = [False]  # --one-slab (diagnostic)
+# A PS receives a call's pushes into one device receive slab, sliced per push
+# (INTEGRATION.md): over separately allocated buffers the reduce's DRAM efficiency
+# depends on where the allocator put them (same bytes, 333-348 us per launch,
+# scripts/probe_placement.py), over slices of one slab it is the same in every order.
+# --separate-buffers restores one allocation per push (diagnostic).
+SLAB = [True]
 
 
 def make_buckets(L, torch, fmt, n, rows_total, value_seed: int = 1000, alloc_seed: int = 0):
     st = torch.cuda.current_stream().cuda_stream
     bufs = []
-    if SLAB[0]:  # diagnostic: the n buckets as slices of one allocation
+    if SLAB[0]:  # the n buckets as slices of one allocation (the receive slab)
         slab = torch.empty(n * rows_total * REC, dtype=torch.uint8, device="cuda")
         mem = [slab[i * rows_total * REC:(i + 1) * rows_total * REC] for i in range(n)]
     else:
@@ -427,7 +432,7 @@ def headline(ctx: Ctx, L, args, out_line: dict):
         algo_per_rank = W * BUCKET + 2 * SHARD
     else:
         group = ShardGroup(fmt, ROWS, COLS, rank, world, device=ctx.local, pieces=args.pieces,
-                           emulate_world=args.emulate_rs)
+                           emulate_world=args.emulate_rs, emulate_channels=args.emulate_channels)
         if args.index_normal_prio:  # diagnostic: the next call's index chain at normal priority
             group.istream = torch.cuda.Stream(device=torch.device("cuda", ctx.local))
         bufs = make_buckets(L, torch, fmt, W, ROWS) + make_buckets(L, torch, fmt, W, ROWS, value_seed=5000)
@@ -512,10 +517,13 @@ def headline(ctx: Ctx, L, args, out_line: dict):
                                "([int32 key][1024 x f32] x 16384) -> 16384x1024 fp32 model per GPU",
                    "pushes_per_gpu": W, "push_bytes": BUCKET, "model_rows": ROWS, "cols": COLS,
                    "parallelism": ("single shard" if not sharded else f"linearSplit({world}) + RCCL reduce-scatter"
-                                   + (f" (DIAGNOSTIC: owner-side footprint of {args.emulate_rs} ranks emulated, "
+                                   + (f" (DIAGNOSTIC: one rank's ring reduce-scatter footprint at {args.emulate_rs} "
+                                      f"ranks emulated on {args.emulate_channels} blocks, pieces {args.pieces}, "
                                       "results not valid)" if args.emulate_rs else "")),
                    "pushes": "16 ascending + 16 permuted per step; two bucket sets stepped alternately "
-                             "(same key order per push position, different values)",
+                             "(same key order per push position, different values)"
+                             + ("; each set's 32 pushes in one device receive slab" if SLAB[0]
+                                else "; one allocation per push"),
                    "algorithmic_bytes_per_step_per_gpu": algo_per_rank},
     })
     if not sharded and k_n > 0:
@@ -1215,11 +1223,14 @@ def main():
     ap.add_argument("--shuffle-keep-parity", action="store_true", help=argparse.SUPPRESS)
     ap.add_argument("--shuffle-orders", type=int, default=0, help=argparse.SUPPRESS)
     ap.add_argument("--alloc-seed", type=int, default=0, help=argparse.SUPPRESS)
-    ap.add_argument("--one-slab", action="store_true", help=argparse.SUPPRESS)
+    ap.add_argument("--separate-buffers", action="store_true",
+                    help="config 2: one allocation per push instead of slices of one receive slab (diagnostic)")
     ap.add_argument("--shuffle-only", choices=["", "asc", "perm"], default="", help=argparse.SUPPRESS)
     ap.add_argument("--emulate-rs", type=int, default=0,
                     help="diagnostic with --group at N = 1: the owner-side HBM footprint of an N-rank "
-                         "reduce-scatter + 1/N apply (results not valid)")
+                         "ring reduce-scatter + 1/N apply (results not valid)")
+    ap.add_argument("--emulate-channels", type=int, default=32,
+                    help="--emulate-rs: blocks of the ring reduce-scatter footprint (RCCL: one per channel)")
     ap.add_argument("--index-normal-prio", action="store_true", help=argparse.SUPPRESS)
     ap.add_argument("--native-group", action="store_true",
                     help="also run the config-2 workload through dml_group at N = 1 (always at N > 1)")
@@ -1246,7 +1257,7 @@ def main():
     # (RCCL refuses two ranks on one device); numbers from it are not measurements
     ap.add_argument("--rehearse-gloo", action="store_true", help=argparse.SUPPRESS)
     args = ap.parse_args()
-    SLAB[0] = args.one_slab
+    SLAB[0] = not args.separate_buffers
     if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
         sys.exit(launch_ranks(args.gpus, sys.argv[1:]))
     # stdout carries exactly the one JSON line: RCCL and other native libraries print

@@ -309,6 +309,9 @@ hipError_t launch_flat_ident(int vtype, int mode, void* shard, int64_t rows, int
 // Ctrl after the index (hctrl) and the pushes' record counts (`need` per push: the
 // model rows).
 bool flat_ident_ok(const Ctrl& hctrl, const Batch& bt, int nb, int64_t need, uint64_t tail_cut);
+// One rank's ring reduce-scatter footprint (diagnostic): one kernel of `channels` blocks.
+hipError_t launch_ring_rs(int vtype, const void* part, void* recv, void* land, int64_t chunk_bytes, int world,
+                          int rank, int channels, hipStream_t st);
 // Task rows per wave of k_flat_ident at this width (a row map's blocks must hold whole waves).
 int flat_ident_rows_per_wave(int vtype, int32_t cols);
 // row shapes whose reduce runs identity-speculative chunks (k_reduce_rows FULL, k_reduce_flat)

@@ -2167,6 +2167,63 @@ __global__ __launch_bounds__(256) void k_stream(uint8_t* __restrict__ dst, const
         if (fold == 0x9E3779B9u) *(uint32_t*)dst = fold;
 }
 
+// Ring reduce-scatter footprint (diagnostic, bench.py --emulate-rs): the local HBM
+// traffic of one rank's ring reduce-scatter, as ONE kernel of `channels` blocks
+// (RCCL runs one persistent block per channel). world - 1 steps: step s reads the
+// chunk the rank sends, (rank - s - 1) mod world, plus the chunk that arrived at
+// step s - 1, and writes their sum where the next rank's write would land (a local
+// stand-in for the peer's write into this rank's buffer); the last step adds the
+// rank's own chunk into recv. A thread owns the same vectors in every step, so the
+// steps need no synchronization. Values are meaningless (no peer contributes).
+template <typename T>
+__global__ __launch_bounds__(256) void k_ring_rs(const T* __restrict__ part, T* __restrict__ recv,
+                                                 T* __restrict__ land, int64_t chunk16, int world, int rank) {
+    constexpr int VEC = Elem<T>::VEC, U = 8;  // 8 vectors per thread per step in flight, as RCCL's unrolled copies
+    const uint8_t* P = (const uint8_t*)part;
+    uint8_t* Lb[2] = {(uint8_t*)land, (uint8_t*)land + chunk16 * 16};
+    const int64_t nthr = (int64_t)gridDim.x * blockDim.x;
+    for (int64_t i0 = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i0 < chunk16; i0 += nthr * U) {
+        for (int s2 = 0; s2 < world; ++s2) {
+            const int64_t c = s2 == world - 1 ? rank : ((rank - s2 - 1) % world + world) % world;
+            u32x4 xa[U], ya[U];
+#pragma unroll
+            for (int u = 0; u < U; ++u) {
+                const int64_t i = i0 + u * nthr;
+                xa[u] = i < chunk16 ? ldg16_nt(P + (c * chunk16 + i) * 16) : u32x4{0u, 0u, 0u, 0u};
+                ya[u] = (s2 > 0 && i < chunk16) ? ldg16_nt(Lb[s2 & 1] + i * 16) : u32x4{0u, 0u, 0u, 0u};
+            }
+#pragma unroll
+            for (int u = 0; u < U; ++u) {
+                const int64_t i = i0 + u * nthr;
+                if (i >= chunk16) continue;
+                T x[VEC], y[VEC];
+                unpack<T>(xa[u], x);
+                unpack<T>(ya[u], y);
+#pragma unroll
+                for (int e = 0; e < VEC; ++e) x[e] = Elem<T>::add(x[e], y[e]);
+                stg16_nt((s2 == world - 1 ? (uint8_t*)recv : Lb[(s2 + 1) & 1]) + i * 16, pack<T>(x));
+            }
+        }
+    }
+}
+
+hipError_t launch_ring_rs(int vtype, const void* part, void* recv, void* land, int64_t chunk_bytes, int world,
+                          int rank, int channels, hipStream_t st) {
+    const int64_t n16 = chunk_bytes / 16;
+    if (n16 <= 0) return hipSuccess;
+    const dim3 g((unsigned)std::max(1, channels)), blk(256);
+    if (vtype == kF64)
+        hipLaunchKernelGGL(k_ring_rs<double>, g, blk, 0, st, (const double*)part, (double*)recv, (double*)land, n16,
+                           world, rank);
+    else if (vtype == kI32)
+        hipLaunchKernelGGL(k_ring_rs<int32_t>, g, blk, 0, st, (const int32_t*)part, (int32_t*)recv, (int32_t*)land,
+                           n16, world, rank);
+    else
+        hipLaunchKernelGGL(k_ring_rs<float>, g, blk, 0, st, (const float*)part, (float*)recv, (float*)land, n16,
+                           world, rank);
+    return hipGetLastError();
+}
+
 // Random-RMW floor (diagnostic): one plain 4-B read-modify-write per update over a
 // globally sorted index list — the best case of config 3's scatter-add (every update
 // in address order, no partition), against which the leaf kernel is judged.

@@ -2419,6 +2419,16 @@ int dml_diag_stream(int32_t copy, void* dev_dst, const void* dev_src, int64_t by
     return DML_OK;
 }
 
+int dml_diag_ring_rs(int32_t value_type, const void* dev_partial, void* dev_recv, void* dev_landing,
+                     int64_t chunk_bytes, int32_t world, int32_t rank, int32_t channels, void* stream) {
+    if (!dev_partial || !dev_recv || !dev_landing || chunk_bytes < 0 || chunk_bytes % 16 || world < 1 || rank < 0 ||
+        rank >= world || channels < 1)
+        return set_err(DML_E_INVALID_ARG, "bad ring reduce-scatter arguments");
+    HIPCHK(launch_ring_rs(value_type, dev_partial, dev_recv, dev_landing, chunk_bytes, world, rank, channels,
+                          (hipStream_t)stream));
+    return DML_OK;
+}
+
 int dml_diag_rmw_floor(float* dev_array, const uint32_t* dev_index, const float* dev_values, int64_t n, void* stream,
                        float* ms) {
     if (!dev_array || n < 0 || (n > 0 && (!dev_index || !dev_values)))

@@ -125,7 +125,8 @@ class HipOps:
 class ShardGroup:
     def __init__(self, fmt: DataDesc, total_rows: int, cols: int, rank: int, world: int,
                  device: Optional[int] = None, ops=None, store_factory=None, pieces: int = 1,
-                 reduce_scatter=None, exchange_only: bool = False, emulate_world: int = 0):
+                 reduce_scatter=None, exchange_only: bool = False, emulate_world: int = 0,
+                 emulate_channels: int = 32):
         import torch
         import torch.distributed as dist
         self.torch, self.dist = torch, dist
@@ -156,13 +157,17 @@ class ShardGroup:
         # 0.441 ms/step against 0.460 for P = 4 and 0.461 for P = 2)
         self.pieces = pieces
         # diagnostic (bench.py --emulate-rs, world 1 only): replace the local shortcut by
-        # the HBM footprint an N-rank call has at its owner — a reduction on the comm
-        # stream that reads the whole partial and writes 1/N of it, then the apply of
-        # 1/N of the shard. The shard's values are then NOT the reduce's result.
-        # emulate_world -1: neither the reduction nor the apply (the pieces alone)
-        if emulate_world and (world != 1 or pieces != 1 or (emulate_world > 1 and self.shard.size() % emulate_world)):
-            raise ValueError("emulate_world needs world 1, pieces 1 and rows divisible by it")
+        # the HBM footprint an N-rank call has at its owner — a RING reduce-scatter of
+        # every piece on the comm stream (N - 1 steps, each reading one 1/N chunk of the
+        # partial and the chunk that arrived and writing their sum where the next rank's
+        # write would land; dml_diag_ring_rs, on `emulate_channels` blocks as RCCL runs one
+        # block per channel), then the apply of 1/N of the shard. The shard's values are
+        # then NOT the reduce's result. emulate_world -1: neither (the pieces alone)
+        if emulate_world and (world != 1 or (emulate_world > 1 and (self.shard.size() // pieces) % emulate_world)):
+            raise ValueError("emulate_world needs world 1 and piece rows divisible by it")
         self.emulate_world = emulate_world
+        self.emulate_channels = emulate_channels
+        self._landing = None
         self._pending: list = []  # (pre-reduce handle, buffer set) not yet reduce-scattered / checked
         self._pctx = None         # speculative pre-reduce context (dml_prectx), created on first use
         self._xbufs: list = []    # exchange buffers the store may still read: (event, recv, send, push seq)
@@ -336,10 +341,17 @@ class ShardGroup:
                 return
             if self.emulate_world > 1:
                 E = self.emulate_world
-                n = partial.numel() // E
+                nper = blk * cols // E  # one emulated rank's chunk of a piece
+                n = P * nper            # its rows of the whole call
                 recv = self._recvs[k]
-                with torch.cuda.stream(self.comm):
-                    torch.sum(partial.view(E, n), dim=0, out=recv[:n])
+                if self._landing is None:
+                    self._landing = torch.empty(2 * nper, dtype=partial.dtype, device=partial.device)
+                esz = partial.element_size()
+                for j in range(P):
+                    check(_lib.load().dml_diag_ring_rs(
+                        self.fmt.valueType, C.c_void_p(partial.data_ptr() + j * blk * cols * esz),
+                        C.c_void_p(recv.data_ptr() + j * nper * esz), C.c_void_p(self._landing.data_ptr()),
+                        nper * esz, E, 0, self.emulate_channels, C.c_void_p(self.comm.cuda_stream)))
                 self._rs_done[k].record(self.comm)
                 if not hasattr(self, "_emu_rows"):
                     self._emu_rows = torch.zeros(n, dtype=partial.dtype, device=partial.device)

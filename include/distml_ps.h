@@ -432,6 +432,16 @@ int dml_diag_stream(int32_t copy, void* dev_dst, const void* dev_src, int64_t by
 int dml_diag_rmw_floor(float* dev_array, const uint32_t* dev_index, const float* dev_values, int64_t n, void* stream,
                        float* ms);
 
+/* Ring reduce-scatter footprint (diagnostic, bench.py --emulate-rs N): the local HBM
+ * traffic one rank's ring reduce-scatter of a world x chunk_bytes partial makes —
+ * world - 1 steps, each reading one chunk of the partial and the chunk that arrived
+ * (dev_landing, 2 x chunk_bytes) and landing their sum in a buffer (the write a peer
+ * makes into this rank's), then the last sum into dev_recv — on a grid of `channels`
+ * blocks (RCCL's one block per channel), enqueued on `stream`. Values are not a
+ * reduce-scatter's (no peer contributes): timing only. */
+int dml_diag_ring_rs(int32_t value_type, const void* dev_partial, void* dev_recv, void* dev_landing,
+                     int64_t chunk_bytes, int32_t world, int32_t rank, int32_t channels, void* stream);
+
 /* --- misc --------------------------------------------------------------- */
 const char* dml_last_error(void);   /* thread-local message for the last failure */
 const char* dml_version(void);

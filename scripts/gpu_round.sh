@@ -1,6 +1,6 @@
 # Round evidence, in two GPU calls (each under gpurun's 20-minute limit):
 #   PART=a: the -m gpu suite, smoke, the default bench line, the sharded path at world 1
-#           (torch binding: plain, emulated 4- and 8-rank owner footprint; native binding)
+#           (torch binding: plain, emulated 4- and 8-rank ring footprint on 64 blocks; native binding)
 #   PART=b: the line profile (kernel stats + separate FETCH_SIZE / WRITE_SIZE passes,
 #           scripts/gpu_prof.sh), the N = 2 legs rehearsed on one GPU (gloo), e2e rates
 set -e
@@ -11,7 +11,7 @@ tail -1 gpurun_out/gpu_tests.log
 timeout -k 10 120 python -c "import __graft_entry__ as g; g.smoke()"
 timeout -k 10 300 python bench.py --steps 20 --warmup 5 > gpurun_out/bench.json 2> gpurun_out/bench.err
 for E in 0 4 8; do
-timeout -k 10 200 python bench.py --group --emulate-rs $E --no-cpu --sparse-steps 0 --legs "" --steps 300 --warmup 50 > gpurun_out/bench_group_e$E.json 2> gpurun_out/bench_group_e$E.err
+timeout -k 10 200 python bench.py --group --emulate-rs $E --emulate-channels 64 --no-cpu --sparse-steps 0 --legs "" --steps 300 --warmup 50 > gpurun_out/bench_group_e$E.json 2> gpurun_out/bench_group_e$E.err
 done
 timeout -k 10 200 python bench.py --native-group --no-cpu --sparse-steps 0 --legs "" --steps 300 --warmup 50 > gpurun_out/bench_native.json 2> gpurun_out/bench_native.err
 python3 - <<'PY'
