@@ -709,7 +709,9 @@ def sparse_leg(ctx: Ctx, L, steps: int, cpu: bool):
         bufs.append(t)
     torch.cuda.synchronize()
     batch = DeviceBatch([b.data_ptr() for b in bufs], [b.numel() for b in bufs])
-    store.set_timing(True, every=2)  # start events on every other leaf launch
+    # start events on every leaf launch (a ~1.2 ms kernel: the events' boundary cost is
+    # under 1 %), so the roofline averages the same launches rocprof's kernel trace does
+    store.set_timing(True, every=1)
 
     def step():
         store.pushDevice(batch)

