@@ -25,6 +25,20 @@
 
 namespace dml {
 
+// A/B switches (scripts/build_ab.sh): k_ada_flat's block barrier before its write-back,
+// and its block size in waves. Measured off / 4 (config-4 AdaGrad leg, one box, 2
+// rounds: 9158-9217 us without the barrier, 9270-9288 with it at 4 waves, 10.3-10.9 ms
+// at 8 and 12 waves, where fewer blocks fit a CU): the waves of an AdaGrad block end
+// unevenly, and waiting for the slowest costs more than the write burst saves.
+#ifdef DML_AB_ADA_BURST
+constexpr bool kAdaBurst = true;
+#else
+constexpr bool kAdaBurst = false;
+#endif
+#ifndef DML_AB_ADA_NW
+#define DML_AB_ADA_NW 4
+#endif
+
 __host__ __device__ inline uint64_t splitmix64_dev(uint64_t x) {
     uint64_t z = x + 0x9E3779B97F4A7C15ull;
     z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
@@ -1280,27 +1294,37 @@ __global__ __launch_bounds__(NW * 64) void k_flat_ident(T* __restrict__ shard, i
 // candidate, with the push that made it; the position is rebuilt from the slot
 // rows in LDS at the end). Same per-element arithmetic and order as k_reduce, so
 // the results (data, alpha, delta, maxDelta/row/col) are the same bit for bit.
-template <int JMAX, int PB>
-__global__ __launch_bounds__(256) void k_ada_flat(float* __restrict__ shard, int64_t rows, int32_t cols, int32_t R,
+template <int JMAX, int PB, int NW>
+__global__ __launch_bounds__(NW * 64) void k_ada_flat(float* __restrict__ shard, int64_t rows, int32_t cols, int32_t R,
                                                   const Batch bt, int nb, int64_t stride, int K,
                                                   int32_t* __restrict__ slot, const uint32_t* __restrict__ rowflag,
                                                   Ctrl* __restrict__ ctrl, uint64_t tail_cut, AdaArgs ada) {
     constexpr int VEC = 4;
     constexpr int RMAX = 16;
-    __shared__ int32_t s_slot[4][RMAX * kMaxW];  // per wave: [row][push], -1 = no record / skipped row
+    __shared__ int32_t s_slot[NW][RMAX * kMaxW];  // per wave: [row][push], -1 = no record / skipped row
     const int lane = threadIdx.x & 63;
     const int wid = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     // XCD-contiguous blocks (xcd_block): config-4 AdaGrad leg 0.590 -> 0.643 of 8 TB/s
     // (2 rounds, same box): the data / delta lines two waves share meet in one L2
-    const int64_t t0 = (xcd_block() * 4 + wid) * R;  // first row of the wave
+    const int64_t t0 = (xcd_block() * NW + wid) * R;  // first row of the wave
     float cand_v = 0.f;
     uint64_t cand_p = kNoPos;
     bool cand_ok = false;
-    if (t0 < rows && !(bt.prev && ctrl_abnormal(bt.prev))) do {
+    // every wave reaches the block barrier before the write-back (a wave past the last
+    // row, or behind a predecessor that needs the host first, does no work)
+    const bool live = t0 < rows && !(bt.prev && ctrl_abnormal(bt.prev));
+    int32_t* const ls = s_slot[wid];
+    bool all_id = false;
+    // record of push b for the row of this lane's vector j
+    auto rec_of = [&](int rl, int b) -> int32_t { return all_id ? (int32_t)(t0 + rl) : ls[rl * kMaxW + b]; };
+    int rc[JMAX];  // (row << 16 | vector within the row)
+    uint32_t on = 0, tch = 0;
+    float acc[JMAX][VEC], dl[JMAX][VEC], lg[JMAX][VEC], rv[JMAX][VEC];
+    int rb[JMAX][VEC];  // chunk push index of the element's last strict rise (-1: none)
+    if (live) do {
         const int NV = cols / VEC;
         const int nrow = (int)(rows - t0 < (int64_t)R ? rows - t0 : (int64_t)R);
         const int ss = slot_stride(nb);
-        int32_t* const ls = s_slot[wid];
         // identity pushes checked record by record before the launch (Batch::ident_ok)
         const uint64_t ident = bt.ident_ok ? ctrl->ident : 0ull;
         const uint64_t nbm = nb >= 64 ? ~0ull : (1ull << nb) - 1ull;
@@ -1308,7 +1332,7 @@ __global__ __launch_bounds__(256) void k_ada_flat(float* __restrict__ shard, int
         // ran for none of them, so no row is flagged and record r holds row r. No slot
         // rows, no flag reads: the data, delta and record loads issue at once instead
         // of behind two dependent DRAM round trips.
-        const bool all_id = (ident & nbm) == nbm;  // wave-uniform
+        all_id = (ident & nbm) == nbm;  // wave-uniform
         uint32_t flg = 0;                          // bit rl: row t0 + rl is flagged (the host replays it)
         if (!all_id) {
             // the rows' flags, one load per row, and the wave's slot rows into LDS,
@@ -1332,13 +1356,6 @@ __global__ __launch_bounds__(256) void k_ada_flat(float* __restrict__ shard, int
             __builtin_amdgcn_wave_barrier();
             __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
         }
-        // record of push b for the row of this lane's vector j
-        auto rec_of = [&](int rl, int b) -> int32_t { return all_id ? (int32_t)(t0 + rl) : ls[rl * kMaxW + b]; };
-
-        int rc[JMAX];  // (row << 16 | vector within the row)
-        uint32_t on = 0, tch = 0;
-        float acc[JMAX][VEC], dl[JMAX][VEC], lg[JMAX][VEC], rv[JMAX][VEC];
-        int rb[JMAX][VEC];  // chunk push index of the element's last strict rise (-1: none)
         const int nvec = nrow * NV;
 #pragma unroll
         for (int j = 0; j < JMAX; ++j) {
@@ -1429,6 +1446,11 @@ __global__ __launch_bounds__(256) void k_ada_flat(float* __restrict__ shard, int
                     }
             }
         }
+    } while (0);
+    // (A/B, off: kAdaBurst) every wave of the block has read and updated its rows before
+    // the block's writes (data, delta, alpha: a third of the kernel's bytes) leave the CU
+    if (kAdaBurst) __syncthreads();
+    if (live) {
         // write-back of the touched vectors: data, delta, alpha where the last delta
         // a push left above 1 sets it (FloatMatrixStoreAdaGrad.java:268-272), and
         // this lane's maxDelta candidate
@@ -1468,8 +1490,8 @@ __global__ __launch_bounds__(256) void k_ada_flat(float* __restrict__ shard, int
                 }
             }
         }
-    } while (0);
-    cand_block_best<4>(cand_ok, cand_v, cand_p);
+    }
+    cand_block_best<NW>(cand_ok, cand_v, cand_p);
     if (threadIdx.x == 0) {
         DeltaCand c;
         c.value = cand_v;
@@ -1714,26 +1736,26 @@ bool spec_shape(int vtype, int32_t cols) {
     return bytes % 4096 == 0 || (cols % VEC == 0 && bytes < 4096);
 }
 
-// k_ada_flat launch: R rows per wave (R = 5 at 200 columns).
-template <int JMAX, int PB>
+// k_ada_flat launch: R rows per wave (R = 5 at 200 columns), NW waves per block.
+template <int JMAX, int PB, int NW>
 static hipError_t launch_ada_flat_t(void* shard, int64_t rows, int32_t cols, const Batch& bt, int nb, int64_t stride,
                                     int K, const int32_t* slot, const uint32_t* rowflag, Ctrl* ctrl,
                                     uint64_t tail_cut, const AdaArgs& ada, hipStream_t st, int64_t* nblocks_out,
                                     LaunchEv ev) {
     const int NV = cols / 4;
     const int R = std::max(1, std::min(16, JMAX * 64 / NV));
-    const int64_t nblocks = ((rows + R - 1) / R + 3) / 4;
+    const int64_t nblocks = ((rows + R - 1) / R + NW - 1) / NW;
     if (nblocks_out) *nblocks_out = nblocks;
     if (nblocks <= 0) return hipSuccess;
-    static const std::string kn = kname("k_ada_flat", JMAX, PB);
+    static const std::string kn = kname("k_ada_flat", JMAX, PB, NW);
     g_kernel_name = kn.c_str();
     if (ev.start || ev.stop)
-        hipExtLaunchKernelGGL((k_ada_flat<JMAX, PB>), dim3((unsigned)nblocks), dim3(256), 0, st, ev.start, ev.stop, 0,
-                              (float*)shard, rows, cols, R, bt, nb, stride, K, const_cast<int32_t*>(slot), rowflag,
-                              ctrl, tail_cut, ada);
+        hipExtLaunchKernelGGL((k_ada_flat<JMAX, PB, NW>), dim3((unsigned)nblocks), dim3(NW * 64), 0, st, ev.start,
+                              ev.stop, 0, (float*)shard, rows, cols, R, bt, nb, stride, K, const_cast<int32_t*>(slot),
+                              rowflag, ctrl, tail_cut, ada);
     else
-        hipLaunchKernelGGL((k_ada_flat<JMAX, PB>), dim3((unsigned)nblocks), dim3(256), 0, st, (float*)shard, rows, cols, R,
-                           bt, nb, stride, K, const_cast<int32_t*>(slot), rowflag, ctrl, tail_cut, ada);
+        hipLaunchKernelGGL((k_ada_flat<JMAX, PB, NW>), dim3((unsigned)nblocks), dim3(NW * 64), 0, st, (float*)shard,
+                           rows, cols, R, bt, nb, stride, K, const_cast<int32_t*>(slot), rowflag, ctrl, tail_cut, ada);
     return hipGetLastError();
 }
 
@@ -1744,8 +1766,8 @@ static hipError_t launch_ada_flat_t(void* shard, int64_t rows, int32_t cols, con
 static hipError_t launch_ada_flat(void* shard, int64_t rows, int32_t cols, const Batch& bt, int nb, int64_t stride,
                                   int K, const int32_t* slot, const uint32_t* rowflag, Ctrl* ctrl, uint64_t tail_cut,
                                   const AdaArgs& ada, hipStream_t st, int64_t* nblocks_out, LaunchEv ev) {
-    return launch_ada_flat_t<4, 2>(shard, rows, cols, bt, nb, stride, K, slot, rowflag, ctrl, tail_cut, ada, st,
-                                   nblocks_out, ev);
+    return launch_ada_flat_t<4, 2, DML_AB_ADA_NW>(shard, rows, cols, bt, nb, stride, K, slot, rowflag, ctrl, tail_cut,
+                                                  ada, st, nblocks_out, ev);
 }
 
 bool reduce_clears_slots(int vtype, int mode, int32_t cols) {
