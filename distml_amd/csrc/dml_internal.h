@@ -81,6 +81,11 @@ struct Batch {
     // before a speculative verdict could be read): the reduce takes slot = row for
     // them and verifies nothing.
     int32_t ident_ok;
+    // Rows any push of the chunk lists (byte per row, written by the key index; null:
+    // not tracked). Sparse-row chunks of k_reduce_rows (LDA's 65 536-row pushes into a
+    // 1 M-row table, config 5) leave ~11 % of the rows untouched: their shard rows are
+    // then neither read nor written.
+    const uint8_t* listed;
 };
 
 // A chunk whose predecessor ended abnormally (error, rows to replay, or a failed

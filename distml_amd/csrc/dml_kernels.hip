@@ -103,6 +103,7 @@ __global__ __launch_bounds__(256) void k_index(const Batch bt, int nb, int64_t n
             atomicMin(&ctrl->cutoff, (unsigned long long)pos_of((uint64_t)bt.bidx[b], (uint64_t)off));
             continue;
         }
+        if (bt.listed) const_cast<uint8_t*>(bt.listed)[idx] = 1u;  // every writer stores the same byte
         const int32_t old = atomicExch(&slot[idx * slot_stride(nb) + ctrl_col(ctrl, b)], (int32_t)r);
         if (old != -1 && !bt.keeps) {
             rowflag[idx] = 1u;
@@ -643,6 +644,9 @@ __global__ __launch_bounds__(64 * WPB) void k_reduce_rows(T* __restrict__ shard,
         // a push repeats this row: the host replays it exactly (a keeping chunk's index
         // flags nothing: no dependent flag load ahead of the row loads)
         if (rowflag && !bt.keeps && rowflag[row[r]]) continue;
+        // a row no push of the chunk lists: its shard row is neither read nor written
+        // (the index marked the listed ones; the load runs beside the flag load above)
+        if (MODE != kPreReduce && bt.listed && !bt.listed[row[r]]) continue;
         live |= 1u << r;
         if (!fb) fb = (const uint8_t*)rowp[r];
     }

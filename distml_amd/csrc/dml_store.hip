@@ -46,6 +46,13 @@ int dml::set_error(int code, const std::string& msg) { return set_err(code, msg)
         if (e_ != hipSuccess) return set_err(DML_E_HIP, std::string(#x) + ": " + hipGetErrorString(e_)); \
     } while (0)
 
+// A/B switch (scripts/build_ab.sh nolisted -DDML_AB_NO_LISTED=1): no listed-row skip
+#ifdef DML_AB_NO_LISTED
+constexpr bool kListedRows = false;
+#else
+constexpr bool kListedRows = true;
+#endif
+
 namespace {
 
 // java.util.Random as its specification defines it: 48-bit LCG (multiplier
@@ -192,6 +199,7 @@ struct Workspace {
     SpStat* hsp = nullptr;            // pinned status of the single-pass sparse partition
     Ctrl* hidx = nullptr;             // pinned copy of ctrl right after the index (flat speculative chunks)
     bool flat_ident = false;          // the chunk's apply runs k_flat_ident (chosen from hidx)
+    uint8_t* listed = nullptr;        // rows the chunk's pushes list (Batch::listed), grown on first use
     bool clears = false;              // the chunk's reduce leaves its slot table all -1
     bool clean = false;               // slot table all -1 and rowflags 0: only the Ctrl needs a reset
     // Kept slot table (the last chunk here was a verified speculative chunk): rowflags
@@ -530,6 +538,19 @@ int launch_chunk(dml_store* s, Chunk& c, Workspace& W, const Ctrl* prev) {
             if (full) {
                 HIPCHK(launch_ident_full(c.bt, c.nb, c.max_nrec, s->stride, s->K, s->first, s->rows, W.ctrl, is));
                 c.bt.ident_ok = 1;
+            }
+        }
+        // Sparse-row chunks of k_reduce_rows (some push lists only part of the rows): the
+        // index marks the rows any push lists, and the reduce skips the others' shard rows
+        c.bt.listed = nullptr;
+        if (kListedRows && !c.spec && !s->adagrad && (reduce_mode(s) == kAdd || reduce_mode(s) == kAddCheckI32) &&
+            !use_flat(vtype_of(s->desc), reduce_mode(s), s->cols, c.bt, c.nb, s->rows)) {
+            bool part = false;
+            for (int j = 0; j < c.nb && !part; ++j) part = c.bt.nrec[j] < s->rows;
+            if (part) {
+                if (!W.listed) HIPCHK(hipMalloc((void**)&W.listed, (size_t)s->rows));
+                HIPCHK(hipMemsetAsync(W.listed, 0, (size_t)s->rows, is));
+                c.bt.listed = W.listed;
             }
         }
         HIPCHK(launch_index(c.bt, c.nb, c.max_nrec, s->stride, s->K, s->first, s->rows, W.slot, W.rowflag, W.ctrl,
@@ -1130,6 +1151,7 @@ void dml_store_destroy(dml_store* s) {
             (void)hipFree(W.sp);
             if (W.hsp) (void)hipHostFree(W.hsp);
             if (W.hidx) (void)hipHostFree(W.hidx);
+            if (W.listed) (void)hipFree(W.listed);
             if (W.hctrl) (void)hipHostFree(W.hctrl);
             if (W.idx_done) (void)hipEventDestroy(W.idx_done);
             if (W.done) (void)hipEventDestroy(W.done);
