@@ -108,6 +108,7 @@ SIGNATURES = {
     "dml_diag_stream": (C.c_int, [_i32, _vp, _vp, _i64, _vp, _P(C.c_float)]),
     "dml_diag_ring_rs": (C.c_int, [_i32, _vp, _vp, _vp, _i64, _i32, _i32, _i32, _vp]),
     "dml_diag_rmw_floor": (C.c_int, [_vp, _vp, _vp, _i64, _vp, _P(C.c_float)]),
+    "dml_diag_store_knob": (C.c_int, [_vp, _i32, _i64]),
     "dml_last_error": (C.c_char_p, []),
     "dml_version": (C.c_char_p, []),
 }

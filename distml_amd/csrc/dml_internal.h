@@ -307,6 +307,8 @@ bool use_flat(int vtype, int mode, int32_t cols, const Batch& bt, int nb, int64_
 // row as record r = row r (flat_ident_ok), no cutoff, no repeated row. Its waves
 // verify every key; a mismatch clears ctrl->spec_ok as k_reduce_flat does.
 constexpr int kFlatIdentWaves = 8;
+hipError_t launch_ada_ident(void* shard, int64_t rows, int32_t cols, const Batch& bt, int nb, int64_t stride, int K,
+                            const AdaArgs& ada, hipStream_t st, int64_t* ncand_out, LaunchEv ev = {});
 hipError_t launch_flat_ident(int vtype, int mode, void* shard, int64_t rows, int32_t cols, const Batch& bt, int nb,
                              int64_t stride, int K, Ctrl* ctrl, hipStream_t st, int64_t* nblocks_out,
                              LaunchEv ev = {}, RowMap rm = {});

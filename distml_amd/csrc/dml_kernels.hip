@@ -35,6 +35,17 @@ constexpr bool kAdaBurst = true;
 #else
 constexpr bool kAdaBurst = false;
 #endif
+#ifndef DML_AB_AI_NW
+#define DML_AB_AI_NW 4
+#endif
+#ifndef DML_AB_AI_BPC
+#define DML_AB_AI_BPC 0
+#endif
+#ifdef DML_AB_AI_BAR
+constexpr bool kAiBar = true;
+#else
+constexpr bool kAiBar = false;
+#endif
 #ifndef DML_AB_ADA_NW
 #define DML_AB_ADA_NW 4
 #endif
@@ -1505,6 +1516,146 @@ __global__ __launch_bounds__(NW * 64) void k_ada_flat(float* __restrict__ shard,
     }
 }
 
+// k_ada_ident: k_ada_flat for the AdaGrad chunks the host has seen to be all identity
+// after the index (every push full-range with record r = row r, checked record by
+// record before the launch; no cutoff, no repeated row: config 4's AdaGrad steady
+// state). Same per-element arithmetic, order and maxDelta candidates as k_ada_flat
+// (bit for bit), with nothing else in it:
+//  - data / delta / alpha offsets from the wave's first row, and record offsets from
+//    its first record, are 32-bit per-lane constants that every array and push shares
+//    (buffer loads at a wave-uniform base; a lane without a vector reads zeros from the
+//    range check), no slot rows, no LDS;
+//  - every load of the wave (data, delta, all pushes) is issued before the first add;
+//  - the maxDelta candidate is reduced per wave (one entry per wave in ada.cand, no
+//    block barrier): a wave leaves as soon as its own rows are written.
+template <int J, int NW, int NB>
+__global__ __launch_bounds__(NW * 64) void k_ada_ident(float* __restrict__ shard, int64_t rows, int32_t cols, int32_t R,
+                                                   const Batch bt, int64_t stride, int K, AdaArgs ada) {
+    constexpr int VEC = 4, NBMAX = NB, nb = NB;  // NB pushes (1..4): their loads all in flight
+    const int lane = threadIdx.x & 63;
+    const int wid = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    const int64_t t0 = (xcd_block() * NW + wid) * R;
+    float cand_v = 0.f;
+    uint64_t cand_p = kNoPos;
+    bool cand_ok = false;
+    const bool live = t0 < rows && !(bt.prev && ctrl_abnormal(bt.prev));
+    if (kAiBar || live) {
+        const int nrow = !live ? 0 : (int)(rows - t0 < (int64_t)R ? rows - t0 : (int64_t)R);
+        const int NV = cols / VEC, nvec = nrow * NV;
+        uint32_t eoff[J], roff[J];
+        int rc[J];  // (row << 16 | vector within the row)
+#pragma unroll
+        for (int j = 0; j < J; ++j) {
+            const int v = j * 64 + lane;
+            const int rl = v / NV, cv = v - rl * NV;
+            const bool on = v < nvec;
+            rc[j] = (rl << 16) | cv;
+            eoff[j] = on ? (uint32_t)((rl * cols + cv * VEC) * 4) : kBufOff;
+            roff[j] = on ? (uint32_t)(rl * stride + K + cv * 16) : kBufOff;
+        }
+        const uint32_t espan = (uint32_t)(nrow * cols * 4), rspan = (uint32_t)(nrow * stride);
+        const int64_t e0 = t0 * (int64_t)cols;
+        const __amdgpu_buffer_rsrc_t ds = buf_rsrc(shard + e0, espan);
+        const __amdgpu_buffer_rsrc_t dd = buf_rsrc(ada.delta + e0, espan);
+        float acc[J][VEC], dl[J][VEC], lg[J][VEC], rv[J][VEC];
+        int rb[J][VEC];  // push of the element's last strict rise (-1: none)
+        u32x4 raw[NBMAX][J];
+#pragma unroll
+        for (int j = 0; j < J; ++j) {
+            unpack<float>(ldb16_nt(ds, eoff[j]), acc[j]);
+            unpack<float>(ldb16_nt(dd, eoff[j]), dl[j]);
+        }
+#pragma unroll
+        for (int b = 0; b < NBMAX; ++b)
+            if (b < nb) {
+                const __amdgpu_buffer_rsrc_t rs = buf_rsrc(bt.base[b] + t0 * stride, rspan);
+#pragma unroll
+                for (int j = 0; j < J; ++j) raw[b][j] = ldb16_nt(rs, roff[j]);
+            }
+#pragma unroll
+        for (int j = 0; j < J; ++j)
+#pragma unroll
+            for (int e = 0; e < VEC; ++e) {
+                lg[j][e] = 0.f;
+                rv[j][e] = 0.f;
+                rb[j][e] = -1;
+            }
+        // k_ada_flat's upd(), pushes in order
+#pragma unroll
+        for (int b = 0; b < NBMAX; ++b)
+            if (b < nb)
+#pragma unroll
+                for (int j = 0; j < J; ++j) {
+                    float u[VEC];
+                    unpack<float>(raw[b][j], u);
+#pragma unroll
+                    for (int e = 0; e < VEC; ++e) {
+                        acc[j][e] = __fadd_rn(acc[j][e], u[e]);
+                        const float nd = __fadd_rn(dl[j][e], __fmul_rn(u[e], u[e]));
+                        if (nd > dl[j][e]) { rv[j][e] = nd; rb[j][e] = b; }
+                        if (nd > 1.0f) lg[j][e] = nd;
+                        dl[j][e] = nd;
+                    }
+                }
+        // (A/B, off: kAiBar) the block's writes leave together
+        if (kAiBar) __syncthreads();
+        const __amdgpu_buffer_rsrc_t da = buf_rsrc(ada.alpha + e0, espan);
+        const uint64_t bi0 = (uint64_t)bt.bidx[0], bi1 = NB > 1 ? (uint64_t)bt.bidx[NB > 1 ? 1 : 0] : 0,
+                       bi2 = NB > 2 ? (uint64_t)bt.bidx[NB > 2 ? 2 : 0] : 0, bi3 = NB > 3 ? (uint64_t)bt.bidx[NB > 3 ? 3 : 0] : 0;
+#pragma unroll
+        for (int j = 0; j < J; ++j) {
+            if (eoff[j] == kBufOff) continue;
+            __builtin_amdgcn_raw_buffer_store_b128(pack<float>(acc[j]), ds, (int)eoff[j], 0, 2);
+            __builtin_amdgcn_raw_buffer_store_b128(pack<float>(dl[j]), dd, (int)eoff[j], 0, 2);
+            // alpha where the last delta a push left above 1 sets it
+            // (FloatMatrixStoreAdaGrad.java:268-272)
+            float na[VEC];
+            bool all_a = true, any_a = false;
+#pragma unroll
+            for (int e = 0; e < VEC; ++e) {
+                na[e] = 0.f;
+                if (lg[j][e] > 1.0f) {
+                    na[e] = (float)((double)ada.initial_alpha / ((double)ada.factor * sqrt((double)lg[j][e])));
+                    if (na[e] < ada.min_alpha) na[e] = ada.min_alpha;
+                    any_a = true;
+                } else {
+                    all_a = false;
+                }
+            }
+            if (all_a) {
+                __builtin_amdgcn_raw_buffer_store_b128(pack<float>(na), da, (int)eoff[j], 0, 2);
+            } else if (any_a) {
+#pragma unroll
+                for (int e = 0; e < VEC; ++e)
+                    if (lg[j][e] > 1.0f)
+                        __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(na[e]), da, (int)(eoff[j] + 4 * e), 0, 0);
+            }
+            const int rl = rc[j] >> 16, cv = rc[j] & 0xFFFF;
+#pragma unroll
+            for (int e = 0; e < VEC; ++e) {
+                if (rb[j][e] < 0) continue;
+                const int g = rb[j][e];  // (a select chain, not a per-lane index into the kernarg table)
+                const uint64_t gb = g == 0 ? bi0 : g == 1 ? bi1 : g == 2 ? bi2 : bi3;
+                const uint64_t p = pos_of(gb,
+                                          (uint64_t)((t0 + rl) * stride + K + (int64_t)(cv * VEC + e) * 4));
+                if (!cand_ok || rv[j][e] > cand_v || (rv[j][e] == cand_v && p < cand_p)) {
+                    cand_ok = true;
+                    cand_v = rv[j][e];
+                    cand_p = p;
+                }
+            }
+        }
+    }
+    cand_block_best<1>(cand_ok, cand_v, cand_p);
+    if (lane == 0) {
+        DeltaCand c;
+        c.value = cand_v;
+        c.valid = cand_ok;
+        c.pos = cand_p;
+        ada.cand[blockIdx.x * (int64_t)NW + wid] = c;
+    }
+}
+
 // Occupancy cap: dynamic LDS (unused by the kernels) so that at most `bpc`
 // 256-thread blocks fit on a CU (160 KiB of LDS per CU). 0 = no cap.
 constexpr unsigned kLdsPerCU = 160 * 1024;
@@ -1761,6 +1912,45 @@ static hipError_t launch_ada_flat_t(void* shard, int64_t rows, int32_t cols, con
         hipLaunchKernelGGL((k_ada_flat<JMAX, PB, NW>), dim3((unsigned)nblocks), dim3(NW * 64), 0, st, (float*)shard,
                            rows, cols, R, bt, nb, stride, K, const_cast<int32_t*>(slot), rowflag, ctrl, tail_cut, ada);
     return hipGetLastError();
+}
+
+// k_ada_ident launch: the all-identity AdaGrad chunks of the flat shape (the host
+// checked the index's Ctrl, as for k_flat_ident), at most 4 pushes. One maxDelta
+// candidate per wave: *ncand_out = the waves launched (<= reduce_blocks(), the
+// candidate buffer's size).
+constexpr int kAdaIdentJ = 4, kAdaIdentWaves = DML_AB_AI_NW;
+
+template <int NB>
+static hipError_t launch_ada_ident_t(void* shard, int64_t rows, int32_t cols, int R, int64_t nblocks, const Batch& bt,
+                                     int64_t stride, int K, const AdaArgs& ada, hipStream_t st, LaunchEv ev) {
+    constexpr int J = kAdaIdentJ, NW = kAdaIdentWaves;
+    static const std::string kn = kname("k_ada_ident", J, NW, NB);
+    g_kernel_name = kn.c_str();
+    const unsigned lds = lds_for_blocks_per_cu(DML_AB_AI_BPC);  // (A/B: occupancy cap, 0 = none)
+    if (ev.start || ev.stop)
+        hipExtLaunchKernelGGL((k_ada_ident<J, NW, NB>), dim3((unsigned)nblocks), dim3(NW * 64), lds, st, ev.start,
+                              ev.stop, 0, (float*)shard, rows, cols, R, bt, stride, K, ada);
+    else
+        hipLaunchKernelGGL((k_ada_ident<J, NW, NB>), dim3((unsigned)nblocks), dim3(NW * 64), lds, st, (float*)shard,
+                           rows, cols, R, bt, stride, K, ada);
+    return hipGetLastError();
+}
+
+hipError_t launch_ada_ident(void* shard, int64_t rows, int32_t cols, const Batch& bt, int nb, int64_t stride, int K,
+                            const AdaArgs& ada, hipStream_t st, int64_t* ncand_out, LaunchEv ev) {
+    constexpr int J = kAdaIdentJ, NW = kAdaIdentWaves;
+    if (nb <= 0 || nb > 4 || cols % 4 || (int64_t)cols * 4 >= 4096) return hipErrorInvalidValue;
+    const int NV = cols / 4;
+    const int R = std::max(1, std::min(16, J * 64 / NV));
+    const int64_t nblocks = ((rows + R - 1) / R + NW - 1) / NW;
+    if (ncand_out) *ncand_out = nblocks * NW;
+    if (nblocks <= 0) return hipSuccess;
+    switch (nb) {
+        case 1: return launch_ada_ident_t<1>(shard, rows, cols, R, nblocks, bt, stride, K, ada, st, ev);
+        case 2: return launch_ada_ident_t<2>(shard, rows, cols, R, nblocks, bt, stride, K, ada, st, ev);
+        case 3: return launch_ada_ident_t<3>(shard, rows, cols, R, nblocks, bt, stride, K, ada, st, ev);
+        default: return launch_ada_ident_t<4>(shard, rows, cols, R, nblocks, bt, stride, K, ada, st, ev);
+    }
 }
 
 // JMAX 4 vectors per lane (R = 5 rows at 200 columns), two pushes per round: for

@@ -47,6 +47,13 @@ int dml::set_error(int code, const std::string& msg) { return set_err(code, msg)
     } while (0)
 
 // A/B switch (scripts/build_ab.sh nolisted -DDML_AB_NO_LISTED=1): no listed-row skip
+// A/B switch (scripts/build_ab.sh noadaident -DDML_AB_NO_ADA_IDENT=1): AdaGrad's identity
+// chunks through k_ada_flat instead of k_ada_ident
+#ifdef DML_AB_NO_ADA_IDENT
+constexpr bool kAdaIdent = false;
+#else
+constexpr bool kAdaIdent = true;
+#endif
 #ifdef DML_AB_NO_LISTED
 constexpr bool kListedRows = false;
 #else
@@ -219,6 +226,7 @@ struct Pending {
 struct dml_store {
     std::mutex mu;
     int device = 0;
+    int64_t ident_full_min = (int64_t)64 << 20;  // DML_KNOB_IDENT_FULL_MIN_BYTES
     hipStream_t stream = nullptr;     // applies (reduce / scatter-add), in push order
     hipStream_t istream = nullptr;    // key index of the next chunk, overlapping the current apply
     hipStream_t cstream = nullptr;    // ctrl read-back, off the apply stream
@@ -475,7 +483,10 @@ int launch_apply(dml_store* s, Chunk& c, Workspace& W, const Ctrl* prev) {
         int64_t nblk = 0;
         W.clears = reduce_clears_slots(vtype_of(s->desc), reduce_mode(s), s->cols);
         c.bt.src = c.in != c.out ? c.in : nullptr;
-        if (W.flat_ident)  // every push verified-identity by the index (the host's Ctrl copy)
+        if (W.flat_ident && s->adagrad)  // every push verified-identity (the host's Ctrl copy)
+            HIPCHK(launch_ada_ident(c.out, s->rows, s->cols, c.bt, c.nb, s->stride, s->K, ada_args(s), s->stream,
+                                    &nblk, ev));
+        else if (W.flat_ident)
             HIPCHK(launch_flat_ident(vtype_of(s->desc), reduce_mode(s), c.out, s->rows, s->cols, c.bt, c.nb,
                                      s->stride, s->K, W.ctrl, s->stream, &nblk, ev));
         else
@@ -531,7 +542,7 @@ int launch_chunk(dml_store* s, Chunk& c, Workspace& W, const Ctrl* prev) {
         // to DRAM; see dml_prereduce_begin)
         c.bt.ident_ok = 0;
         if (s->adagrad && c.tail_cut == kNoPos &&
-            (int64_t)s->rows * slot_stride(c.nb) * 4 > ((int64_t)64 << 20) &&
+            (int64_t)s->rows * slot_stride(c.nb) * 4 > s->ident_full_min &&
             use_flat(vtype_of(s->desc), reduce_mode(s), s->cols, c.bt, c.nb, s->rows)) {
             bool full = c.nb > 0;
             for (int j = 0; j < c.nb && full; ++j) full = c.bt.nrec[j] == s->rows;
@@ -559,8 +570,9 @@ int launch_chunk(dml_store* s, Chunk& c, Workspace& W, const Ctrl* prev) {
         // cutoff, repeats) is final here; a pinned copy lets the host pick the lean
         // all-identity kernel after the wait below (k_flat_ident)
         W.flat_ident = false;
-        if (c.spec && reduce_mode(s) == kAdd && c.tail_cut == kNoPos &&
-            use_flat(vtype_of(s->desc), kAdd, s->cols, c.bt, c.nb, s->rows)) {
+        // AdaGrad chunks checked record by record (ident_ok) likewise pick k_ada_ident
+        if (((c.spec && reduce_mode(s) == kAdd) || (kAdaIdent && s->adagrad && c.bt.ident_ok)) &&
+            c.tail_cut == kNoPos && use_flat(vtype_of(s->desc), reduce_mode(s), s->cols, c.bt, c.nb, s->rows)) {
             if (!W.hidx) HIPCHK(hipHostMalloc((void**)&W.hidx, sizeof(Ctrl), hipHostMallocDefault));
             W.hidx->cutoff = 0;  // not all-identity unless the copy lands
             HIPCHK(hipMemcpyAsync(W.hidx, W.ctrl, sizeof(Ctrl), hipMemcpyDeviceToHost, is));
@@ -1592,6 +1604,16 @@ int dml_store_set_timing(dml_store* s, int32_t enable) {
     s->timing_every = enable > 1 ? enable : 1;
     s->timing_k = 0;
     return DML_OK;
+}
+
+int dml_diag_store_knob(dml_store* s, int32_t knob, int64_t value) {
+    if (int rc = check_store(s)) return rc;
+    if (value < 0) return set_err(DML_E_INVALID_ARG, "negative knob value");
+    std::lock_guard<std::mutex> lk(s->mu);
+    switch (knob) {
+        case DML_KNOB_IDENT_FULL_MIN_BYTES: s->ident_full_min = value; return DML_OK;
+        default: return set_err(DML_E_INVALID_ARG, "unknown knob");
+    }
 }
 
 int dml_store_kernel_name(dml_store* s, char* out, int32_t cap) {

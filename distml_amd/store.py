@@ -385,6 +385,10 @@ class DataStore:
         """Kernel timing of the dominant reduce: every launch, or one chunk in `every`."""
         check(_lib.load().dml_store_set_timing(self._h, (max(int(every), 1) if on else 0)), self)
 
+    def set_knob(self, knob: int, value: int):
+        """Diagnostic tuning knob (dml_diag_store_knob), e.g. DML_KNOB_IDENT_FULL_MIN_BYTES = 1."""
+        check(_lib.load().dml_diag_store_knob(self._h, int(knob), int(value)), self)
+
     def kernel_name(self) -> str:
         """Instantiation of the dominant kernel last launched (dml_store_kernel_name)."""
         buf = C.create_string_buffer(512)

@@ -442,6 +442,15 @@ int dml_diag_rmw_floor(float* dev_array, const uint32_t* dev_index, const float*
 int dml_diag_ring_rs(int32_t value_type, const void* dev_partial, void* dev_recv, void* dev_landing,
                      int64_t chunk_bytes, int32_t world, int32_t rank, int32_t channels, void* stream);
 
+/* Store tuning knob (diagnostic / tests): DML_KNOB_IDENT_FULL_MIN_BYTES = the slot-table
+ * size (bytes) from which an AdaGrad chunk of full-range pushes checks every record's key
+ * up front (k_ident_full) instead of running the key index, so that all-identity chunks
+ * run k_ada_ident (default 64 MiB: where the index's slot-table atomics leave the caches).
+ * Lowering it lets tests drive that path at small sizes; results are the same either way.
+ * Returns DML_E_INVALID_ARG for an unknown knob or a negative value. */
+#define DML_KNOB_IDENT_FULL_MIN_BYTES 1
+int dml_diag_store_knob(dml_store* s, int32_t knob, int64_t value);
+
 /* --- misc --------------------------------------------------------------- */
 const char* dml_last_error(void);   /* thread-local message for the last failure */
 const char* dml_version(void);

@@ -46,10 +46,11 @@ __device__ inline u32x4 addu(u32x4 a, u32x4 b) {
     return r;
 }
 
-template <int NR, int NO, int U, int LP, int SP, bool INPLACE, bool PERSIST, bool SYNC = false>
+__device__ inline int64_t xcd_remap();
+template <int NR, int NO, int U, int LP, int SP, bool INPLACE, bool PERSIST, bool SYNC = false, bool XCD = false>
 __global__ __launch_bounds__(256) void k_mix(Arr a, Arr o, int64_t ntiles) {
     constexpr uint32_t TILE = 256u * U * 16u;
-    for (int64_t t = blockIdx.x; t < ntiles; t += PERSIST ? gridDim.x : ntiles) {
+    for (int64_t t = XCD ? xcd_remap() : (int64_t)blockIdx.x; t < ntiles; t += PERSIST ? gridDim.x : ntiles) {
         const int64_t base = t * (int64_t)TILE;
         u32x4 acc[U];
 #pragma unroll
@@ -67,6 +68,12 @@ __global__ __launch_bounds__(256) void k_mix(Arr a, Arr o, int64_t ntiles) {
 #pragma unroll
             for (int u = 0; u < U; ++u) acc[u] = addu(acc[u], v[r][u]);
         if (SYNC) __syncthreads();
+        if (NO == 0) {  // reads only: keep the loads live
+            uint32_t x = 0;
+#pragma unroll
+            for (int u = 0; u < U; ++u) x ^= acc[u].x ^ acc[u].y ^ acc[u].z ^ acc[u].w;
+            if (x == 0x9e3779b9u) o.p[0][threadIdx.x] = 1;
+        }
 #pragma unroll
         for (int w = 0; w < NO; ++w) {
             const auto rs = rsrc((INPLACE ? a.p[w] : o.p[w]) + base, TILE);
@@ -77,6 +84,98 @@ __global__ __launch_bounds__(256) void k_mix(Arr a, Arr o, int64_t ntiles) {
                 __builtin_amdgcn_raw_buffer_store_b128(x, rs, (int)((u * 256 + threadIdx.x) * 16), 0, SP);
             }
         }
+    }
+}
+
+// AdaGrad-shaped stream: data += u0 + u1 and delta += u0^2 + u1^2 per element (two
+// pushes, in place), with k_ada_flat's per-element bookkeeping (last strict rise, last
+// delta above 1, maxDelta candidate with its position, reduced per wave) when BOOK; REC:
+// the pushes are 804-B records ([4-B key][200 floats]) as in config 4, else flat arrays.
+__device__ inline int64_t xcd_remap() {  // XCD x runs the x-th contiguous run of blocks
+    const int64_t nbk = gridDim.x, b = blockIdx.x, per = (nbk + 7) / 8, x = b % 8, i = b / 8;
+    const int64_t full = nbk - (per - 1) * 8;
+    return x < full ? x * per + i : full * per + (x - full) * (per - 1) + i;
+}
+template <int U, bool BOOK, bool REC, bool XCD = false>
+__global__ __launch_bounds__(256) void k_adalike(Arr a, Arr o, int64_t ntiles) {
+    constexpr uint32_t TILE = 256u * U * 16u;
+    const int64_t t = XCD ? xcd_remap() : (int64_t)blockIdx.x;
+    const int64_t base = t * (int64_t)TILE;
+    const auto rd = rsrc(a.p[0] + base, TILE), rl = rsrc(a.p[1] + base, TILE);
+    // record layout: element index i = base/4 + (u*256 + tid)*4 -> row i / 200, col i % 200
+    __amdgpu_buffer_rsrc_t rp[2];
+    uint32_t poff[U];
+    const int64_t e0 = base / 4, row0 = e0 / 200;
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+        const int64_t e = e0 + (int64_t)(u * 256 + threadIdx.x) * 4;
+        poff[u] = REC ? (uint32_t)((e / 200 - row0) * 804 + 4 + (e % 200) * 4) : (uint32_t)((u * 256 + threadIdx.x) * 16);
+    }
+#pragma unroll
+    for (int b = 0; b < 2; ++b) rp[b] = REC ? rsrc(a.p[2 + b] + row0 * 804, TILE / 200 * 804 + 2 * 804) : rsrc(a.p[2 + b] + base, TILE);
+    u32x4 d[U], l[U], q[2][U];
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+        d[u] = __builtin_amdgcn_raw_buffer_load_b128(rd, (int)((u * 256 + threadIdx.x) * 16), 0, 2);
+        l[u] = __builtin_amdgcn_raw_buffer_load_b128(rl, (int)((u * 256 + threadIdx.x) * 16), 0, 2);
+    }
+#pragma unroll
+    for (int b = 0; b < 2; ++b)
+#pragma unroll
+        for (int u = 0; u < U; ++u) q[b][u] = __builtin_amdgcn_raw_buffer_load_b128(rp[b], (int)poff[u], 0, 2);
+    float cv = 0.f;
+    uint64_t cp = ~0ull;
+    bool cok = false;
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+        float acc[4], dl[4], lg[4] = {0, 0, 0, 0}, rv[4] = {0, 0, 0, 0};
+        int rb[4] = {-1, -1, -1, -1};
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+            acc[e] = __uint_as_float(d[u][e]);
+            dl[e] = __uint_as_float(l[u][e]);
+        }
+#pragma unroll
+        for (int b = 0; b < 2; ++b)
+#pragma unroll
+            for (int e = 0; e < 4; ++e) {
+                const float x = __uint_as_float(q[b][u][e]);
+                acc[e] = __fadd_rn(acc[e], x);
+                const float nd = __fadd_rn(dl[e], __fmul_rn(x, x));
+                if (BOOK) {
+                    if (nd > dl[e]) { rv[e] = nd; rb[e] = b; }
+                    if (nd > 1.0f) lg[e] = nd;
+                }
+                dl[e] = nd;
+            }
+        u32x4 od, ol;
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+            od[e] = __float_as_uint(acc[e]);
+            ol[e] = __float_as_uint(dl[e]);
+        }
+        __builtin_amdgcn_raw_buffer_store_b128(od, rd, (int)((u * 256 + threadIdx.x) * 16), 0, 2);
+        __builtin_amdgcn_raw_buffer_store_b128(ol, rl, (int)((u * 256 + threadIdx.x) * 16), 0, 2);
+        if (BOOK) {
+#pragma unroll
+            for (int e = 0; e < 4; ++e) {
+                if (lg[e] > 1.0f) o.p[0][(base + (u * 256 + threadIdx.x) * 16 + e * 4) & 0xFFFF] = 1;
+                if (rb[e] < 0) continue;
+                const uint64_t p = ((uint64_t)rb[e] << 40) | (uint64_t)(poff[u] + e * 4);
+                if (!cok || rv[e] > cv || (rv[e] == cv && p < cp)) { cok = true; cv = rv[e]; cp = p; }
+            }
+        }
+    }
+    if (BOOK) {
+#pragma unroll
+        for (int m = 32; m > 0; m >>= 1) {
+            const float ov = __shfl_xor(cv, m);
+            const uint32_t lo = (uint32_t)__shfl_xor((int)(uint32_t)cp, m), hi = (uint32_t)__shfl_xor((int)(uint32_t)(cp >> 32), m);
+            const bool ook = __shfl_xor((int)cok, m) != 0;
+            const uint64_t op = (uint64_t)lo | ((uint64_t)hi << 32);
+            if (ook && (!cok || ov > cv || (ov == cv && op < cp))) { cok = true; cv = ov; cp = op; }
+        }
+        if ((threadIdx.x & 63) == 0) *(uint64_t*)(o.p[1] + (blockIdx.x * 4 + (threadIdx.x >> 6)) * 16) = cp ^ __float_as_uint(cv);
     }
 }
 
@@ -93,7 +192,7 @@ int main(int argc, char** argv) {
     const int64_t n = (int64_t)(gib * (1 << 30)) / (1 << 20) * (1 << 20);  // bytes per array, MiB multiple
     Arr a{}, o{};
     for (int i = 0; i < 17; ++i) {
-        CK(hipMalloc(&a.p[i], n));
+        CK(hipMalloc(&a.p[i], n + n / 128 + (1 << 20)));  // room for 804-B records of n / 4 floats
         hipLaunchKernelGGL(k_fill, dim3(8192), dim3(256), 0, 0, a.p[i], n, 11u * i + 1u);
     }
     for (int i = 0; i < 2; ++i) CK(hipMalloc(&o.p[i], n));
@@ -155,6 +254,15 @@ int main(int argc, char** argv) {
     run("r4w2 in place U4 nt nt sync", k_mix<4, 2, 4, 2, 2, true, false, true>, 4, 2, 4, false);
     run("r4w2 in place U4 nt nt persist", k_mix<4, 2, 4, 2, 2, true, true>, 4, 2, 4, true);
     run("r4w2 out U4 nt nt", k_mix<4, 2, 4, 2, 2, false, false>, 4, 2, 4, false);
+    run("ada U4 plain", k_adalike<4, false, false>, 4, 2, 4, false);
+    run("ada U4 book", k_adalike<4, true, false>, 4, 2, 4, false);
+    run("ada U4 rec", k_adalike<4, false, true>, 4, 2, 4, false);
+    run("ada U4 book rec", k_adalike<4, true, true>, 4, 2, 4, false);
+    run("ada U2 book rec", k_adalike<2, true, true>, 4, 2, 2, false);
+    run("ada U4 book rec xcd", k_adalike<4, true, true, true>, 4, 2, 4, false);
+    run("ada U4 plain xcd", k_adalike<4, false, false, true>, 4, 2, 4, false);
+    run("r4w2 in place U4 nt nt xcd", k_mix<4, 2, 4, 2, 2, true, false, false, true>, 4, 2, 4, false);
+    run("r17w1 in place U2 nt nt xcd", k_mix<17, 1, 2, 2, 2, true, false, false, true>, 17, 1, 2, false);
     // 17 : 1 (sixteen pushes + shard -> shard)
     run("r17w1 in place U2 nt nt", k_mix<17, 1, 2, 2, 2, true, false>, 17, 1, 2, false);
     run("r17w1 in place U2 nt nt sync", k_mix<17, 1, 2, 2, 2, true, false, true>, 17, 1, 2, false);

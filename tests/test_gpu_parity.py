@@ -1617,7 +1617,7 @@ def _perm10m(b, rows):
     return a, b * 7919 % rows
 
 
-@pytest.mark.parametrize("case", ["sum_ascending", "sum_permuted", "adagrad", "prereduce_world8"])
+@pytest.mark.parametrize("case", ["sum_ascending", "sum_permuted", "adagrad", "adagrad_ascending", "prereduce_world8"])
 def test_config4_model_size_sampled_rows(oracle, case):
     """The config-4 legs at the size bench.py times: the 10 M x 200 fp32
     model (8 GB per array; byte offsets past 2^32), device-resident full-range pushes,
@@ -1625,22 +1625,25 @@ def test_config4_model_size_sampled_rows(oracle, case):
     records (pyoracle.synth_dense_rows: a full-range push's per-element result does not
     depend on record order). sum_*: k_reduce_flat, 4 pushes (FloatMatrixStore.java:
     200-222), ascending (identity speculation) or permuted; adagrad: k_ada_flat, 2
-    pushes, data / alpha / delta (FloatMatrixStoreAdaGrad.java:262-277); prereduce_world8:
+    pushes, data / alpha / delta (FloatMatrixStoreAdaGrad.java:262-277), one ascending and
+    one permuted (adagrad: k_ada_flat) or both ascending (adagrad_ascending: k_ada_ident,
+    the bench's 4a leg); prereduce_world8:
     the kPreReduce partial a rank writes at N = 8 ([rank][row], 8 x 1 250 000 rows), one
     ascending and one permuted push summed in push order. All bit-exact."""
     import ctypes as C
     from distml_amd import DataDesc, DataStore, KeyList, KeyRange, _lib
     from distml_amd.group import HipOps
     rows, cols = 10_000_000, 200
-    ada = case == "adagrad"
-    W = {"adagrad": 2, "prereduce_world8": 2}.get(case, 4)
+    ada = case.startswith("adagrad")
+    W = {"adagrad": 2, "adagrad_ascending": 2, "prereduce_world8": 2}.get(case, 4)
     fmt = DataDesc(1, 0, 1, False, True, ada)
     L = _lib.load()
     pick = _config4_rows(rows)
     s0 = torch.cuda.current_stream().cuda_stream
     dev = []
     for b in range(W):
-        pa, pc = (1, 0) if case == "sum_ascending" or (case != "sum_permuted" and b == 0) else _perm10m(b, rows)
+        pa, pc = (1, 0) if case in ("sum_ascending", "adagrad_ascending") or (case != "sum_permuted" and b == 0) \
+            else _perm10m(b, rows)
         t = torch.empty(rows * (4 + 4 * cols), dtype=torch.uint8, device="cuda")
         assert L.dml_synth_dense_bucket(t.data_ptr(), C.byref(fmt.to_c()), 0, rows, rows, cols, 3000 + b, pa, pc,
                                         C.c_void_p(s0)) == 0
@@ -1668,6 +1671,9 @@ def test_config4_model_size_sampled_rows(oracle, case):
         o.synth_fill_rows(pick, 13)
         st.pushDevice([t.data_ptr() for t in dev], [t.numel() for t in dev])
         st.flush()
+        if ada:
+            want = "dml::k_ada_ident<" if case == "adagrad_ascending" else "dml::k_ada_flat<"
+            assert st.kernel_name().startswith(want), (st.kernel_name(), want)
         if not ada:
             rec = np.frombuffer(st.handleFetch(fmt, KeyList(pick.tolist())), np.uint8).reshape(len(pick), 4 + 4 * cols)
             assert rec[:, :4].copy().view("<i4").ravel().tolist() == pick.tolist()
@@ -1983,6 +1989,55 @@ def test_adagrad_flat_exact(oracle, case, W, cols):
     a, d = s.adagrad_state()
     assert kat.bits_equal(a, o.alpha) and kat.bits_equal(d, o.delta)
     assert s.maxDelta() == o.max_delta()
+    s.close()
+
+
+@pytest.mark.parametrize("cols", [200, 48])
+@pytest.mark.parametrize("W", [1, 2, 3, 4])
+@pytest.mark.parametrize("case", ["plain", "large", "swapped", "partial"])
+def test_adagrad_ident_exact(oracle, case, W, cols):
+    """k_ada_ident (AdaGrad chunks of full-range pushes whose records are rows in order,
+    every key checked before the launch) bit-exact against the oracle:
+    data, alpha, delta, maxDelta/row/col. The key check's threshold is lowered
+    (DML_KNOB_IDENT_FULL_MIN_BYTES) so the path runs at this size. `large`: delta past 1
+    (alpha written) plus a NaN and an Inf element; `swapped`: the last push has two
+    records swapped (not identity: k_ada_flat takes the chunk); `partial`: the last push
+    omits the last row (not full-range: the key index, k_ada_flat). Two batches, so the
+    second starts from the first's delta and maxDelta."""
+    from distml_amd import DataDesc, encode_matrix_push
+    rng = np.random.default_rng(100 * W + cols + len(case))
+    first, rows = 50, 2999  # a short last wave
+    fmt = DataDesc(1, 0, 1, False, True, True)
+    s, _ = mk_store(fmt, first, first + rows - 1, cols)
+    s.set_knob(1, 0)
+    o = oracle_store(oracle, fmt, first, first + rows - 1, cols)
+    s.setAlpha(0.025, 0.0001, 1.5)
+    o.set_alpha(0.025, 0.0001, 1.5)
+    init = rng.standard_normal((rows, cols)).astype(np.float32)
+    s.load_values(init)
+    o.data[:] = init
+    for batch in range(2):
+        pushes = []
+        for b in range(W):
+            keys = np.arange(rows)
+            scale = 0.7 if case == "large" else 1e-2
+            v = (rng.standard_normal((rows, cols)) * scale).astype(np.float32)
+            if case == "large" and b == 0 and batch == 0:
+                v[10, 3], v[2000, 5] = np.nan, np.inf
+            if b == W - 1 and case == "swapped":
+                keys[[7, 1900]] = keys[[1900, 7]]
+            if b == W - 1 and case == "partial":
+                keys, v = keys[:-1], v[:-1]
+            pushes.append(encode_matrix_push(keys + first, v, 0, 1))
+        for p in pushes:
+            assert o.push(p) == 0
+        s.handlePushBatch(fmt, pushes)
+        want = "dml::k_ada_ident<" if case in ("plain", "large") else "dml::k_ada_flat<"
+        assert s.kernel_name().startswith(want), (s.kernel_name(), want)
+        assert kat.bits_equal(s.values(), o.data)
+        a, d = s.adagrad_state()
+        assert kat.bits_equal(a, o.alpha) and kat.bits_equal(d, o.delta)
+        assert s.maxDelta() == o.max_delta()
     s.close()
 
 
