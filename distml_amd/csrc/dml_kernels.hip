@@ -35,6 +35,24 @@ constexpr bool kAdaBurst = true;
 #else
 constexpr bool kAdaBurst = false;
 #endif
+// (A/B) k_ada_ident (NOXCD_IDENT) / k_flat_ident (FI_NOXCD) blocks in dispatch order instead of
+// XCD-contiguous; k_flat_ident's ring depth, vectors per lane, waves per block (FI_D, FI_J, FI_NW)
+#ifdef DML_AB_NOXCD_IDENT
+constexpr bool kIdentXcd = false;
+#else
+constexpr bool kIdentXcd = true;
+#endif
+#ifdef DML_AB_FI_NOXCD
+constexpr bool kFlatIdentXcd = false;
+#else
+constexpr bool kFlatIdentXcd = true;
+#endif
+#ifndef DML_AB_FI_J
+#define DML_AB_FI_J 8
+#endif
+#ifndef DML_AB_FI_D
+#define DML_AB_FI_D 3
+#endif
 #ifndef DML_AB_AI_NW
 #define DML_AB_AI_NW 4
 #endif
@@ -1207,7 +1225,7 @@ __global__ __launch_bounds__(NW * 64) void k_flat_ident(T* __restrict__ shard, i
     static_assert(MODE == kAdd || MODE == kPreReduce, "plain sums only");
     const int lane = threadIdx.x & 63;
     const int wid = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-    const int64_t t0 = (xcd_block() * NW + wid) * R;
+    const int64_t t0 = ((kFlatIdentXcd ? xcd_block() : (int64_t)blockIdx.x) * NW + wid) * R;
     // every wave reaches the block barrier below: a wave past the last row, or behind
     // a predecessor that needs the host first, does no work and writes nothing
     const bool live = t0 < rows && !(bt.prev && ctrl_abnormal(bt.prev));
@@ -1534,7 +1552,7 @@ __global__ __launch_bounds__(NW * 64) void k_ada_ident(float* __restrict__ shard
     constexpr int VEC = 4, NBMAX = NB, nb = NB;  // NB pushes (1..4): their loads all in flight
     const int lane = threadIdx.x & 63;
     const int wid = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-    const int64_t t0 = (xcd_block() * NW + wid) * R;
+    const int64_t t0 = ((kIdentXcd ? xcd_block() : (int64_t)blockIdx.x) * NW + wid) * R;
     float cand_v = 0.f;
     uint64_t cand_p = kNoPos;
     bool cand_ok = false;
@@ -1818,7 +1836,7 @@ static hipError_t launch_flat(void* shard, int64_t rows, int32_t cols, const Bat
 // pushes in flight, 8-wave blocks (one per CU at 2 waves per SIMD): the best of the
 // shapes scripts/ubench_flat.hip measured (config 4: 0.768 of 8 TB/s against 0.727
 // for k_reduce_flat's loop on one box).
-constexpr int kFlatIdentJ = 8;  // 16-B vectors per lane
+constexpr int kFlatIdentJ = DML_AB_FI_J;  // 16-B vectors per lane
 
 int flat_ident_rows_per_wave(int vtype, int32_t cols) {
     const int NV = cols / (vtype == kF64 ? 2 : 4);
@@ -1829,7 +1847,7 @@ template <typename T, int MODE>
 static hipError_t launch_flat_ident_t(void* shard, int64_t rows, int32_t cols, const Batch& bt, int nb,
                                       int64_t stride, int K, Ctrl* ctrl, hipStream_t st, int64_t* nblocks_out,
                                       LaunchEv ev, RowMap rm) {
-    constexpr int VEC = Elem<T>::VEC, J = kFlatIdentJ, D = 3, NW = kFlatIdentWaves;
+    constexpr int VEC = Elem<T>::VEC, J = kFlatIdentJ, D = DML_AB_FI_D, NW = kFlatIdentWaves;
     const int NV = cols / VEC;
     const int R = std::max(1, std::min(16, J * 64 / NV));
     const int64_t nblocks = ((rows + R - 1) / R + NW - 1) / NW;

@@ -9,7 +9,14 @@ for r in $(seq 1 $ROUNDS); do
   for v in $VARIANTS; do
     if [ $v = new ]; then cp /tmp/ab_new.so distml_amd/libdistml_ps.so; else cp scripts/ab/libdistml_ps_$v.so distml_amd/libdistml_ps.so; fi
     timeout -k 10 300 python bench.py $ARGS > gpurun_out/abm_${v}_$r.json 2> gpurun_out/abm_${v}_$r.err
-    python3 -c "import json,sys; d=json.load(open(sys.argv[1])); x=d[sys.argv[3]] if sys.argv[3] != 'line' else d; r=x['roofline']; print(sys.argv[2], x['ms_per_step'], r['frac'], r['avg_kernel_us'], r['kernel'])" gpurun_out/abm_${v}_$r.json "$v $r" ${LEG:-line}
+    python3 -c "
+import json, sys
+d = json.load(open(sys.argv[1]))
+for leg in sys.argv[3].split(','):
+    x = d[leg] if leg != 'line' else d
+    r = x['roofline']
+    print(sys.argv[2], leg, x['ms_per_step'], r['frac'], r['avg_kernel_us'], r['kernel'])
+" gpurun_out/abm_${v}_$r.json "$v $r" ${LEG:-line}
   done
 done
 cp /tmp/ab_new.so distml_amd/libdistml_ps.so
