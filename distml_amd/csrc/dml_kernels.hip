@@ -53,6 +53,11 @@ constexpr bool kFlatIdentXcd = true;
 #ifndef DML_AB_FI_D
 #define DML_AB_FI_D 3
 #endif
+// (A/B) k_reduce_rows DEPTH 3: minimum waves per SIMD the register allocation must allow
+#ifndef DML_AB_D3_WAVES
+#define DML_AB_D3_WAVES 1
+#endif
+constexpr int kD3Waves = DML_AB_D3_WAVES;
 #ifndef DML_AB_AI_NW
 #define DML_AB_AI_NW 4
 #endif
@@ -615,7 +620,7 @@ __device__ inline int64_t xcd_block() {
 // (same per-element add order, cutoff and negativity rules); rows narrower than
 // one vector use k_reduce.
 template <typename T, int MODE, int CPW, int RPW, bool NT, bool FULL, int DEPTH, int WPB = 4, int SNT = 0>
-__global__ __launch_bounds__(64 * WPB) void k_reduce_rows(T* __restrict__ shard, int64_t rows, int32_t cols,
+__global__ __launch_bounds__(64 * WPB, DEPTH == 3 ? kD3Waves : 1) void k_reduce_rows(T* __restrict__ shard, int64_t rows, int32_t cols,
                                                      int32_t ngroups, const Batch bt, int nb, int64_t stride, int K,
                                                      int32_t* __restrict__ slot,
                                                      const uint32_t* __restrict__ rowflag, Ctrl* __restrict__ ctrl,
@@ -793,6 +798,38 @@ __global__ __launch_bounds__(64 * WPB) void k_reduce_rows(T* __restrict__ shard,
     // record start carries the key at no extra instruction; otherwise one key load.
     const bool spec_idle = !FULL && ident != 0ull && ((cg * CPW + CPW - 1) * 64 + 63) * VEC >= cols;
     const bool spec_lane = spec_idle && lane == 63;
+    // One record vector into a row chunk, as the reference adds it (one add per element).
+    // Whole-vector rows (cols % VEC == 0, wave-uniform): no lane is ragged, so no shift
+    // select; a lane past the row's last column adds what it loaded and never stores it.
+    // kAddCheckI32: the counters after every add are OR-ed into negbits (one instruction
+    // per element); the first negative's position is found after the loop, only when
+    // some lane saw one (rare), by replaying the wave's adds from the shard (neg_first).
+    const bool aligned = FULL || cols % VEC == 0;
+    uint32_t negbits = 0;
+    auto add_vec = [&](T (&a)[VEC], const u32x4& rw, int c) {
+        T t[VEC];
+        unpack<T>(rw, t);
+        if (aligned) {
+#pragma unroll
+            for (int e = 0; e < VEC; ++e) a[e] = Elem<T>::add(a[e], t[e]);
+            if constexpr (MODE == kAddCheckI32)
+                negbits |= nv[c] > 0 ? ((uint32_t)a[0] | (uint32_t)a[1] | (uint32_t)a[2] | (uint32_t)a[3]) : 0u;
+        } else {
+            T u[VEC];
+#pragma unroll
+            for (int e = 0; e < VEC; ++e) {  // u[e] = t[e + sh] without runtime register indexing
+                u[e] = t[e];
+#pragma unroll
+                for (int k = 1; k < VEC - e; ++k) u[e] = sh[c] == k ? t[e + k] : u[e];
+            }
+#pragma unroll
+            for (int e = 0; e < VEC; ++e)
+                if (e < nv[c]) {
+                    a[e] = Elem<T>::add(a[e], u[e]);
+                    if constexpr (MODE == kAddCheckI32) negbits |= (uint32_t)a[e];
+                }
+        }
+    };
     if constexpr (DEPTH == 3) {
         // Pair-packed: the wave's (push, row) records in push order, RPW of them per
         // load group whatever push they come from. A batch whose pushes list few of
@@ -870,28 +907,7 @@ __global__ __launch_bounds__(64 * WPB) void k_reduce_rows(T* __restrict__ shard,
                 for (int r = 0; r < RPW; ++r) {
                     if (r != pr[g]) continue;  // wave-uniform: static register indices below
 #pragma unroll
-                    for (int c = 0; c < CPW; ++c) {
-                        T t[VEC], u[VEC];
-                        unpack<T>(raw[g][c], t);
-#pragma unroll
-                        for (int e = 0; e < VEC; ++e) {
-                            u[e] = t[e];
-#pragma unroll
-                            for (int k = 1; k < VEC - e; ++k) u[e] = sh[c] == k ? t[e + k] : u[e];
-                        }
-#pragma unroll
-                        for (int e = 0; e < VEC; ++e)
-                            if (e < nv[c]) {
-                                acc[r][c][e] = Elem<T>::add(acc[r][c][e], u[e]);
-                                if constexpr (MODE == kAddCheckI32)
-                                    if (acc[r][c][e] < 0) {
-                                        const uint64_t p = pos_of((uint64_t)bt.bidx[pb[g]],
-                                                                  (uint64_t)((int64_t)prr[g] * stride + voff[c] +
-                                                                             e * (int64_t)sizeof(T)));
-                                        if (p < negpos) negpos = p;
-                                    }
-                            }
-                    }
+                    for (int c = 0; c < CPW; ++c) add_vec(acc[r][c], raw[g][c], c);
                 }
             }
             if constexpr (MODE == kAdd) {
@@ -965,30 +981,36 @@ __global__ __launch_bounds__(64 * WPB) void k_reduce_rows(T* __restrict__ shard,
         for (int r = 0; r < RPW; ++r) {
             if (rr[r] < 0) continue;  // wave-uniform
 #pragma unroll
-            for (int c = 0; c < CPW; ++c) {
-                T t[VEC], u[VEC];
-                unpack<T>(raw[r][c], t);
+            for (int c = 0; c < CPW; ++c) add_vec(acc[r][c], raw[r][c], c);
+        }
+    }
+
+    if constexpr (MODE == kAddCheckI32) {
+        // neg_first: some add left a counter negative. Replay this wave's adds element by
+        // element from the shard rows (still unwritten: this wave stores them below), in
+        // push order, and take the earliest position that left a counter negative (min
+        // over positions = first in the reference's order, IntMatrixStore.java:172-176).
+        if (__ballot((int32_t)negbits < 0)) {
+            for (int r = 0; r < RPW; ++r) {
+                if (!(touched >> r & 1u)) continue;
 #pragma unroll
-                for (int e = 0; e < VEC; ++e) {  // u[e] = t[e + sh] without runtime register indexing
-                    u[e] = t[e];
-#pragma unroll
-                    for (int k = 1; k < VEC - e; ++k) u[e] = sh[c] == k ? t[e + k] : u[e];
-                }
-#pragma unroll
-                for (int e = 0; e < VEC; ++e)
-                    if (e < nv[c]) {
-                        acc[r][c][e] = Elem<T>::add(acc[r][c][e], u[e]);
-                        if constexpr (MODE == kAddCheckI32)
-                            if (acc[r][c][e] < 0) {
-                                const uint64_t p = pos_of((uint64_t)bt.bidx[b],
-                                                          (uint64_t)((int64_t)rr[r] * stride + voff[c] + e * (int64_t)sizeof(T)));
-                                if (p < negpos) negpos = p;  // min over positions = first in the reference's order
+                for (int c = 0; c < CPW; ++c)
+                    for (int e = 0; e < nv[c]; ++e) {
+                        T a = rowp[r][c0[c] + e];
+                        for (int b = 0; b < nb; ++b) {
+                            const int32_t rrb = __builtin_amdgcn_readlane(vslot[r], b);
+                            if (rrb < 0) continue;
+                            const uint64_t off = (uint64_t)((int64_t)rrb * stride + voff[c] + e * (int64_t)sizeof(T));
+                            a = Elem<T>::add(a, Elem<T>::load(bt.base[b] + off));
+                            if (a < 0) {
+                                const uint64_t p = pos_of((uint64_t)bt.bidx[b], off);
+                                if (p < negpos) negpos = p;
                             }
+                        }
                     }
             }
         }
     }
-
     if (MODE == kPreReduce) touched = live;  // every pre-reduce row is written (zeros if no push has it)
 #pragma unroll
     for (int r = 0; r < RPW; ++r) {
