@@ -53,6 +53,14 @@ constexpr bool kFlatIdentXcd = true;
 #ifndef DML_AB_FI_D
 #define DML_AB_FI_D 3
 #endif
+// (A/B) k_reduce_rows DEPTH 3 for rows of >= 4 chunks (config 5): waves per block, rows per wave
+#ifndef DML_AB_C5_WPB
+#define DML_AB_C5_WPB 2
+#endif
+#ifndef DML_AB_C5_RPW
+#define DML_AB_C5_RPW 4
+#endif
+constexpr int kC5Wpb = DML_AB_C5_WPB, kC5Rpw = DML_AB_C5_RPW;
 // (A/B) k_reduce_rows DEPTH 3: minimum waves per SIMD the register allocation must allow
 #ifndef DML_AB_D3_WAVES
 #define DML_AB_D3_WAVES 1
@@ -1795,9 +1803,9 @@ static hipError_t launch_auto(void* shard, int64_t rows, int32_t cols, const Bat
             // sooner): config 5 428 -> 400 us, 0.565 -> 0.604 of peak, measured against
             // nt loads, 1/4/8-wave blocks, CPW 1/2, RPW 2, cached stores.
             if (nchunks >= 4)
-                return launch_reduce_t<T, MODE, 3, false, 2, 1, 4, 4>(shard, rows, cols, bt, nb, stride, K, slot,
-                                                                     rowflag, ctrl, tail_cut, ada, st, nblocks_out,
-                                                                     ev, rm);
+                return launch_reduce_t<T, MODE, 3, false, kC5Wpb, 1, 4, kC5Rpw>(shard, rows, cols, bt, nb, stride, K,
+                                                                               slot, rowflag, ctrl, tail_cut, ada, st,
+                                                                               nblocks_out, ev, rm);
             if (cols % (64 * VEC * 2) == 0) return DML_LFN(1, 2, 4);
             if (nchunks >= 2) return DML_LN(3, 2, 4);
             if (cols % (64 * VEC) == 0) return DML_LFN(1, 1, 4);
