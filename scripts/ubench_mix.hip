@@ -10,6 +10,7 @@
 // loads / stores (0 default, 2 nt, 16 sc1, 18 nt sc1); PERSIST: a grid of 2048 blocks
 // walks the tiles, else one block per tile.
 #include <hip/hip_runtime.h>
+#include <hip/hip_ext.h>
 
 #include <cstdio>
 #include <cstdlib>
@@ -224,6 +225,48 @@ int main(int argc, char** argv) {
                name, nr, no, gib, best * 1e3, sum / 6 * 1e3, bytes / best / 1e6, bytes / best / 1e6 / 8000.0);
         fflush(stdout);
     };
+    if (!strcmp(filt, "boundary")) {
+        // Kernel boundary cost: 50 back-to-back launches of a 256 MiB read-only pass,
+        // plain launches against hipExtLaunchKernelGGL carrying a completion event (the
+        // store's per-chunk `applied`), and one carrying start + stop events.
+        const int64_t nb = 256LL << 20, tiles = nb / (256 * 4 * 16);
+        hipEvent_t ev[2];
+        CK(hipEventCreate(&ev[0]));
+        CK(hipEventCreate(&ev[1]));
+        hipEvent_t evd;
+        CK(hipEventCreateWithFlags(&evd, hipEventDisableTiming));
+        for (int mode = 0; mode < 4; ++mode) {
+            float best = 1e30f;
+            for (int rep = 0; rep < 5; ++rep) {
+                CK(hipEventRecord(e0));
+                for (int i = 0; i < 50; ++i) {
+                    if (mode == 0)
+                        hipLaunchKernelGGL((k_mix<1, 0, 4, 2, 0, false, false>), dim3((unsigned)tiles), dim3(256), 0, 0, a, o, tiles);
+                    else if (mode == 1)
+                        hipExtLaunchKernelGGL((k_mix<1, 0, 4, 2, 0, false, false>), dim3((unsigned)tiles), dim3(256), 0, 0,
+                                              nullptr, ev[i & 1], 0, a, o, tiles);
+                    else if (mode == 2)
+                        hipExtLaunchKernelGGL((k_mix<1, 0, 4, 2, 0, false, false>), dim3((unsigned)tiles), dim3(256), 0, 0,
+                                              ev[0], ev[1], 0, a, o, tiles);
+                    else {
+                        hipLaunchKernelGGL((k_mix<1, 0, 4, 2, 0, false, false>), dim3((unsigned)tiles), dim3(256), 0, 0, a, o, tiles);
+                        CK(hipEventRecord(evd, 0));
+                    }
+                }
+                CK(hipEventRecord(e1));
+                CK(hipEventSynchronize(e1));
+                float ms;
+                CK(hipEventElapsedTime(&ms, e0, e1));
+                if (ms < best) best = ms;
+            }
+            static const char* nm[] = {"plain launches", "ext launch + completion event", "ext launch + start/stop events",
+                                       "plain launch + hipEventRecord (no timing)"};
+            printf("{\"kernel\": \"boundary: %s\", \"launches\": 50, \"bytes_each\": %lld, \"us_per_launch\": %.2f}\n", nm[mode],
+                   (long long)nb, best * 1e3 / 50);
+            fflush(stdout);
+        }
+        return 0;
+    }
     // reads only
     run("read1 U4 nt", k_mix<1, 0, 4, 2, 0, false, false>, 1, 0, 4, false);
     run("read1 U4 default", k_mix<1, 0, 4, 0, 0, false, false>, 1, 0, 4, false);
