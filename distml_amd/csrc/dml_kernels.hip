@@ -1984,13 +1984,19 @@ static hipError_t launch_ada_ident_t(void* shard, int64_t rows, int32_t cols, in
     return hipGetLastError();
 }
 
+// rows per wave and blocks of a k_ada_ident launch
+static int ada_ident_rows_per_wave(int32_t cols) { return std::max(1, std::min(16, kAdaIdentJ * 64 / (cols / 4))); }
+static int64_t ada_ident_blocks(int64_t rows, int32_t cols) {
+    const int R = ada_ident_rows_per_wave(cols);
+    return ((rows + R - 1) / R + kAdaIdentWaves - 1) / kAdaIdentWaves;
+}
+
 hipError_t launch_ada_ident(void* shard, int64_t rows, int32_t cols, const Batch& bt, int nb, int64_t stride, int K,
                             const AdaArgs& ada, hipStream_t st, int64_t* ncand_out, LaunchEv ev) {
-    constexpr int J = kAdaIdentJ, NW = kAdaIdentWaves;
+    constexpr int NW = kAdaIdentWaves;
     if (nb <= 0 || nb > 4 || cols % 4 || (int64_t)cols * 4 >= 4096) return hipErrorInvalidValue;
-    const int NV = cols / 4;
-    const int R = std::max(1, std::min(16, J * 64 / NV));
-    const int64_t nblocks = ((rows + R - 1) / R + NW - 1) / NW;
+    const int R = ada_ident_rows_per_wave(cols);
+    const int64_t nblocks = ada_ident_blocks(rows, cols);
     if (ncand_out) *ncand_out = nblocks * NW;
     if (nblocks <= 0) return hipSuccess;
     switch (nb) {
@@ -2026,10 +2032,15 @@ bool reduce_clears_slots(int vtype, int mode, int32_t cols) {
 }
 
 int64_t reduce_blocks(int vtype, int64_t rows, int32_t cols) {
-    // AdaGrad (the only caller that needs it) always runs one row and one chunk per wave, 4 waves per block
+    // The most maxDelta candidates one AdaGrad apply writes (the candidate buffer's size):
+    // k_reduce runs one row and one chunk per wave, 4 waves per block, one candidate per
+    // block; k_ada_flat fewer; k_ada_ident one per wave of its (rounded-up) grid.
     const int VEC = vtype == kF64 ? 2 : 4;
     const int64_t nchunks = (cols + 64 * VEC - 1) / (64 * VEC);
-    return (rows * nchunks + 3) / 4;
+    int64_t n = (rows * nchunks + 3) / 4;
+    if (vtype == kF32 && cols >= 4 && cols % 4 == 0 && (int64_t)cols * 4 < 4096)
+        n = std::max<int64_t>(n, ada_ident_blocks(rows, cols) * kAdaIdentWaves);
+    return n;
 }
 
 hipError_t launch_reduce(int vtype, int mode, void* shard, int64_t rows, int32_t cols, const Batch& bt, int nb,

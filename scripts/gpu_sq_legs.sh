@@ -11,7 +11,7 @@ timeout -s KILL 240 rocprofv3 --pmc $P1 -d $O/sq1 -o run --output-format csv -- 
 timeout -s KILL 240 rocprofv3 --pmc $P2 -d $O/sq2 -o run --output-format csv -- python3 bench.py $BA > $O/sq2.log 2>&1
 timeout -s KILL 120 rocprofv3 --pmc $P1 -d $O/sqm1 -o run --output-format csv -- scripts/ubench_mix 8 "r4w2 in place U4 nt nt" > $O/sqm1.log 2>&1
 timeout -s KILL 120 rocprofv3 --pmc $P2 -d $O/sqm2 -o run --output-format csv -- scripts/ubench_mix 8 "r4w2 in place U4 nt nt" > $O/sqm2.log 2>&1
-M="k_ada_flat k_flat_ident k_reduce_rows<int k_mix"
+M="k_ada_flat k_ada_ident k_flat_ident k_reduce_rows<int k_mix"
 python3 scripts/pmc_reduce.py $O/sq_legs.json $O/sq1 $O/sq2 --match $M > /dev/null
 python3 scripts/pmc_reduce.py $O/sq_mix.json $O/sqm1 $O/sqm2 --match $M > /dev/null
 rm -rf $O/sq1 $O/sq2 $O/sqm1 $O/sqm2

@@ -1992,9 +1992,9 @@ def test_adagrad_flat_exact(oracle, case, W, cols):
     s.close()
 
 
-@pytest.mark.parametrize("cols", [200, 48])
+@pytest.mark.parametrize("cols", [200, 256, 48])
 @pytest.mark.parametrize("W", [1, 2, 3, 4])
-@pytest.mark.parametrize("case", ["plain", "large", "swapped", "partial"])
+@pytest.mark.parametrize("case", ["plain", "large", "swapped", "partial", "tiny"])
 def test_adagrad_ident_exact(oracle, case, W, cols):
     """k_ada_ident (AdaGrad chunks of full-range pushes whose records are rows in order,
     every key checked before the launch) bit-exact against the oracle:
@@ -2003,10 +2003,11 @@ def test_adagrad_ident_exact(oracle, case, W, cols):
     (alpha written) plus a NaN and an Inf element; `swapped`: the last push has two
     records swapped (not identity: k_ada_flat takes the chunk); `partial`: the last push
     omits the last row (not full-range: the key index, k_ada_flat). Two batches, so the
-    second starts from the first's delta and maxDelta."""
+    second starts from the first's delta and maxDelta. `tiny`: 5 rows, a grid rounded up
+    past the rows (more candidate slots than k_reduce's count at 256 columns)."""
     from distml_amd import DataDesc, encode_matrix_push
     rng = np.random.default_rng(100 * W + cols + len(case))
-    first, rows = 50, 2999  # a short last wave
+    first, rows = 50, (5 if case == "tiny" else 2999)  # a short last wave
     fmt = DataDesc(1, 0, 1, False, True, True)
     s, _ = mk_store(fmt, first, first + rows - 1, cols)
     s.set_knob(1, 0)
@@ -2024,6 +2025,8 @@ def test_adagrad_ident_exact(oracle, case, W, cols):
             v = (rng.standard_normal((rows, cols)) * scale).astype(np.float32)
             if case == "large" and b == 0 and batch == 0:
                 v[10, 3], v[2000, 5] = np.nan, np.inf
+            if case == "tiny":
+                v *= 100.0  # delta past 1: alpha written
             if b == W - 1 and case == "swapped":
                 keys[[7, 1900]] = keys[[1900, 7]]
             if b == W - 1 and case == "partial":
@@ -2032,7 +2035,7 @@ def test_adagrad_ident_exact(oracle, case, W, cols):
         for p in pushes:
             assert o.push(p) == 0
         s.handlePushBatch(fmt, pushes)
-        want = "dml::k_ada_ident<" if case in ("plain", "large") else "dml::k_ada_flat<"
+        want = "dml::k_ada_ident<" if case in ("plain", "large", "tiny") else "dml::k_ada_flat<"
         assert s.kernel_name().startswith(want), (s.kernel_name(), want)
         assert kat.bits_equal(s.values(), o.data)
         a, d = s.adagrad_state()
