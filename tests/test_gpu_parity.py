@@ -274,6 +274,48 @@ def test_batch_error_state_matches_sequential(oracle, kind):
         s.close()
 
 
+@pytest.mark.parametrize("cols", [48, 37, 1000, 1024, 2048, 3])
+def test_int32_negative_widths_exact(oracle, cols):
+    """IntMatrixStore's negativity check (IntMatrixStore.java:172-176) at every
+    k_reduce_rows shape: whole-vector rows (48, 1000: the config-5 width, 1024: whole
+    4-KiB rows, 2048: two waves per row), a ragged width (37) and rows narrower than one
+    vector (3). The reduce ORs the counters after each add and replays a wave's adds from
+    the shard only when one went negative (neg_first): the error, its (key, col) and the
+    rolled-back store must equal the oracle's, for a negative reached mid-batch by a later
+    push of a row two pushes list, and a second one further on."""
+    from distml_amd import DataDesc, DistMLException, encode_matrix_push
+    rng = np.random.default_rng(cols)
+    first, rows = 0, 96
+    fmt = DataDesc(1, 0, 0)
+    pushes = rand_matrix_pushes(rng, first, rows, cols, 0, 0, 6, 0.7)
+    c = cols // 2
+    dip = np.zeros((1, cols), np.int32)
+    dip[0, c] = -7                      # row 9 is 5..8: negative after this add ...
+    lift = np.zeros((1, cols), np.int32)
+    lift[0, c] = 100                    # ... and positive again after the next push's
+    pushes[2] = pushes[2] + encode_matrix_push([9], dip, 0, 0)
+    pushes[3] = encode_matrix_push([9], lift, 0, 0) + pushes[3]
+    late = np.zeros((1, cols), np.int32)
+    late[0, cols - 1] = -1000
+    pushes[4] = pushes[4] + encode_matrix_push([40], late, 0, 0)
+    init = rng.integers(5, 9, size=(rows, cols)).astype(np.int32)
+    o = oracle_store(oracle, fmt, first, rows - 1, cols)
+    o.data[:] = init
+    rc = 0
+    for p in pushes:
+        rc = o.push(p)
+        if rc:
+            break
+    assert rc != 0
+    s, _ = mk_store(fmt, first, rows - 1, cols)
+    s.load_values(init)
+    with pytest.raises(DistMLException) as ei:
+        s.handlePushBatch(fmt, pushes)
+    assert (ei.value.code, ei.value.key, ei.value.col) == o.error()
+    assert kat.bits_equal(s.values(), o.data)
+    s.close()
+
+
 @pytest.mark.parametrize("middle", ["normal", "dup", "key", "neg"])
 def test_pipelined_batches(oracle, middle):
     """Several device batches in flight (no flush between them): a repeated row in
