@@ -60,7 +60,10 @@ constexpr bool kFlatIdentXcd = true;
 #ifndef DML_AB_C5_RPW
 #define DML_AB_C5_RPW 4
 #endif
-constexpr int kC5Wpb = DML_AB_C5_WPB, kC5Rpw = DML_AB_C5_RPW;
+#ifndef DML_AB_C5_BPC
+#define DML_AB_C5_BPC 0
+#endif
+constexpr int kC5Wpb = DML_AB_C5_WPB, kC5Rpw = DML_AB_C5_RPW, kC5Bpc = DML_AB_C5_BPC;  // BPC: blocks per CU cap
 // (A/B) k_reduce_rows DEPTH 3: minimum waves per SIMD the register allocation must allow
 #ifndef DML_AB_D3_WAVES
 #define DML_AB_D3_WAVES 1
@@ -1805,7 +1808,7 @@ static hipError_t launch_auto(void* shard, int64_t rows, int32_t cols, const Bat
             if (nchunks >= 4)
                 return launch_reduce_t<T, MODE, 3, false, kC5Wpb, 1, 4, kC5Rpw>(shard, rows, cols, bt, nb, stride, K,
                                                                                slot, rowflag, ctrl, tail_cut, ada, st,
-                                                                               nblocks_out, ev, rm);
+                                                                               nblocks_out, ev, rm, kC5Bpc);
             if (cols % (64 * VEC * 2) == 0) return DML_LFN(1, 2, 4);
             if (nchunks >= 2) return DML_LN(3, 2, 4);
             if (cols % (64 * VEC) == 0) return DML_LFN(1, 1, 4);
