@@ -70,7 +70,7 @@ constexpr int kC5Wpb = DML_AB_C5_WPB, kC5Rpw = DML_AB_C5_RPW, kC5Bpc = DML_AB_C5
 #endif
 constexpr int kD3Waves = DML_AB_D3_WAVES;
 #ifndef DML_AB_AI_NW
-#define DML_AB_AI_NW 4
+#define DML_AB_AI_NW 2
 #endif
 #ifndef DML_AB_AI_BPC
 #define DML_AB_AI_BPC 0
@@ -1969,7 +1969,13 @@ static hipError_t launch_ada_flat_t(void* shard, int64_t rows, int32_t cols, con
 // checked the index's Ctrl, as for k_flat_ident), at most 4 pushes. One maxDelta
 // candidate per wave: *ncand_out = the waves launched (<= reduce_blocks(), the
 // candidate buffer's size).
-constexpr int kAdaIdentJ = 4, kAdaIdentWaves = DML_AB_AI_NW;
+// 8 vectors per lane (10 rows of 800 B per wave), 2-wave blocks: the k_ada_ident shapes
+// measured on one box (J 2/4/8 x 1/2/4/8 waves): J 8 at 1-2 waves and J 2 at 2-4 waves
+// 8.20-8.43 ms, J 4 at any block size 8.69-8.81 ms (its 5-row waves split 64-B sectors)
+#ifndef DML_AB_AI_J
+#define DML_AB_AI_J 8
+#endif
+constexpr int kAdaIdentJ = DML_AB_AI_J, kAdaIdentWaves = DML_AB_AI_NW;
 
 template <int NB>
 static hipError_t launch_ada_ident_t(void* shard, int64_t rows, int32_t cols, int R, int64_t nblocks, const Batch& bt,
@@ -1987,8 +1993,16 @@ static hipError_t launch_ada_ident_t(void* shard, int64_t rows, int32_t cols, in
     return hipGetLastError();
 }
 
-// rows per wave and blocks of a k_ada_ident launch
-static int ada_ident_rows_per_wave(int32_t cols) { return std::max(1, std::min(16, kAdaIdentJ * 64 / (cols / 4))); }
+// Rows per wave and blocks of a k_ada_ident launch. A wave's rows span a whole number of
+// 64-B sectors where any count up to its vectors allows: its non-temporal data / delta
+// stores then never share a sector with a neighbouring wave's (config-4 AdaGrad, 800-B
+// rows: 5 rows = 4 000 B ran 8.69-8.80 ms, 2 or 10 rows 8.20-8.43 ms, one box, 2 rounds).
+static int ada_ident_rows_per_wave(int32_t cols) {
+    const int rmax = std::max(1, std::min(16, kAdaIdentJ * 64 / (cols / 4)));
+    for (int r = rmax; r > 1; --r)
+        if ((int64_t)r * cols * 4 % 64 == 0) return r;
+    return rmax;
+}
 static int64_t ada_ident_blocks(int64_t rows, int32_t cols) {
     const int R = ada_ident_rows_per_wave(cols);
     return ((rows + R - 1) / R + kAdaIdentWaves - 1) / kAdaIdentWaves;
