@@ -4,48 +4,110 @@ LogisticRegression.scala:290-291 casts its store to DoubleArrayStore and
 Word2Vec.scala:814-817 to FloatMatrixStoreAdaGrad, then iterate them. So a GPU
 store must BE the concrete class: integration/jni/Gpu<Store>.java extends <Store>
 for all seven stores of DataStore.createStore (DataStore.java:50-92), overrides every
-public method the parent declares (names from tests/golden/ref_store_methods.json;
-indexOf / keyOf only read localRows, which init() sets, and stay inherited), and
-fills the parent's localData (and AdaGrad's alpha / delta) from the device in
-snapshot(), which iter() calls. GpuStores.createStore mirrors the dispatch. No JDK
-exists here, so these are source checks; the snapshot entry point itself runs on the
-mock JVM on the GPU (tests/test_jni_shim.py::test_mock_jvm_snapshot_on_gpu).
+public method the parent declares with the parent's exact signature (VERDICT r5 #6:
+modifiers, return type, parameter types and `throws` from
+tests/golden/ref_store_methods.json; indexOf / keyOf only read localRows, which init()
+sets, and stay inherited), and fills the parent's localData (and AdaGrad's alpha /
+delta) from the device in snapshot(), which iter() calls. GpuStores.createStore
+mirrors the dispatch. No JDK exists here, so these are source checks (a wrong
+parameter type would compile as an overload and leave the parent's heap body in
+place; an added checked exception would not compile); the snapshot entry point
+itself runs on the mock JVM on the GPU (tests/test_jni_shim.py::test_mock_jvm_snapshot_on_gpu).
 """
 import json
 import os
 import re
+import sys
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 JNI = os.path.join(ROOT, "integration", "jni")
 FIX = os.path.join(ROOT, "tests", "golden", "ref_store_methods.json")
 INHERITED = {"indexOf", "keyOf"}  # read localRows only (set by init), no localData
+sys.path.insert(0, os.path.join(ROOT, "tests", "golden"))
+import make_ref_store_methods  # noqa: E402  (the signature parser; reads no reference file itself)
 
 
 def _src(name):
     return open(os.path.join(JNI, name + ".java")).read()
 
 
-def _declared(src):
-    return set(re.findall(r"^    public (?!class\b|static\b)(?:[\w\[\]<>.]+ )?(\w+)\(", src, re.M))
+def _key(s):
+    return s["name"], tuple(s["params"])
+
+
+def check_overrides(child: str, parent_sigs, where: str):
+    """Every public non-static parent method (less INHERITED) is declared in the child
+    with the same parameter types and return type, public, throwing no checked
+    exception the parent's does not (JLS 8.4.8.3); no child method reuses a parent
+    method's name with other parameter types (an overload beside the parent's body)."""
+    mine = {_key(s): s for s in make_ref_store_methods.signatures(child)}
+    assert "class Iter" not in child, where  # iter() returns the parent's member class
+    names = {s["name"] for s in parent_sigs}
+    for p in parent_sigs:
+        if "static" in p["mods"] or p["name"] in INHERITED:
+            continue
+        c = mine.get(_key(p))
+        assert c is not None, (where, "missing override", p)
+        assert c["ret"] == p["ret"], (where, p["name"], c["ret"], p["ret"])
+        assert c["mods"][0] == "public" and "static" not in c["mods"] and "abstract" not in c["mods"], (where, c)
+        assert set(c["throws"]) <= set(p["throws"]), (where, p["name"], c["throws"], p["throws"])
+    keys = {_key(p) for p in parent_sigs}
+    for k, c in mine.items():
+        if c["name"] in names:
+            assert k in keys, (where, "overload, not an override", c)
 
 
 def test_store_methods_fixture_current():
     if not os.path.isdir("/root/reference"):
         return
-    import sys
-    sys.path.insert(0, os.path.join(ROOT, "tests", "golden"))
-    import make_ref_store_methods
     assert make_ref_store_methods.methods() == json.load(open(FIX))
+
+
+def test_fixture_holds_full_signatures():
+    ref = json.load(open(FIX))
+    assert sorted(ref) == sorted(["DataStore", "DoubleArrayStore", "DoubleMatrixStore", "FloatArrayStore",
+                                  "FloatMatrixStore", "FloatMatrixStoreAdaGrad", "IntArrayStore", "IntMatrixStore"])
+    sync = [s for s in ref["DataStore"] if s["name"] == "syncTo"]
+    assert sync == [{"mods": ["public", "abstract"], "ret": "void", "name": "syncTo",
+                     "params": ["DataOutputStream", "int", "int"], "throws": ["IOException"]}]
+    it = [s for s in ref["FloatMatrixStoreAdaGrad"] if s["name"] == "iter"]
+    assert it and it[0]["ret"] == "Iter" and it[0]["params"] == []
+
+
+def test_parser_catches_wrong_overrides():
+    """The checker itself: an overload (wrong parameter type), a wrong return type and
+    an added checked exception are each reported."""
+    parent = make_ref_store_methods.signatures(
+        "    public void init(KeyCollection keys, int cols) {\n"
+        "    public byte[] handleFetch(DataDesc format, KeyCollection rows) {\n"
+        "    public void writeAll(DataOutputStream os) throws IOException {\n")
+    good = ("    public void init(KeyCollection keys, int cols) { }\n"
+            "    public byte[] handleFetch(DataDesc format, KeyCollection rows) { return null; }\n"
+            "    public void writeAll(DataOutputStream os) throws IOException { }\n")
+    check_overrides(good, parent, "good")
+    for bad in (good.replace("int cols", "long cols"), good.replace("public byte[] handleFetch", "public Iter handleFetch"),
+                good.replace("throws IOException { }", "throws IOException, InterruptedException { }")):
+        try:
+            check_overrides(bad, parent, "bad")
+        except AssertionError:
+            continue
+        raise AssertionError("not caught: " + bad)
 
 
 def test_every_store_has_a_gpu_subclass_overriding_its_methods():
     ref = json.load(open(FIX))
-    assert len(ref) == 7
-    for parent, methods in ref.items():
+    base = ref["DataStore"]
+    for parent, sigs in ref.items():
+        if parent == "DataStore":
+            continue
         src = _src("Gpu" + parent)
         assert re.search(rf"public class Gpu{parent} extends {parent} \{{", src), parent
-        missing = set(methods) - INHERITED - _declared(src)
-        assert not missing, (parent, missing)
+        check_overrides(src, sigs, "Gpu" + parent)
+        # DataStore's own no-op rand / zero / set, where the child overrides them
+        own = {_key(s) for s in sigs}
+        mine = {_key(s) for s in make_ref_store_methods.signatures(src)}
+        check_overrides(src, [s for s in base if _key(s) not in own and _key(s) in mine], "Gpu" + parent + "/DataStore")
+        methods = {s["name"] for s in sigs}
         # the heap arrays are never allocated at init: only snapshot() fills them
         init = src[src.index("public void init("):]
         init = init[:init.index("\n    }\n")]
@@ -63,10 +125,19 @@ def test_every_store_has_a_gpu_subclass_overriding_its_methods():
             assert "gpu.maxDelta(" in push and '"max delta: " + maxDeltaRow + ", " + maxDeltaCol + ", " + maxDelta' in push
 
 
+def test_gpu_data_store_implements_data_store():
+    """GpuDataStore extends DataStore directly: every abstract method implemented with
+    DataStore's signature, and the no-op rand / zero / set overridden with theirs."""
+    base = json.load(open(FIX))["DataStore"]
+    src = _src("GpuDataStore")
+    assert re.search(r"public class GpuDataStore extends DataStore \{", src)
+    check_overrides(src, base, "GpuDataStore")
+
+
 def test_factory_mirrors_create_store():
     src = _src("GpuStores")
     made = re.findall(r"(Gpu\w+Store\w*) store = new \1\(format, device\);", src)
-    assert sorted(made) == sorted("Gpu" + p for p in json.load(open(FIX))), made
+    assert sorted(made) == sorted("Gpu" + p for p in json.load(open(FIX)) if p != "DataStore"), made
     assert "throw new IllegalArgumentException(\"Unrecognized matrix type: \"" in src
 
 
