@@ -54,6 +54,7 @@ SIGNATURES = {
     "dml_store_error_state": (C.c_int, [_vp, _P(_i64), _P(_i32)]),
     "dml_store_clear_error": (None, [_vp]),
     "dml_store_shape": (C.c_int, [_vp, _P(_i64), _P(_i32)]),
+    "dml_store_value_type": (C.c_int, [_vp, _P(_i32), _P(_i32)]),
     "dml_store_read_dense": (C.c_int, [_vp, _vp, _i64]),
     "dml_store_write_dense": (C.c_int, [_vp, _vp, _i64]),
     "dml_store_device_ptr": (C.c_int, [_vp, _P(_vp)]),

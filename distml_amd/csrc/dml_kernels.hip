@@ -1001,24 +1001,33 @@ __global__ __launch_bounds__(64 * WPB, DEPTH == 3 ? kD3Waves : 1) void k_reduce_
         // element from the shard rows (still unwritten: this wave stores them below), in
         // push order, and take the earliest position that left a counter negative (min
         // over positions = first in the reference's order, IntMatrixStore.java:172-176).
+        // The push loop is outermost and wave-uniform, so each push's slot of row r is read
+        // once, with every lane active; a lane's elements keep their running
+        // sums in registers, so the adds per element stay in push order.
         if (__ballot((int32_t)negbits < 0)) {
             for (int r = 0; r < RPW; ++r) {
                 if (!(touched >> r & 1u)) continue;
+                T a[CPW][VEC];
 #pragma unroll
                 for (int c = 0; c < CPW; ++c)
-                    for (int e = 0; e < nv[c]; ++e) {
-                        T a = rowp[r][c0[c] + e];
-                        for (int b = 0; b < nb; ++b) {
-                            const int32_t rrb = __builtin_amdgcn_readlane(vslot[r], b);
-                            if (rrb < 0) continue;
+#pragma unroll
+                    for (int e = 0; e < VEC; ++e) a[c][e] = e < nv[c] ? rowp[r][c0[c] + e] : T(0);
+                for (int b = 0; b < nb; ++b) {
+                    const int32_t rrb = __builtin_amdgcn_readlane(vslot[r], b);
+                    if (rrb < 0) continue;  // wave-uniform
+#pragma unroll
+                    for (int c = 0; c < CPW; ++c)
+#pragma unroll
+                        for (int e = 0; e < VEC; ++e) {
+                            if (e >= nv[c]) continue;
                             const uint64_t off = (uint64_t)((int64_t)rrb * stride + voff[c] + e * (int64_t)sizeof(T));
-                            a = Elem<T>::add(a, Elem<T>::load(bt.base[b] + off));
-                            if (a < 0) {
+                            a[c][e] = Elem<T>::add(a[c][e], Elem<T>::load(bt.base[b] + off));
+                            if (a[c][e] < 0) {
                                 const uint64_t p = pos_of((uint64_t)bt.bidx[b], off);
                                 if (p < negpos) negpos = p;
                             }
                         }
-                    }
+                }
             }
         }
     }

@@ -1333,6 +1333,13 @@ int dml_store_shape(dml_store* s, int64_t* rows, int32_t* cols) {
     return DML_OK;
 }
 
+int dml_store_value_type(dml_store* s, int32_t* value_type, int32_t* adagrad) {
+    if (int rc = check_store(s)) return rc;
+    if (value_type) *value_type = s->desc.value_type;
+    if (adagrad) *adagrad = s->adagrad ? 1 : 0;
+    return DML_OK;
+}
+
 int dml_store_read_dense(dml_store* s, void* host_dst, int64_t bytes) {
     if (int rc = check_store(s)) return rc;
     std::lock_guard<std::mutex> lk(s->mu);

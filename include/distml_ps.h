@@ -160,6 +160,10 @@ void dml_store_clear_error(dml_store* s);
 /* KeyRange size (KeyRange.java:92-94) and rowSize() (FloatMatrixStore.java:24-26;
  * 1 for arrays). */
 int dml_store_shape(dml_store* s, int64_t* rows, int32_t* cols);
+/* The store's DataDesc value type (DML_ELEMENT_TYPE_*) and whether it is an AdaGrad
+ * store (DataDesc.java:21-42): the element type its rows hold for dml_store_read_rows
+ * (the JNI snapshot checks the Java array it fills against it). */
+int dml_store_value_type(dml_store* s, int32_t* value_type, int32_t* adagrad);
 
 /* Raw row-major shard values (rows*cols elements of the store's value type)
  * to/from host memory; test/oracle access and initial load. */

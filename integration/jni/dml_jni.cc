@@ -230,6 +230,15 @@ JNIEXPORT void JNICALL FN(nativeSnapshot)(JNIEnv* env, jclass, jlong h, jint whi
     int64_t rows = 0;
     int32_t cols = 0;
     if (int rc = dml_store_shape(H(h), &rows, &cols)) { throw_for(env, rc); return; }
+    // the array must hold the store's own element type (alpha / delta: float), or the
+    // rows would be reinterpreted
+    int32_t vt = -1, ada = 0;
+    if (int rc = dml_store_value_type(H(h), &vt, &ada)) { throw_for(env, rc); return; }
+    if ((which == 0 && elem != vt) || ((which == 1 || which == 2) && (elem != DML_ELEMENT_TYPE_FLOAT || !ada))) {
+        env->ThrowNew(env->FindClass("java/lang/IllegalArgumentException"),
+                      "snapshot element type does not match the store");
+        return;
+    }
     const int64_t esz = elem == DML_ELEMENT_TYPE_DOUBLE ? 8 : 4;
     const int64_t per_row = dims == 2 ? cols : 1;  // elements per local row
     if ((dims != 1 && dims != 2) || (elem != DML_ELEMENT_TYPE_INT && elem != DML_ELEMENT_TYPE_FLOAT &&

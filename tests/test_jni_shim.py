@@ -267,8 +267,8 @@ def test_mock_jvm_snapshot_on_gpu(oracle):
     localData (and alpha / delta, which the AdaGrad Iter prints) with nativeSnapshot,
     in bounded row chunks; the AdaGrad push reports maxDelta through nativeMaxDelta
     (FloatMatrixStoreAdaGrad.java:246). Keys and values bit-exact against the oracle.
-    Also an IntMatrixStore snapshot (int[][]), a wrong-shape array
-    (IllegalArgumentException) and a fetch past the Java array limit (OutOfMemoryError)."""
+    Also an IntMatrixStore snapshot (int[][]), a wrong-shape array and arrays of
+    another element type than the store's (IllegalArgumentException), and a fetch past the Java array limit (OutOfMemoryError)."""
     import numpy as np
     from distml_amd import encode_array_push, encode_matrix_push
     jvm = MockJVM()
@@ -295,6 +295,11 @@ def test_mock_jvm_snapshot_on_gpu(oracle):
     bad = jvm.prim("D", n - 1)
     _, exc = jvm.call("nativeSnapshot", h, 0, 3, 1, bad)
     assert exc and exc[0] == "java/lang/IllegalArgumentException"
+    # an array of another element type than the store's, and the AdaGrad
+    # side arrays on a store without them: refused, nothing written
+    for which, elem in ((0, 1), (0, 0), (1, 1), (2, 1)):
+        _, exc = jvm.call("nativeSnapshot", h, which, elem, 1, jvm.prim("F" if elem == 1 else "I", n))
+        assert exc and exc[0] == "java/lang/IllegalArgumentException", (which, elem, exc)
     jvm.call("nativeDestroy", h)
 
     # FloatMatrixStoreAdaGrad shard (Word2Vec syn0): rows 0..2999 x 100, two pushes
@@ -319,6 +324,10 @@ def test_mock_jvm_snapshot_on_gpu(oracle):
         assert exc is None, exc
         assert jvm.read_matrix(m, np.float32).tobytes() == np.ascontiguousarray(want).tobytes(), which
         jvm.L.mock_free(m)
+    m = jvm.matrix("D", rows, cols)  # alpha / delta are float, whatever array is passed
+    _, exc = jvm.call("nativeSnapshot", h, 1, 3, 2, m)
+    assert exc and exc[0] == "java/lang/IllegalArgumentException", exc
+    jvm.L.mock_free(m)
     jvm.call("nativeDestroy", h)
 
     # IntMatrixStore: int[][], and rows large enough to take several 16 MiB chunks
