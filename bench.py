@@ -65,7 +65,9 @@ HBM_PEAK_GBS = 8000.0                    # MI355X_MICROARCH.md: HBM3E 8.0 TB/s (
 
 C4_ROWS, C4_COLS = 10_000_000, 200       # Word2Vec rows (BASELINE config 4)
 C5_ROWS, C5_COLS, C5_W, C5_NNZ = 1_000_000, 1000, 32, 65536  # LDA word-topic counts (config 5)
+C5_TOPICS = 1000                         # LDA doc-topic totals (IntArrayStore, K topics)
 SHUFFLE_ORDERS = 64                      # seeded push orders of the headline's arrival-order sub-line
+RS_CHANNELS = 128                        # RCCL channels (CTAs) per collective
 
 
 # ---------------------------------------------------------------- HBM footprint
@@ -516,6 +518,7 @@ def headline(ctx: Ctx, L, args, out_line: dict):
         "config": {"workload": "config2: dense fp32 reduce, 32 device-resident pushes x 64 MiB "
                                "([int32 key][1024 x f32] x 16384) -> 16384x1024 fp32 model per GPU",
                    "pushes_per_gpu": W, "push_bytes": BUCKET, "model_rows": ROWS, "cols": COLS,
+                   "rccl_channels": int(os.environ.get("NCCL_MAX_NCHANNELS", "0")) if sharded else None,
                    "parallelism": ("single shard" if not sharded else f"linearSplit({world}) + RCCL reduce-scatter"
                                    + (f" (DIAGNOSTIC: one rank's ring reduce-scatter footprint at {args.emulate_rs} "
                                       f"ranks emulated on {args.emulate_channels} blocks, pieces {args.pieces}, "
@@ -688,7 +691,7 @@ def stream_peaks(L, torch, nbytes: int = 1 << 31, reps: int = 5):
 
 
 # ---------------------------------------------------------------- config 3 (N=1)
-def sparse_leg(ctx: Ctx, L, steps: int, cpu: bool):
+def sparse_leg(ctx: Ctx, L, steps: int, cpu: bool, cu_split: int = 0):
     """Config 3 (reported beside the headline): 1e9-dim fp32 FloatArrayStore shard
     (4 GB), 32 device-resident pushes x 1e6 unique keys ([int64 key][f32] = 12 B),
     ordered per-push scatter-add. Algorithmic bytes per step = 32 x 12e6 + 2 x 4 x 32e6."""
@@ -700,6 +703,8 @@ def sparse_leg(ctx: Ctx, L, steps: int, cpu: bool):
     # the shard, the pushes, and three partition workspaces (~40 B per record of a chunk)
     hbm_check(torch, "sparse", {"shard": 4 * dim, "pushes": w * nnz * 12, "workspaces": 3 * 40 * w * nnz})
     store = DataStore(fmt, KeyRange(0, dim - 1), device=ctx.local)
+    if cu_split:  # the partition's stream on part of the CUs, the leaf's on the rest
+        store.set_knob(2, cu_split)
     bufs = []
     st = torch.cuda.current_stream().cuda_stream
     for b in range(w):
@@ -858,6 +863,14 @@ def leg_config4(ctx: Ctx, L, args) -> dict:
                            "unit": "GB/s", "frac": round(algo / k_s / 1e9 / HBM_PEAK_GBS, 4),
                            **traffic_for("leg4", kn), "kernel": kn,
                            "avg_kernel_us": round(k_s * 1e6, 1), "launches": k_n}
+        if asc:
+            # the plain stream of the same bytes over the same allocations (dml_diag_dense_floor:
+            # no key checks; out of place like the speculative chunk): the live ceiling
+            fl, oop = dense_floor(L, store, ptrs, lens, st)
+            out["roofline"].update({"measured_stream_floor_us": round(fl * 1e3, 1),
+                                    "measured_stream_floor_frac": round(algo / (fl * 1e-3) / 1e9 / HBM_PEAK_GBS, 4),
+                                    "frac_of_measured_floor": round(fl * 1e-3 / k_s, 3),
+                                    "floor_layout": "out of place" if oop else "in place"})
     elif pre_n:
         out["roofline"] = prereduce_roofline(L, ctx, args.pieces, pre_ms, pre_n,
                                              w * rows * rec + world * group.step_rows * cols * 4, "config 4")
@@ -960,6 +973,13 @@ def leg_config4_ada(ctx: Ctx, L, args) -> dict:
                            "unit": "GB/s", "frac": round(owner / k_s / 1e9 / HBM_PEAK_GBS, 4),
                            **tr, "kernel": kn, "rank": rank,
                            "avg_kernel_us": round(k_s * 1e6, 1), "launches": k_n}
+        if world == 1 and not moments:
+            # AdaGrad's data / delta stream with the same pushes, plain (dml_diag_dense_floor,
+            # in place, no maxDelta / alpha bookkeeping): the live 4-read / 2-write ceiling
+            fl, _ = dense_floor(L, store, ptrs, lens, torch.cuda.current_stream().cuda_stream)
+            out["roofline"].update({"measured_stream_floor_us": round(fl * 1e3, 1),
+                                    "measured_stream_floor_frac": round(owner / (fl * 1e-3) / 1e9 / HBM_PEAK_GBS, 4),
+                                    "frac_of_measured_floor": round(fl * 1e-3 / k_s, 3)})
     group.close()
     del bufs, ptrs
     torch.cuda.synchronize()
@@ -1003,43 +1023,83 @@ def leg_config5(ctx: Ctx, L, args) -> dict:
         neg.append(n.view(torch.uint8).view(-1))
     torch.cuda.synchronize()
     sets = [DeviceBatch([b.data_ptr() for b in s], [b.numel() for b in s]) for s in (pos, neg)]
+    # the doc-topic totals (LightLDA.scala:224-239: dtm.push(dt) beside wtm.push(wt)): an
+    # IntArrayStore of the K = 1000 topics (IntArrayWithIntKey, [int32 key][int32] records),
+    # linearSplit over the ranks like the word-topic rows; every worker's push lists all
+    # its topics (a HashMap<Int> of small keys: ascending), applied with the check after
+    # every add (IntArrayStore.java:97-113); alternating with the negations as above
+    afmt = DataDesc(DataDesc.DATA_TYPE_ARRAY, DataDesc.KEY_TYPE_INT, DataDesc.ELEMENT_TYPE_INT)
+    ash = KeyRange(0, C5_TOPICS - 1).linearSplit(world)[rank]
+    A = ash.size()
+    astore = DataStore(afmt, ash, device=ctx.local)
+    astore.synth_fill(12)
+    apos, aneg = [], []
+    for b in range(C5_W):
+        t = torch.empty(A * 8, dtype=torch.uint8, device="cuda")
+        assert L.dml_synth_sparse_bucket(t.data_ptr(), C.byref(afmt.to_c()), ash.firstKey, A, A, 4100 + b, 1, 0,
+                                         C.c_void_p(st)) == 0
+        apos.append(t)
+        n = t.clone().view(torch.int32).view(A, 2)
+        n[:, 1] = -n[:, 1]
+        aneg.append(n.view(torch.uint8).view(-1))
+    torch.cuda.synchronize()
+    asets = [DeviceBatch([b.data_ptr() for b in s], [b.numel() for b in s]) for s in (apos, aneg)]
     k = [0]
 
     def step():
         store.pushDevice(sets[k[0] & 1])
+        astore.pushDevice(asets[k[0] & 1])
         k[0] += 1
+
+    def finish():
+        store.flush()
+        astore.flush()
 
     store.set_timing(True)
     for _ in range(args.c5_warmup):
         step()
-    store.flush()
+    finish()
     store.kernel_time(reset=True)
     steps = args.c5_steps + (args.c5_steps & 1)  # even: the counts return to their start
-    el = timed_steps(ctx, step, store.flush, steps, 0)
+    el = timed_steps(ctx, step, finish, steps, 0)
     k_ms, k_n = store.kernel_time(reset=True)
     store.set_timing(False)
     assert store.error_state()[0] == 0, store.error_state()
+    assert astore.error_state()[0] == 0, astore.error_state()
+    astore.close()
     touched = int(round(S * (1 - (1 - nrec / S) ** C5_W)))
-    algo = C5_W * nrec * rec + 2 * 4 * cols * touched
+    # word-topic rows + doc-topic totals (each push byte once, the touched entries read and written once)
+    algo_rows = C5_W * nrec * rec + 2 * 4 * cols * touched
+    algo = algo_rows + C5_W * A * 8 + 2 * 4 * A
     algo_all = algo
     if world > 1:
         t = torch.tensor([float(algo)], dtype=torch.float64, device=ctx.coll_device())
         ctx.dist.all_reduce(t)
         algo_all = float(t.item())
     out = {"workload": f"config5: LDA IntMatrixStore {C5_ROWS}x{cols} int32 (negativity check), {C5_W} pushes x "
-                       f"{C5_NNZ} distinct rows split per shard; this rank: shard of {S} rows, {nrec} records per push",
+                       f"{C5_NNZ} distinct rows split per shard, plus the IntArrayStore doc-topic totals ({C5_TOPICS} "
+                       f"topics, {C5_W} pushes of every topic); this rank: shard of {S} rows, {nrec} records per push, "
+                       f"{A} topics",
            "value": round(algo_all * steps / el / 2**30, 2), "unit": "GiB/s", "n_gpus": world,
            "pushes": C5_W, "steps": steps, "ms_per_step": round(el / steps * 1e3, 3), "scaling": "strong",
            "dtype": "i32", "parallelism": "single shard" if world == 1 else f"linearSplit({world}), client-split pushes",
            "algorithmic_bytes_per_step_per_gpu": algo, "algorithmic_bytes_per_step": int(algo_all)}
     if k_n:
+        # the word-topic reduce is the dominant kernel (the doc-topic totals' partition and
+        # leaf, 256 KB per step, run beside it on the array store's streams)
         k_s = k_ms / k_n / 1e3
         kn = store.kernel_name()
         tr = traffic_for("leg5", kn) if world == 1 else {"traffic": None, "traffic_stale": "profiled at N = 1 only"}
-        out["roofline"] = {"bound": "hbm", "achieved": round(algo / k_s / 1e9, 1), "peak": HBM_PEAK_GBS,
-                           "unit": "GB/s", "frac": round(algo / k_s / 1e9 / HBM_PEAK_GBS, 4),
-                           **tr, "kernel": kn, "rank": rank,
+        out["roofline"] = {"bound": "hbm", "achieved": round(algo_rows / k_s / 1e9, 1), "peak": HBM_PEAK_GBS,
+                           "unit": "GB/s", "frac": round(algo_rows / k_s / 1e9 / HBM_PEAK_GBS, 4),
+                           **tr, "kernel": kn, "rank": rank, "algorithmic_bytes_per_launch": algo_rows,
                            "avg_kernel_us": round(k_s * 1e6, 1), "launches": k_n}
+        # the same records gathered by row into the touched rows, plain (dml_diag_gather_floor:
+        # no key index, slot table or negativity check), timed after the steps into the
+        # store's shard (left as it was: the pushes and their negations, applied in turn)
+        fl = gather_floor(L, torch, store, pos + neg, S, cols, shard.firstKey, rec, st)
+        out["roofline"]["measured_gather_floor_us"] = round(fl * 1e3, 1)
+        out["roofline"]["frac_of_measured_floor"] = round(fl * 1e-3 / k_s, 3)
     store.close()
     del pos, neg, sets
     torch.cuda.synchronize()
@@ -1047,6 +1107,52 @@ def leg_config5(ctx: Ctx, L, args) -> dict:
     if world == 1 and not args.no_cpu:
         out["cpu_baseline"] = leg_cpu_baseline("5")
     return out
+
+
+def dense_floor(L, store, ptrs, lens, st, reps: int = 3):
+    """Best of `reps` dml_diag_dense_floor runs (ms) over the leg's own shard and pushes
+    (the same allocations), and whether it wrote out of place (k_flat_ident's layout)."""
+    n = len(ptrs)
+    P, Ln = (C.c_void_p * n)(*ptrs), (C.c_int64 * n)(*lens)
+    best, ms, oop = None, C.c_float(), C.c_int32()
+    for _ in range(reps):
+        assert L.dml_diag_dense_floor(C.c_void_p(store._h), P, Ln, n, C.c_void_p(st), C.byref(ms), C.byref(oop)) == 0
+        best = ms.value if best is None else min(best, ms.value)
+    return best, bool(oop.value)
+
+
+def gather_floor(L, torch, store, bufs, rows, cols, first, rec, st, reps: int = 3) -> float:
+    """Best of `reps` dml_diag_gather_floor runs (ms) over the records of `bufs`: the
+    first half ([:W]) then the second ([W:]) in turn, so the shard ends where it began.
+    Row lists are built on the device: every record's row, stable-sorted by row, with
+    the records of one row in push order."""
+    half = len(bufs) // 2
+    lists = []
+    for part in (bufs[:half], bufs[half:]):
+        rows_l, addr_l = [], []
+        for b in part:
+            r = b.view(-1, rec)[:, :4].contiguous().view(torch.int32).view(-1).to(torch.int64) - first
+            rows_l.append(r)
+            addr_l.append(b.data_ptr() + 4 + torch.arange(r.numel(), device="cuda", dtype=torch.int64) * rec)
+        r = torch.cat(rows_l)
+        a = torch.cat(addr_l)
+        o = torch.sort(r, stable=True).indices
+        r, a = r[o], a[o]
+        cnt = torch.bincount(r, minlength=rows)
+        trow = torch.nonzero(cnt).view(-1).to(torch.int32)
+        tptr = torch.zeros(trow.numel() + 1, dtype=torch.int32, device="cuda")
+        tptr[1:] = torch.cumsum(cnt[cnt > 0], 0).to(torch.int32)
+        lists.append((trow, tptr, a.contiguous()))
+    torch.cuda.synchronize()
+    best, ms = None, C.c_float()
+    for i in range(2 * reps):
+        trow, tptr, a = lists[i & 1]
+        assert L.dml_diag_gather_floor(C.c_void_p(store.device_ptr()), cols, C.c_void_p(trow.data_ptr()),
+                                       C.c_void_p(tptr.data_ptr()), C.c_void_p(a.data_ptr()), trow.numel(),
+                                       C.c_void_p(st), C.byref(ms)) == 0
+        best = ms.value if best is None else min(best, ms.value)
+    del lists
+    return best
 
 
 # ---------------------------------------------------------------- configs 4 and 5, one shard
@@ -1222,6 +1328,8 @@ def main():
     ap.add_argument("--no-timing", action="store_true", help="no kernel timing events in the timed region")
     ap.add_argument("--sparse-steps", type=int, default=20, help="config-3 sparse leg steps (0 = skip; N=1 only)")
     ap.add_argument("--pieces", type=int, default=1, help="pre-reduce row slices per call (sharded path)")
+    ap.add_argument("--sparse-cu-split", type=int, default=0,
+                    help="config 3: CUs of the partition's stream (| pattern << 16; 0 = every CU for both)")
     ap.add_argument("--shuffle-keep-parity", action="store_true", help=argparse.SUPPRESS)
     ap.add_argument("--shuffle-orders", type=int, default=0, help=argparse.SUPPRESS)
     ap.add_argument("--alloc-seed", type=int, default=0, help=argparse.SUPPRESS)
@@ -1231,7 +1339,7 @@ def main():
     ap.add_argument("--emulate-rs", type=int, default=0,
                     help="diagnostic with --group at N = 1: the owner-side HBM footprint of an N-rank "
                          "ring reduce-scatter + 1/N apply (results not valid)")
-    ap.add_argument("--emulate-channels", type=int, default=32,
+    ap.add_argument("--emulate-channels", type=int, default=RS_CHANNELS,
                     help="--emulate-rs: blocks of the ring reduce-scatter footprint (RCCL: one per channel)")
     ap.add_argument("--index-normal-prio", action="store_true", help=argparse.SUPPRESS)
     ap.add_argument("--native-group", action="store_true",
@@ -1260,6 +1368,12 @@ def main():
     ap.add_argument("--rehearse-gloo", action="store_true", help=argparse.SUPPRESS)
     args = ap.parse_args()
     SLAB[0] = not args.separate_buffers
+    # RCCL's channel count for the torch binding's reduce-scatter, pinned before any GPU
+    # call (RCCL reads it at communicator creation; the native group pins the same count
+    # through ncclCommInitRankConfig): the one-GPU ring emulation favours
+    # 128 blocks at N = 4 and 8 over RCCL's own choice
+    for k in ("NCCL_MIN_NCHANNELS", "NCCL_MAX_NCHANNELS"):
+        os.environ.setdefault(k, str(RS_CHANNELS))
     if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
         sys.exit(launch_ranks(args.gpus, sys.argv[1:]))
     # stdout carries exactly the one JSON line: RCCL and other native libraries print
@@ -1316,7 +1430,7 @@ def main():
         line["native_group"] = guarded_leg(ctx, line, out, "native_group", lambda: leg_native_group(ctx, L, args),
                                            seconds=180.0)
     if world == 1 and not args.group and args.sparse_steps > 0:
-        line["sparse"] = sparse_leg(ctx, L, args.sparse_steps, cpu=not args.no_cpu)
+        line["sparse"] = sparse_leg(ctx, L, args.sparse_steps, cpu=not args.no_cpu, cu_split=args.sparse_cu_split)
     if rank == 0 and world == 1 and not args.no_cpu and not args.group:
         line["cpu_baseline"] = cpu_baseline()
     if args.rehearse_gloo and world > 1:

@@ -34,7 +34,8 @@ class dml_store_counters(C.Structure):
     """Mirror of dml_store_counters (dml_store_stats)."""
     _fields_ = [("chunks", C.c_int64), ("spec_chunks", C.c_int64), ("spec_reruns", C.c_int64),
                 ("identity_pushes", C.c_int64), ("reused_pushes", C.c_int64), ("indexed_pushes", C.c_int64),
-                ("sparse_big_chunks", C.c_int64), ("sparse_replays", C.c_int64)]
+                ("sparse_big_chunks", C.c_int64), ("sparse_replays", C.c_int64),
+                ("ident_launches", C.c_int64)]
 
 
 # Every symbol include/distml_ps.h declares, with its ctypes signature.
@@ -109,6 +110,8 @@ SIGNATURES = {
     "dml_diag_stream": (C.c_int, [_i32, _vp, _vp, _i64, _vp, _P(C.c_float)]),
     "dml_diag_ring_rs": (C.c_int, [_i32, _vp, _vp, _vp, _i64, _i32, _i32, _i32, _vp]),
     "dml_diag_rmw_floor": (C.c_int, [_vp, _vp, _vp, _i64, _vp, _P(C.c_float)]),
+    "dml_diag_gather_floor": (C.c_int, [_vp, _i32, _vp, _vp, _vp, _i64, _vp, _P(C.c_float)]),
+    "dml_diag_dense_floor": (C.c_int, [_vp, _vp, _vp, _i32, _vp, _P(C.c_float), _P(_i32)]),
     "dml_diag_store_knob": (C.c_int, [_vp, _i32, _i64]),
     "dml_last_error": (C.c_char_p, []),
     "dml_version": (C.c_char_p, []),

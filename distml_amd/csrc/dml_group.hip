@@ -17,8 +17,9 @@
 // Calls are asynchronous and overlap exactly as in group.py: the next call's key
 // index runs on a high-priority side stream, two partial / receive buffer sets
 // alternate, and a call's key / repeated-row errors surface at the next call or
-// at dml_group_flush. The communicator comes from ncclCommInitRank with a
-// unique id the caller distributes (the JVM's control plane).
+// at dml_group_flush. The communicator comes from ncclCommInitRankConfig (the
+// channel count pinned, kRsChannels) with a unique id the caller distributes (the
+// JVM's control plane).
 #include <rccl/rccl.h>
 
 #include <algorithm>
@@ -108,6 +109,8 @@ struct dml_group {
 };
 
 namespace {
+
+constexpr int kRsChannels = 128;  // RCCL CTAs (channels) per collective of the group
 
 // A/B switch for the race check (scripts/build_ab.sh nofix -DDML_AB_NO_FAIL_ORDER=1): the
 // local-failure path without its stream orders, to show the asynchronous RCCL stand-in
@@ -264,7 +267,14 @@ int group_init(dml_group* g, const uint8_t* unique_id) {
     GHIP(hipMalloc((void**)&g->xcnt, sizeof(int64_t) * 4 * (size_t)g->world * kMaxW));
     ncclUniqueId id;
     memcpy(&id, unique_id, sizeof id);
-    GNCCL(ncclCommInitRank(&g->comm, g->world, id, g->rank));
+    // The reduce-scatter's channel count is pinned instead of left to RCCL's tuning: one
+    // rank's ring footprint emulated on one GPU beside the real pre-reduce (DESIGN.md §6,
+    // bench.py --emulate-rs) runs N = 4 / 8 at 2.6x / 5.3x the one-GPU store with 32
+    // blocks, 3.0x / 6.1x with 64 and 3.4x / 6.7x with 128
+    ncclConfig_t cfg = NCCL_CONFIG_INITIALIZER;
+    cfg.minCTAs = kRsChannels;
+    cfg.maxCTAs = kRsChannels;
+    GNCCL(ncclCommInitRankConfig(&g->comm, g->world, id, g->rank, &cfg));
     return DML_OK;
 }
 

@@ -292,6 +292,10 @@ hipError_t launch_ada_moments(float* shard, const float* src, int64_t rows, int3
 
 hipError_t launch_stream(bool copy, void* dst, const void* src, int64_t n16, hipStream_t st, LaunchEv ev);
 hipError_t launch_rmw_floor(float* a, const uint32_t* idx, const float* v, int64_t n, hipStream_t st, LaunchEv ev);
+hipError_t launch_dense_floor(const float* data, float* out, float* delta, const Batch& bt, int nb, int64_t stride,
+                              int K, int32_t cols, int64_t elems, hipStream_t st, LaunchEv ev);
+hipError_t launch_gather_floor(int32_t* shard, int32_t cols, const int32_t* trow, const int32_t* tptr,
+                               const uint64_t* addr, int64_t ntouched, hipStream_t st, LaunchEv ev);
 hipError_t launch_rand(int vtype, void* p, int64_t rows, int32_t cols, uint64_t s0, hipStream_t st);
 hipError_t launch_synth_fill(int vtype, void* p, int64_t n, uint64_t s0, hipStream_t st);
 hipError_t launch_key_rows(const uint8_t* base, int64_t nrec, int64_t stride, int K, int64_t first, int64_t rows,

@@ -2545,6 +2545,130 @@ hipError_t launch_rmw_floor(float* a, const uint32_t* idx, const float* v, int64
     return hipGetLastError();
 }
 
+// Row-gather floor (diagnostic, config 5): the touched rows of an int32 shard in row
+// order, each read once, every record that lists it (listed in push order by the
+// caller, `addr` = the record's value bytes) gathered and added, the row written once
+// — the same bytes as the IntMatrixStore reduce with no key index, slot table,
+// negativity check or error bookkeeping. One wave per touched row (<= 256 16-B
+// vectors: cols <= 1024), four records' loads in flight, XCD-contiguous blocks as the
+// product's DEPTH-3 reduce. The values are meaningful (plain wrapping int adds).
+__global__ __launch_bounds__(256) void k_gather_floor(int32_t* __restrict__ shard, int32_t cols,
+                                                      const int32_t* __restrict__ trow, const int32_t* __restrict__ tptr,
+                                                      const uint64_t* __restrict__ addr, int64_t ntouched) {
+    const int64_t w = xcd_block() * 4 + (threadIdx.x >> 6);
+    if (w >= ntouched) return;
+    const int lane = threadIdx.x & 63, nvec = cols / 4;
+    uint8_t* rowp = (uint8_t*)(shard + (int64_t)trow[w] * cols);
+    const int32_t b0 = tptr[w], b1 = tptr[w + 1];
+    u32x4 acc[4];
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+        const int v = lane + 64 * j;
+        acc[j] = v < nvec ? ldg16_nt(rowp + v * 16) : u32x4{0u, 0u, 0u, 0u};
+    }
+    for (int32_t e = b0; e < b1; e += 4) {
+        u32x4 x[4][4];
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+            const uint64_t a = e + k < b1 ? uni64(addr[e + k]) : 0ull;
+#pragma unroll
+            for (int j = 0; j < 4; ++j) {
+                const int v = lane + 64 * j;
+                x[k][j] = (a && v < nvec) ? ldg16_nt((const uint8_t*)a + v * 16) : u32x4{0u, 0u, 0u, 0u};
+            }
+        }
+#pragma unroll
+        for (int k = 0; k < 4; ++k)
+#pragma unroll
+            for (int j = 0; j < 4; ++j) acc[j] += x[k][j];
+    }
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+        const int v = lane + 64 * j;
+        if (v < nvec) stg16_nt(rowp + v * 16, acc[j]);
+    }
+}
+
+hipError_t launch_gather_floor(int32_t* shard, int32_t cols, const int32_t* trow, const int32_t* tptr,
+                               const uint64_t* addr, int64_t ntouched, hipStream_t st, LaunchEv ev) {
+    if (ntouched <= 0) return hipSuccess;
+    const unsigned grid = (unsigned)((ntouched + 3) / 4);
+    hipExtLaunchKernelGGL(k_gather_floor, dim3(grid), dim3(256), 0, st, ev.start, ev.stop, 0, shard, cols, trow, tptr,
+                          addr, ntouched);
+    return hipGetLastError();
+}
+
+// Dense stream floor (diagnostic, config 4 and its AdaGrad variant): the shard's
+// elements in order, each read once with the same element of every full-range push
+// whose records are rows in order (record r = row r, values 4 bytes after the key),
+// summed in push order and written once — to `out` (the speculative second buffer,
+// as k_flat_ident writes it) or in place; ADA: delta += u·u beside it (AdaGrad's
+// data / delta stream, k_ada_ident's bytes). No key checks, slot tables or maxDelta
+// bookkeeping: the plain stream of the same bytes, over the same allocations.
+template <bool ADA>
+__global__ __launch_bounds__(256) void k_dense_floor(const float* __restrict__ data, float* __restrict__ out,
+                                                     float* __restrict__ delta, Batch bt, int nb, int64_t stride,
+                                                     int K, int32_t cols, int64_t nvec) {
+    constexpr int U = 2, D = 4;
+    const int64_t v0 = xcd_block() * (256 * U) + threadIdx.x;
+    int64_t off[U];
+    bool ok[U];
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+        const int64_t v = v0 + u * 256, e = v * 4;
+        ok[u] = v < nvec;
+        off[u] = (e / cols) * stride + K + (e % cols) * 4;
+    }
+    u32x4 acc[U], dl[U];
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+        const int64_t v = v0 + u * 256;
+        acc[u] = ok[u] ? ldg16_nt((const uint8_t*)data + v * 16) : u32x4{0u, 0u, 0u, 0u};
+        if (ADA) dl[u] = ok[u] ? ldg16_nt((const uint8_t*)delta + v * 16) : u32x4{0u, 0u, 0u, 0u};
+    }
+    for (int b = 0; b < nb; b += D) {
+        u32x4 x[D][U];
+#pragma unroll
+        for (int d = 0; d < D; ++d)
+#pragma unroll
+            for (int u = 0; u < U; ++u)
+                x[d][u] = (b + d < nb && ok[u]) ? ldg16_nt(bt.base[b + d] + off[u]) : u32x4{0u, 0u, 0u, 0u};
+#pragma unroll
+        for (int d = 0; d < D; ++d) {
+            if (b + d >= nb) break;
+#pragma unroll
+            for (int u = 0; u < U; ++u)
+#pragma unroll
+                for (int e = 0; e < 4; ++e) {
+                    const float g = __uint_as_float(x[d][u][e]);
+                    acc[u][e] = __float_as_uint(__fadd_rn(__uint_as_float(acc[u][e]), g));
+                    if (ADA) dl[u][e] = __float_as_uint(__fadd_rn(__uint_as_float(dl[u][e]), __fmul_rn(g, g)));
+                }
+        }
+    }
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+        if (!ok[u]) continue;
+        const int64_t v = v0 + u * 256;
+        stg16_nt((uint8_t*)out + v * 16, acc[u]);
+        if (ADA) stg16_nt((uint8_t*)delta + v * 16, dl[u]);
+    }
+}
+
+hipError_t launch_dense_floor(const float* data, float* out, float* delta, const Batch& bt, int nb, int64_t stride,
+                              int K, int32_t cols, int64_t elems, hipStream_t st, LaunchEv ev) {
+    const int64_t nvec = elems / 4;
+    if (nvec <= 0) return hipSuccess;
+    const unsigned grid = (unsigned)((nvec + 511) / 512);
+    if (delta)
+        hipExtLaunchKernelGGL(k_dense_floor<true>, dim3(grid), dim3(256), 0, st, ev.start, ev.stop, 0, data, out, delta,
+                              bt, nb, stride, K, cols, nvec);
+    else
+        hipExtLaunchKernelGGL(k_dense_floor<false>, dim3(grid), dim3(256), 0, st, ev.start, ev.stop, 0, data, out,
+                              delta, bt, nb, stride, K, cols, nvec);
+    return hipGetLastError();
+}
+
 hipError_t launch_stream(bool copy, void* dst, const void* src, int64_t n16, hipStream_t st, LaunchEv ev) {
     if (n16 <= 0) return hipSuccess;
     const int64_t want = (n16 + 1023) / 1024;  // one 256-thread block per 4 wave steps

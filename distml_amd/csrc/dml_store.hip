@@ -15,6 +15,7 @@
 // exception carries.
 #include "distml_ps.h"
 #include "dml_internal.h"
+#include <hip/hip_ext.h>
 
 #include <algorithm>
 #include <cmath>
@@ -483,6 +484,7 @@ int launch_apply(dml_store* s, Chunk& c, Workspace& W, const Ctrl* prev) {
         int64_t nblk = 0;
         W.clears = reduce_clears_slots(vtype_of(s->desc), reduce_mode(s), s->cols);
         c.bt.src = c.in != c.out ? c.in : nullptr;
+        if (W.flat_ident) s->st.ident_launches += 1;
         if (W.flat_ident && s->adagrad)  // every push verified-identity (the host's Ctrl copy)
             HIPCHK(launch_ada_ident(c.out, s->rows, s->cols, c.bt, c.nb, s->stride, s->K, ada_args(s), s->stream,
                                     &nblk, ev));
@@ -1613,12 +1615,46 @@ int dml_store_set_timing(dml_store* s, int32_t enable) {
     return DML_OK;
 }
 
+// DML_KNOB_INDEX_CUS: the index stream (the next chunk's key index / sparse partition)
+// on k of the device's CUs and the apply stream on the others (k = 0: both streams on
+// every CU, the default). pattern 0 spreads the k CUs evenly over the CU numbering,
+// 1 takes the first k. Caller holds s->mu.
+static int set_cu_split(dml_store* s, int k, int pattern) {
+    DeviceGuard g(s->device);
+    int ncu = 0;
+    HIPCHK(hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, s->device));
+    if (k < 0 || k >= ncu || pattern < 0 || pattern > 1) return set_err(DML_E_INVALID_ARG, "bad CU split");
+    if (int rc = begin_call(s)) return rc;
+    HIPCHK(hipStreamSynchronize(s->stream));
+    HIPCHK(hipStreamSynchronize(s->istream));
+    const int words = (ncu + 31) / 32;
+    std::vector<uint32_t> mi((size_t)words, 0u), ma((size_t)words, 0u);
+    for (int c = 0; c < ncu; ++c) {
+        const bool idx = k > 0 && (pattern == 1 ? c < k : (int64_t)c * k % ncu < k);
+        (idx ? mi : ma)[(size_t)(c / 32)] |= 1u << (c % 32);
+    }
+    hipStream_t ns = nullptr, ni = nullptr;
+    if (k == 0) {
+        HIPCHK(hipStreamCreateWithFlags(&ns, hipStreamNonBlocking));
+        HIPCHK(hipStreamCreateWithFlags(&ni, hipStreamNonBlocking));
+    } else {
+        HIPCHK(hipExtStreamCreateWithCUMask(&ns, (uint32_t)words, ma.data()));
+        HIPCHK(hipExtStreamCreateWithCUMask(&ni, (uint32_t)words, mi.data()));
+    }
+    (void)hipStreamDestroy(s->stream);
+    (void)hipStreamDestroy(s->istream);
+    s->stream = ns;
+    s->istream = ni;
+    return DML_OK;
+}
+
 int dml_diag_store_knob(dml_store* s, int32_t knob, int64_t value) {
     if (int rc = check_store(s)) return rc;
     if (value < 0) return set_err(DML_E_INVALID_ARG, "negative knob value");
     std::lock_guard<std::mutex> lk(s->mu);
     switch (knob) {
         case DML_KNOB_IDENT_FULL_MIN_BYTES: s->ident_full_min = value; return DML_OK;
+        case DML_KNOB_INDEX_CUS: return set_cu_split(s, (int)(value & 0xFFFF), (int)(value >> 16));
         default: return set_err(DML_E_INVALID_ARG, "unknown knob");
     }
 }
@@ -2143,10 +2179,14 @@ int dml_prereduce_piece(dml_prereduce* p, int64_t row_block, int64_t row_stride,
     // the lean kernel, when no wave's rows straddle two row blocks of the map
     const int Rw = flat_ident_rows_per_wave(p->desc.value_type, p->cols);
     if (p->hidx && p->idx_waited && (row_block % Rw == 0 || ntask_rows <= row_block) &&
-        flat_ident_ok(*p->hidx, p->bt, p->nb, p->rows, kNoPos))
+        flat_ident_ok(*p->hidx, p->bt, p->nb, p->rows, kNoPos)) {
+        if (p->ctx) {
+            std::lock_guard<std::mutex> lk(p->ctx->mu);
+            p->ctx->st.ident_launches += 1;
+        }
         HIPCHK(launch_flat_ident(p->desc.value_type, kPreReduce, dev_out, ntask_rows, p->cols, p->bt, p->nb, p->stride,
                                  p->K, p->ctrl, st, nullptr, ev, rm));
-    else
+    } else
         HIPCHK(launch_reduce(p->desc.value_type, kPreReduce, dev_out, ntask_rows, p->cols, p->bt, p->nb, p->stride,
                              p->K, p->slot, nullptr, p->ctrl, kNoPos, none, st, nullptr, ev, rm));
     p->done_ev = ev.stop;
@@ -2489,6 +2529,61 @@ int dml_diag_rmw_floor(float* dev_array, const uint32_t* dev_index, const float*
     HIPCHK(hipEventCreate(&e0));
     hipError_t e = hipEventCreate(&e1);
     if (e == hipSuccess) e = launch_rmw_floor(dev_array, dev_index, dev_values, n, st, LaunchEv{e0, e1});
+    if (e == hipSuccess) e = hipEventSynchronize(e1);
+    float t = 0.f;
+    if (e == hipSuccess) e = hipEventElapsedTime(&t, e0, e1);
+    (void)hipEventDestroy(e0);
+    if (e1) (void)hipEventDestroy(e1);
+    if (e != hipSuccess) return set_err(DML_E_HIP, hipGetErrorString(e));
+    if (ms) *ms = t;
+    return DML_OK;
+}
+
+int dml_diag_dense_floor(dml_store* s, const void* const* dev_bufs, const int64_t* lens, int32_t n, void* stream,
+                         float* ms, int32_t* out_of_place) {
+    if (int rc = check_store(s)) return rc;
+    if (!s->is_matrix || s->V != 4 || vtype_of(s->desc) != kF32 || s->cols % 4 || n < 1 || n > kMaxW || !dev_bufs ||
+        !lens)
+        return set_err(DML_E_INVALID_ARG, "dense floor: an f32 matrix store of whole 16-B vectors, 1..64 pushes");
+    for (int b = 0; b < n; ++b)
+        if (!dev_bufs[b] || lens[b] != s->rows * s->stride)
+            return set_err(DML_E_INVALID_ARG, "dense floor: every push lists every row once (full range)");
+    std::lock_guard<std::mutex> lk(s->mu);
+    DeviceGuard g(s->device);
+    if (int rc = begin_call(s)) return rc;
+    Batch bt{};
+    for (int b = 0; b < n; ++b) bt.base[b] = (const uint8_t*)dev_bufs[b];
+    // out of place into the speculative second buffer where the store has one (k_flat_ident's
+    // layout); AdaGrad stores apply in place (k_ada_ident)
+    float* out = (float*)(s->data_alt && !s->adagrad ? s->data_alt : s->data);
+    if (out_of_place) *out_of_place = out != s->data ? 1 : 0;
+    hipStream_t st = (hipStream_t)stream;
+    hipEvent_t e0 = nullptr, e1 = nullptr;
+    HIPCHK(hipEventCreate(&e0));
+    hipError_t e = hipEventCreate(&e1);
+    if (e == hipSuccess)
+        e = launch_dense_floor((const float*)s->data, out, s->adagrad ? s->delta : nullptr, bt, n, s->stride, s->K,
+                               s->cols, s->rows * s->cols, st, LaunchEv{e0, e1});
+    if (e == hipSuccess) e = hipEventSynchronize(e1);
+    float t = 0.f;
+    if (e == hipSuccess) e = hipEventElapsedTime(&t, e0, e1);
+    (void)hipEventDestroy(e0);
+    if (e1) (void)hipEventDestroy(e1);
+    if (e != hipSuccess) return set_err(DML_E_HIP, hipGetErrorString(e));
+    if (ms) *ms = t;
+    return DML_OK;
+}
+
+int dml_diag_gather_floor(int32_t* dev_shard, int32_t cols, const int32_t* dev_rows, const int32_t* dev_ptr,
+                          const uint64_t* dev_addr, int64_t ntouched, void* stream, float* ms) {
+    if (!dev_shard || cols <= 0 || cols % 4 || cols > 1024 || ntouched < 0 ||
+        (ntouched > 0 && (!dev_rows || !dev_ptr || !dev_addr)) || (uintptr_t)dev_shard % 16)
+        return set_err(DML_E_INVALID_ARG, "bad gather floor arguments (cols a multiple of 4, at most 1024)");
+    hipStream_t st = (hipStream_t)stream;
+    hipEvent_t e0 = nullptr, e1 = nullptr;
+    HIPCHK(hipEventCreate(&e0));
+    hipError_t e = hipEventCreate(&e1);
+    if (e == hipSuccess) e = launch_gather_floor(dev_shard, cols, dev_rows, dev_ptr, dev_addr, ntouched, st, LaunchEv{e0, e1});
     if (e == hipSuccess) e = hipEventSynchronize(e1);
     float t = 0.f;
     if (e == hipSuccess) e = hipEventElapsedTime(&t, e0, e1);

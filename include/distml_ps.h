@@ -147,6 +147,8 @@ typedef struct dml_store_counters {
     int64_t indexed_pushes;
     int64_t sparse_big_chunks;  /* array chunks applied through the one-level partition (big leaves) */
     int64_t sparse_replays;     /* array chunks with leaves the exact replay applied */
+    int64_t ident_launches;     /* chunks / pre-reduce pieces launched through the all-identity
+                                   kernels (k_flat_ident, k_ada_ident) */
 } dml_store_counters;
 int dml_store_stats(dml_store* s, dml_store_counters* out, int32_t reset);
 
@@ -436,6 +438,27 @@ int dml_diag_stream(int32_t copy, void* dev_dst, const void* dev_src, int64_t by
 int dml_diag_rmw_floor(float* dev_array, const uint32_t* dev_index, const float* dev_values, int64_t n, void* stream,
                        float* ms);
 
+/* Dense stream floor (diagnostic, config 4 and its AdaGrad variant): the store's f32
+ * shard (cols a multiple of 4) plus n full-range pushes whose records are rows in order
+ * (lens[b] = rows x record stride; record r is taken to be row r, keys not read), each
+ * element summed in push order and written once: into the speculative second buffer
+ * where the store has one (as k_flat_ident writes, *out_of_place = 1; the committed
+ * shard is left alone), else in place; AdaGrad stores also delta += u·u in place (alpha
+ * and maxDelta untouched). The plain stream of the reduce's bytes over the same
+ * allocations, timed on `stream`, *ms = kernel time: bench.py's config-4 legs report
+ * their kernels against it. */
+int dml_diag_dense_floor(dml_store* s, const void* const* dev_bufs, const int64_t* lens, int32_t n, void* stream,
+                         float* ms, int32_t* out_of_place);
+
+/* Row-gather floor (diagnostic, config 5): for each of the ntouched rows dev_rows[i] of
+ * an int32 shard (row-major, `cols` a multiple of 4, at most 1024), read the row once,
+ * add the records dev_addr[dev_ptr[i] .. dev_ptr[i+1]) (device addresses of each
+ * record's first value, in push order) and write the row once: the IntMatrixStore
+ * reduce's bytes with no key index, slot table or negativity check. Timed on `stream`,
+ * *ms = kernel time. bench.py's config-5 leg reports the reduce against it. */
+int dml_diag_gather_floor(int32_t* dev_shard, int32_t cols, const int32_t* dev_rows, const int32_t* dev_ptr,
+                          const uint64_t* dev_addr, int64_t ntouched, void* stream, float* ms);
+
 /* Ring reduce-scatter footprint (diagnostic, bench.py --emulate-rs N): the local HBM
  * traffic one rank's ring reduce-scatter of a world x chunk_bytes partial makes —
  * world - 1 steps, each reading one chunk of the partial and the chunk that arrived
@@ -453,6 +476,11 @@ int dml_diag_ring_rs(int32_t value_type, const void* dev_partial, void* dev_recv
  * Lowering it lets tests drive that path at small sizes; results are the same either way.
  * Returns DML_E_INVALID_ARG for an unknown knob or a negative value. */
 #define DML_KNOB_IDENT_FULL_MIN_BYTES 1
+/* DML_KNOB_INDEX_CUS = k | pattern << 16: the store's index stream (the next chunk's key
+ * index or sparse partition) on k CUs and its apply stream on the others, k = 0 (the
+ * default) both on every CU; pattern 0 spreads the k CUs evenly over the CU numbering,
+ * 1 takes the first k (config 3: the partition beside the leaf). */
+#define DML_KNOB_INDEX_CUS 2
 int dml_diag_store_knob(dml_store* s, int32_t knob, int64_t value);
 
 /* --- misc --------------------------------------------------------------- */

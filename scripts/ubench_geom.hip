@@ -53,7 +53,9 @@ __device__ inline int64_t xcd_remap() {  // XCD x runs the x-th contiguous run o
     return x < full ? x * per + i : full * per + (x - full) * (per - 1) + i;
 }
 
-// MODE 0: shard read + pushes, shard written; 1: pushes only (reads); 2: shard read + pushes, no write
+// MODE 0: shard read + pushes, shard written in place; 1: pushes only (reads); 2: shard
+// read + pushes, no write; 3: shard read + pushes, written to the second shard buffer
+// (out of place: the product's speculative chunks, which keep their input for a re-run)
 template <int U, int D, int K, int MODE, bool XCD>
 __global__ __launch_bounds__(256) void k_geo(Ptrs p, int W, uint8_t* shard, uint8_t* sink) {
     const int64_t blk = XCD ? xcd_remap() : (int64_t)blockIdx.x;
@@ -61,6 +63,7 @@ __global__ __launch_bounds__(256) void k_geo(Ptrs p, int W, uint8_t* shard, uint
     const int lane = threadIdx.x & 63;
     constexpr uint32_t SB = U * 1024u;
     const auto rs = rsrc(shard + g * SB, SB);
+    const auto ro = rsrc((MODE == 3 ? sink : shard) + g * SB, SB);
     u32x4 acc[U];
 #pragma unroll
     for (int u = 0; u < U; ++u)
@@ -78,9 +81,9 @@ __global__ __launch_bounds__(256) void k_geo(Ptrs p, int W, uint8_t* shard, uint
 #pragma unroll
             for (int j = 0; j < K * U; ++j) acc[j % U] = addf(acc[j % U], v[d][j]);
     }
-    if (MODE == 0) {
+    if (MODE == 0 || MODE == 3) {
 #pragma unroll
-        for (int u = 0; u < U; ++u) __builtin_amdgcn_raw_buffer_store_b128(acc[u], rs, u * 1024 + lane * 16, 0, 2);
+        for (int u = 0; u < U; ++u) __builtin_amdgcn_raw_buffer_store_b128(acc[u], ro, u * 1024 + lane * 16, 0, 2);
     } else {
         uint32_t x = 0;
 #pragma unroll
@@ -111,6 +114,7 @@ struct Geo {  // one allocation set
     std::vector<uint8_t*> allocs;
     Ptrs p{};
     uint8_t* shard = nullptr;
+    uint8_t* shard2 = nullptr;  // out-of-place output (MODE 3)
 };
 
 static void alloc_geo(Geo& g) {
@@ -128,6 +132,8 @@ static void alloc_geo(Geo& g) {
     }
     CK(hipMalloc(&g.shard, g.S));
     g.allocs.push_back(g.shard);
+    CK(hipMalloc(&g.shard2, g.S));
+    g.allocs.push_back(g.shard2);
     for (int b = 0; b < g.W; ++b) hipLaunchKernelGGL(k_fill, dim3(8192), dim3(256), 0, 0, g.p.p[b], P, 17u * b + 3u);
     hipLaunchKernelGGL(k_fill, dim3(8192), dim3(256), 0, 0, g.shard, g.S, 99u);
     CK(hipDeviceSynchronize());
@@ -148,7 +154,7 @@ static void time_case(const Geo& g, const Kern& k, int reps, float& best, float&
     float sum = 0.f;
     for (int it = 0; it <= reps; ++it) {
         CK(hipEventRecord(e0));
-        hipLaunchKernelGGL(k.f, dim3(grid), dim3(256), 0, 0, g.p, g.W, g.shard, g_sink);
+        hipLaunchKernelGGL(k.f, dim3(grid), dim3(256), 0, 0, g.p, g.W, g.shard, k.mode == 3 ? g.shard2 : g_sink);
         CK(hipEventRecord(e1));
         CK(hipEventSynchronize(e1));
         float ms;
@@ -164,13 +170,13 @@ static void time_case(const Geo& g, const Kern& k, int reps, float& best, float&
 
 static void report(const char* label, const Geo& g, const Kern& k, int round, float best, float mean) {
     const double P = (double)g.S * g.K;
-    const double bytes = g.W * P + (k.mode != 1 ? g.S : 0) + (k.mode == 0 ? g.S : 0);
-    const double wshare = k.mode == 0 ? g.S / bytes : 0.0;
+    const double bytes = g.W * P + (k.mode != 1 ? g.S : 0) + (k.mode == 0 || k.mode == 3 ? g.S : 0);
+    const double wshare = k.mode == 0 || k.mode == 3 ? g.S / bytes : 0.0;
     printf("{\"case\": \"%s\", \"round\": %d, \"W\": %d, \"push_bytes\": %.0f, \"shard_bytes\": %lld, \"layout\": \"%s\", "
            "\"U_KiB_per_wave\": %d, \"D\": %d, \"K\": %d, \"mode\": \"%s\", \"xcd\": %d, \"write_share\": %.4f, "
            "\"best_us\": %.1f, \"mean_us\": %.1f, \"frac_best\": %.4f, \"frac_mean\": %.4f}\n",
            label, round, g.W, P, (long long)g.S, g.slab ? "slab" : "separate", k.U, k.D, k.K,
-           k.mode == 0 ? "rmw" : k.mode == 1 ? "push reads only" : "shard+push reads", (int)k.xcd, wshare, best, mean,
+           k.mode == 0 ? "rmw" : k.mode == 1 ? "push reads only" : k.mode == 2 ? "shard+push reads" : "out of place", (int)k.xcd, wshare, best, mean,
            bytes / best / 1e6 / 8000.0, bytes / mean / 1e6 / 8000.0);
     fflush(stdout);
 }
@@ -194,7 +200,7 @@ int main(int argc, char** argv) {
     std::vector<Case> cases = {
         // config 2: 32 x 64 MiB pushes in one slab -> 64 MiB shard
         {"g2: 32 x 64 MiB slab", 32, 1, 64 * MiB, true,
-         {base, KN(4, 4, 1, 1, true), KN(4, 4, 1, 2, true), KN(4, 4, 1, 0, false), KN(2, 8, 1, 0, true), KN(8, 2, 1, 0, true),
+         {base, KN(4, 4, 1, 3, true), KN(4, 4, 1, 1, true), KN(4, 4, 1, 2, true), KN(4, 4, 1, 0, false), KN(2, 8, 1, 0, true), KN(8, 2, 1, 0, true),
           KN(16, 1, 1, 0, true)},
          20},
         {"g2 separate: 32 x 64 MiB", 32, 1, 64 * MiB, false, {base}, 20},
@@ -204,7 +210,7 @@ int main(int argc, char** argv) {
         {"mall: 32 x 128 MiB slab", 32, 1, 128 * MiB, true, {base}, 10},
         {"mall: 32 x 256 MiB slab", 32, 1, 256 * MiB, true, {base}, 10},
         {"mall: 32 x 512 MiB slab", 32, 1, 512 * MiB, true, {base, KN(4, 4, 1, 1, true)}, 6},
-        {"mall: 32 x 1 GiB slab", 32, 1, 1024 * MiB, true, {base, KN(4, 4, 1, 1, true)}, 5},
+        {"mall: 32 x 1 GiB slab", 32, 1, 1024 * MiB, true, {base, KN(4, 4, 1, 3, true), KN(4, 4, 1, 1, true)}, 5},
         {"mall: 16 x 1 GiB slab", 16, 1, 1024 * MiB, true, {base, KN(4, 4, 1, 1, true)}, 5},
         // 16 streams at config 2's write share (each push twice the shard's bytes)
         {"x: 16 x 2 GiB slab, 1 GiB shard (K 2)", 16, 2, 1024 * MiB, true, {base16, KN(4, 4, 2, 1, true)}, 5},
@@ -213,7 +219,7 @@ int main(int argc, char** argv) {
         {"x: 32 x 4 GB separate", 32, 1, 4000 * MiB, false, {base, KN(4, 4, 1, 1, true)}, 3},
         // config 4: 16 x 8 GB separate allocations -> 8 GB shard
         {"g4: 16 x 8 GB separate", 16, 1, 7630 * MiB, false,
-         {base, KN(4, 4, 1, 1, true), KN(4, 4, 1, 2, true), KN(4, 4, 1, 0, false), KN(2, 8, 1, 0, true), KN(8, 2, 1, 0, true),
+         {base, KN(4, 4, 1, 3, true), KN(4, 4, 1, 1, true), KN(4, 4, 1, 2, true), KN(4, 4, 1, 0, false), KN(2, 8, 1, 0, true), KN(8, 2, 1, 0, true),
           KN(16, 1, 1, 0, true)},
          3},
         {"g4 slab: 16 x 8 GB slab", 16, 1, 7630 * MiB, true, {base}, 3},
@@ -229,6 +235,9 @@ int main(int argc, char** argv) {
             report("alt g2: 32 x 64 MiB slab", a, base, r, best, mean);
             time_case(b, base, 4, best, mean);
             report("alt g4: 16 x 8 GB separate", b, base, r, best, mean);
+            const Kern oop = KN(4, 4, 1, 3, true);
+            time_case(b, oop, 4, best, mean);
+            report("alt g4: 16 x 8 GB separate", b, oop, r, best, mean);
         }
         free_geo(a);
         free_geo(b);

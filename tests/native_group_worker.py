@@ -19,6 +19,9 @@ Cases (generators shared with tests/test_gpu_group.py):
   beginfail int32 full-range calls; rank 0's call 1 hands over a ragged push, so its
             _begin_ctx fails (no pieces, no host wait for the set's last apply): it
             raises at once, contributes zeros, every rank finishes every call
+  asc       CALLS full-range calls whose pushes all list the rows in ascending order
+            (Java HashMap<Integer> order, config 4's case): the pre-reduce pieces take
+            the all-identity kernel (k_flat_ident) where no wave straddles a row block
   jni       int32 full-range calls and a pushLocal through the JNI shim's GpuShardGroup
             entry points (integration/jni/dml_jni.cc on the mock JNIEnv of tests/jni_mock)
 Writes out/<case>_<rank>.npz and prints one JSON line.
@@ -105,7 +108,7 @@ def main():
     uid = read_uid(a.uid_file, a.rank)
     world, rank = a.world, a.rank
     errors, res = [], {}
-    if a.case in ("full", "fault", "local", "beginfail"):
+    if a.case in ("full", "fault", "local", "beginfail", "asc"):
         vt = 0 if a.case in ("fault", "local", "beginfail") else a.vt
         rows, cols = a.rows, a.cols
         g = NativeShardGroup(DataDesc(1, 0, vt), rows, cols, rank, world, uid, device=a.device, pieces=a.pieces)
@@ -115,7 +118,8 @@ def main():
             g.debug_fail_verify(2)  # call 1's verdict (finished during call 2)
         calls = 1 if a.case == "local" else G.CALLS
         for call in range(calls):
-            bufs = G._buckets(pyoracle, vt, rank, a.pushes, rows, cols, call)
+            bufs = (G._asc_buckets(pyoracle, vt, rank, a.pushes, rows, cols, call) if a.case == "asc"
+                    else G._buckets(pyoracle, vt, rank, a.pushes, rows, cols, call))
             ptrs = [H.put(b) for b in bufs]
             lens = [b.nbytes for b in bufs]
             if a.case == "beginfail" and rank == 0 and call == 1:
@@ -142,7 +146,7 @@ def main():
         except Exception as e:
             errors.append(["flush", type(e).__name__, str(e)[:200]])
         res["data"] = g.store.values()
-        res["stats"] = np.array([g.prereduce_stats().get(k, 0) for k in ("spec_chunks", "spec_reruns")])
+        res["stats"] = np.array([g.prereduce_stats().get(k, 0) for k in ("spec_chunks", "spec_reruns", "ident_launches")])
     elif a.case == "jni":
         # the same full-range calls driven through the JNI shim's GpuShardGroup entry points
         # (integration/jni/dml_jni.cc linked with the in-process mock JNIEnv), int32, then
@@ -199,13 +203,15 @@ def main():
         g.close()
     H.free()
     np.savez(os.path.join(a.out, f"{a.case}_{rank}.npz"), **res)
-    calls = None
+    calls, ctas = None, None
     if dbl is not None:
         dbl.rccl_double_calls.restype = C.c_int64
         calls = int(dbl.rccl_double_calls())
+        dbl.rccl_double_ctas.restype = C.c_int32
+        ctas = [int(dbl.rccl_double_ctas(0)), int(dbl.rccl_double_ctas(1))]
     libs = {n: ln.split()[-1] for ln in open("/proc/self/maps") for n in ("librccl", "libdistml_ps")
             if n in ln}
-    print(json.dumps({"rank": rank, "errors": errors, "double_calls": calls, "libs": libs}), flush=True)
+    print(json.dumps({"rank": rank, "errors": errors, "double_calls": calls, "ctas": ctas, "libs": libs}), flush=True)
 
 
 if __name__ == "__main__":

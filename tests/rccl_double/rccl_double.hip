@@ -1,5 +1,5 @@
 // rccl_double.hip — TEST-ONLY stand-in for the RCCL entry points libdistml_ps.so
-// calls (ncclGetUniqueId, ncclCommInitRank, ncclReduceScatter, ncclSend/ncclRecv
+// calls (ncclGetUniqueId, ncclCommInitRank(Config), ncclReduceScatter, ncclSend/ncclRecv
 // in ncclGroupStart/End, ncclCommDestroy, ncclGetErrorString), so that the native
 // group's N > 1 schedule (distml_amd/csrc/dml_group.hip) runs with several ranks
 // on ONE GPU: RCCL itself refuses two ranks per device.
@@ -331,6 +331,10 @@ extern "C" {
 
 // Collectives this process ran through the double (tests assert it was used).
 int64_t rccl_double_calls(void) { return g_calls.load(); }
+// minCTAs / maxCTAs of the last ncclCommInitRankConfig (-1: none, or left undefined):
+// tests assert the library pins the reduce-scatter's channel count
+static int g_min_ctas = -1, g_max_ctas = -1;
+int32_t rccl_double_ctas(int32_t which) { return which ? g_max_ctas : g_min_ctas; }
 
 const char* ncclGetErrorString(ncclResult_t r) {
     switch (r) {
@@ -390,6 +394,17 @@ ncclResult_t ncclCommInitRank(ncclComm_t* out, int nranks, ncclUniqueId id, int 
     c->helper = std::thread(helper_main, c);
     *out = c;
     return ncclSuccess;
+}
+
+// RCCL's config variant: checks the initializer's size / magic as RCCL does, records the
+// CTA bounds, then the same communicator (the double has no channels to size)
+ncclResult_t ncclCommInitRankConfig(ncclComm_t* out, int nranks, ncclUniqueId id, int rank, ncclConfig_t* config) {
+    if (config && (config->size != sizeof(ncclConfig_t) || config->magic != 0xcafebeef)) return ncclInvalidArgument;
+    if (config) {
+        g_min_ctas = config->minCTAs == NCCL_CONFIG_UNDEF_INT ? -1 : config->minCTAs;
+        g_max_ctas = config->maxCTAs == NCCL_CONFIG_UNDEF_INT ? -1 : config->maxCTAs;
+    }
+    return ncclCommInitRank(out, nranks, id, rank);
 }
 
 ncclResult_t ncclCommDestroy(ncclComm_t c) {

@@ -521,6 +521,58 @@ def test_synth_kernel_matches_oracle_generator(oracle):
     assert t.cpu().numpy().tobytes() == oracle.synth_sparse_bucket(1, 1, 0, 10**9, 1000, 9, 123457, 99).tobytes()
 
 
+def test_gather_floor_diag_is_the_plain_row_sum():
+    """dml_diag_gather_floor (config 5's measured ceiling, bench.gather_floor) does the
+    reduce's work: every record added to its row, each touched row read and written
+    once — int32 wrapping sums equal numpy's on 6 pushes of 200 distinct rows of 500."""
+    import bench
+    from distml_amd import DataDesc, _lib
+    L = _lib.load()
+    rows, cols, nrec = 500, 100, 200
+    fmt = DataDesc(1, 0, 0)
+    s, _ = mk_store(fmt, 0, rows - 1, cols)
+    s.synth_fill(11)
+    want = s.values().astype(np.int64)
+    bufs = synth_device_buckets(L, fmt.to_c(), 0, rows, nrec, cols, [70 + b for b in range(6)],
+                                [(a, 13 * b) for b, a in enumerate((7, 9, 11, 13, 17, 19))])
+    for b in bufs:
+        rec = b.cpu().numpy().reshape(nrec, 1 + cols).view("<i4")
+        np.add.at(want, rec[:, 0], rec[:, 1:].astype(np.int64))
+    ms = bench.gather_floor(L, torch, s, bufs, rows, cols, 0, 4 + 4 * cols, 0, reps=1)
+    assert ms > 0
+    assert np.array_equal(s.values(), want.astype(np.uint32).view(np.int32).reshape(rows, cols))
+    s.close()
+
+
+@pytest.mark.parametrize("ada", [False, True])
+def test_dense_floor_diag_is_the_plain_stream(oracle, ada):
+    """dml_diag_dense_floor (the config-4 legs' live ceiling, bench.dense_floor) moves the
+    reduce's bytes with the reduce's arithmetic: on a store without a second buffer it
+    writes in place exactly the oracle's sums (AdaGrad: and delta), for 5 ascending
+    full-range pushes of 300 x 200 f32."""
+    import bench
+    from distml_amd import DataDesc, _lib
+    L = _lib.load()
+    rows, cols, W = 300, 200, 5
+    fmt = DataDesc(1, 0, 1, False, True, ada)
+    s, _ = mk_store(fmt, 0, rows - 1, cols)
+    s.synth_fill(13)
+    o = oracle_store(oracle, fmt, 0, rows - 1, cols)
+    o.synth_fill(13)
+    if ada:
+        s.setAlpha(0.025, 0.0001, 1.0)
+        o.set_alpha(0.025, 0.0001, 1.0)
+    bufs = synth_device_buckets(L, fmt.to_c(), 0, rows, rows, cols, [90 + b for b in range(W)], [(1, 0)] * W)
+    for b in bufs:
+        assert o.push(b.cpu().numpy().tobytes()) == 0
+    ms, oop = bench.dense_floor(L, s, [b.data_ptr() for b in bufs], [b.numel() for b in bufs], 0, reps=1)
+    assert ms > 0 and not oop
+    assert kat.bits_equal(s.values(), o.data)
+    if ada:
+        assert kat.bits_equal(s.adagrad_state()[1], o.delta)
+    s.close()
+
+
 def config2_perm(b, rows=16384):
     # ascending row order (Java HashMap<Integer> order) for even pushes, a seeded permutation for odd
     return (1, 0) if b % 2 == 0 else ((2 * b + 1) * 2654435761 % rows | 1, (b * 7919) % rows)

@@ -71,6 +71,8 @@ def run_ranks(tmp_path, world, case, double=True, delay_us=DELAY_US, **kw):
         assert "libdistml_ps" in d["libs"], d
         if double:
             assert d["double_calls"] > 0, d  # the collectives ran through the stand-in
+            # the communicator pins RCCL's channel count (ncclCommInitRankConfig)
+            assert d["ctas"] == [128, 128], d
     return outs
 
 
@@ -103,11 +105,42 @@ def test_native_group_full_range(tmp_path, oracle, world, vt, rows, cols, pieces
     if cols % 4 == 0:  # whole 16-B vectors: the speculative pre-reduce runs
         for r in range(world):
             st = np.load(tmp_path / f"full_{r}.npz")["stats"].tolist()
-            assert st == [G.CALLS, 1 if r == 0 else 0], (r, st)
+            assert st[:2] == [G.CALLS, 1 if r == 0 else 0], (r, st)
     if vt == 0:
         assert np.array_equal(got, o.data)
     else:
-        G.check_full_range(got, o, init, all_b, rows, cols)
+        G.check_full_range(got, o, init, all_b, rows, cols, f"native world {world} pieces {pieces} cols {cols}")
+
+
+# (world, vt, rows, pieces, ident): 200 columns (800-B rows, the flat kernels, 10 rows per
+# k_flat_ident wave); 1198 rows over 3 ranks: step 400, the last shard 2 rows short;
+# pieces 2: 200-row blocks; 999 rows over 2: step 500, pieces 4: 125-row blocks, which a
+# 10-row wave would straddle, so the pieces fall back to k_reduce_flat
+@pytest.mark.parametrize("world,vt,rows,pieces,ident", [
+    (3, 1, 1198, 1, True), (3, 0, 1198, 2, True), (2, 1, 999, 4, False)])
+def test_native_group_ascending_flat_ident(tmp_path, oracle, world, vt, rows, pieces, ident):
+    """full-range calls whose pushes all list the rows in ascending order at a
+    flat width take the all-identity kernel in the pre-reduce pieces (row map: strided
+    row blocks, [rank][row] output, the short last shard's padding rows) — asserted
+    through the pre-reduce counters — or, where a wave would straddle two row blocks,
+    k_reduce_flat. int32 bit-exact, fp32 within the reduce-scatter bound (kat.rs_parity)."""
+    cols, W = 200, 4
+    run_ranks(tmp_path, world, "asc", vt=vt, rows=rows, cols=cols, pushes=W, pieces=pieces)
+    for r in range(world):
+        st = np.load(tmp_path / f"asc_{r}.npz")["stats"].tolist()
+        assert st[:2] == [G.CALLS, 0], (r, st)
+        assert st[2] == (G.CALLS * pieces if ident else 0), (r, st)
+    got = shards(tmp_path, "asc", world, shape=(rows, cols))
+    init = G._init(vt, rows, cols)
+    o = oracle.OracleStore(1, 0, vt, 0, rows - 1, cols)
+    o.data[:] = init
+    all_b = [b for c in range(G.CALLS) for r in range(world) for b in G._asc_buckets(oracle, vt, r, W, rows, cols, c)]
+    for b in all_b:
+        assert o.push(b.tobytes()) == 0
+    if vt == 0:
+        assert np.array_equal(got, o.data)
+    else:
+        G.check_full_range(got, o, init, all_b, rows, cols, f"native ascending world {world} pieces {pieces}")
 
 
 @pytest.mark.parametrize("world,vt", [(2, 1), (3, 1), (4, 1), (3, 0)])
