@@ -112,14 +112,6 @@ namespace {
 
 constexpr int kRsChannels = 128;  // RCCL CTAs (channels) per collective of the group
 
-// A/B switch for the race check (scripts/build_ab.sh nofix -DDML_AB_NO_FAIL_ORDER=1): the
-// local-failure path without its stream orders, to show the asynchronous RCCL stand-in
-// (tests/rccl_double) catches the race they close
-#ifdef DML_AB_NO_FAIL_ORDER
-constexpr bool kFailOrder = false;
-#else
-constexpr bool kFailOrder = true;
-#endif
 
 // The oldest pending call: read its verdict (a failed speculation re-runs its
 // pieces exactly), then reduce-scatter its partial on the communication stream
@@ -152,7 +144,7 @@ int finish_front(dml_group* g) {
         // that failed in _begin_ctx skipped the host wait for it
         (void)hipStreamSynchronize(g->cstream);
         if (c.h) (void)dml_prereduce_stream_wait(c.h, g->rstream);
-        if (kFailOrder) (void)hipStreamWaitEvent(g->rstream, g->applied[c.set], 0);
+        (void)hipStreamWaitEvent(g->rstream, g->applied[c.set], 0);
         (void)hipMemsetAsync(part, 0, (size_t)(W * S * C) * g->vbytes, g->rstream);
     }
     int crc = DML_OK;  // the collective's own status
@@ -167,7 +159,7 @@ int finish_front(dml_group* g) {
         // the set stays busy until the zero-contribution reduce-scatter has read the
         // partial and written recv: its next use (two calls on) waits on applied[set],
         // which for this call is the scatter itself (there is no apply)
-        if (W > 1 && kFailOrder) {
+        if (W > 1) {
             (void)hipEventRecord(g->rs_done[c.set], g->rstream);
             (void)hipEventRecord(g->applied[c.set], g->rstream);
         }

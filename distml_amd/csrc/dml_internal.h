@@ -310,10 +310,7 @@ bool use_flat(int vtype, int mode, int32_t cols, const Batch& bt, int nb, int64_
 // the host has seen, after its index, to be all identity — every push lists every
 // row as record r = row r (flat_ident_ok), no cutoff, no repeated row. Its waves
 // verify every key; a mismatch clears ctrl->spec_ok as k_reduce_flat does.
-#ifndef DML_AB_FI_NW
-#define DML_AB_FI_NW 8
-#endif
-constexpr int kFlatIdentWaves = DML_AB_FI_NW;
+constexpr int kFlatIdentWaves = 8;  // waves per block (their rows written after one block barrier)
 hipError_t launch_ada_ident(void* shard, int64_t rows, int32_t cols, const Batch& bt, int nb, int64_t stride, int K,
                             const AdaArgs& ada, hipStream_t st, int64_t* ncand_out, LaunchEv ev = {});
 hipError_t launch_flat_ident(int vtype, int mode, void* shard, int64_t rows, int32_t cols, const Batch& bt, int nb,

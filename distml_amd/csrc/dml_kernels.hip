@@ -25,64 +25,12 @@
 
 namespace dml {
 
-// A/B switches (scripts/build_ab.sh): k_ada_flat's block barrier before its write-back,
-// and its block size in waves. Measured off / 4 (config-4 AdaGrad leg, one box, 2
-// rounds: 9158-9217 us without the barrier, 9270-9288 with it at 4 waves, 10.3-10.9 ms
-// at 8 and 12 waves, where fewer blocks fit a CU): the waves of an AdaGrad block end
-// unevenly, and waiting for the slowest costs more than the write burst saves.
-#ifdef DML_AB_ADA_BURST
-constexpr bool kAdaBurst = true;
-#else
-constexpr bool kAdaBurst = false;
-#endif
-// (A/B) k_ada_ident (NOXCD_IDENT) / k_flat_ident (FI_NOXCD) blocks in dispatch order instead of
-// XCD-contiguous; k_flat_ident's ring depth, vectors per lane, waves per block (FI_D, FI_J, FI_NW)
-#ifdef DML_AB_NOXCD_IDENT
-constexpr bool kIdentXcd = false;
-#else
-constexpr bool kIdentXcd = true;
-#endif
-#ifdef DML_AB_FI_NOXCD
-constexpr bool kFlatIdentXcd = false;
-#else
-constexpr bool kFlatIdentXcd = true;
-#endif
-#ifndef DML_AB_FI_J
-#define DML_AB_FI_J 8
-#endif
-#ifndef DML_AB_FI_D
-#define DML_AB_FI_D 3
-#endif
-// (A/B) k_reduce_rows DEPTH 3 for rows of >= 4 chunks (config 5): waves per block, rows per wave
-#ifndef DML_AB_C5_WPB
-#define DML_AB_C5_WPB 2
-#endif
-#ifndef DML_AB_C5_RPW
-#define DML_AB_C5_RPW 4
-#endif
-#ifndef DML_AB_C5_BPC
-#define DML_AB_C5_BPC 0
-#endif
-constexpr int kC5Wpb = DML_AB_C5_WPB, kC5Rpw = DML_AB_C5_RPW, kC5Bpc = DML_AB_C5_BPC;  // BPC: blocks per CU cap
-// (A/B) k_reduce_rows DEPTH 3: minimum waves per SIMD the register allocation must allow
-#ifndef DML_AB_D3_WAVES
-#define DML_AB_D3_WAVES 1
-#endif
-constexpr int kD3Waves = DML_AB_D3_WAVES;
-#ifndef DML_AB_AI_NW
-#define DML_AB_AI_NW 2
-#endif
-#ifndef DML_AB_AI_BPC
-#define DML_AB_AI_BPC 0
-#endif
-#ifdef DML_AB_AI_BAR
-constexpr bool kAiBar = true;
-#else
-constexpr bool kAiBar = false;
-#endif
-#ifndef DML_AB_ADA_NW
-#define DML_AB_ADA_NW 4
-#endif
+// Shapes measured against their alternatives (alternating builds on one box, DESIGN.md
+// §4 and profiles/r05_ab_*.txt); the rejected variants (block barriers before the
+// write-back, dispatch-order blocks, occupancy caps) are in the history, not here.
+constexpr int kC5Wpb = 2, kC5Rpw = 4;  // k_reduce_rows DEPTH 3 (config 5): waves per block, rows per wave
+constexpr int kD3Waves = 1;            // DEPTH 3: minimum waves per SIMD its registers must allow
+constexpr int kAdaFlatWaves = 4;       // k_ada_flat: waves per block
 
 __host__ __device__ inline uint64_t splitmix64_dev(uint64_t x) {
     uint64_t z = x + 0x9E3779B97F4A7C15ull;
@@ -1267,7 +1215,7 @@ __global__ __launch_bounds__(NW * 64) void k_flat_ident(T* __restrict__ shard, i
     static_assert(MODE == kAdd || MODE == kPreReduce, "plain sums only");
     const int lane = threadIdx.x & 63;
     const int wid = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-    const int64_t t0 = ((kFlatIdentXcd ? xcd_block() : (int64_t)blockIdx.x) * NW + wid) * R;
+    const int64_t t0 = (xcd_block() * NW + wid) * R;
     // every wave reaches the block barrier below: a wave past the last row, or behind
     // a predecessor that needs the host first, does no work and writes nothing
     const bool live = t0 < rows && !(bt.prev && ctrl_abnormal(bt.prev));
@@ -1522,9 +1470,6 @@ __global__ __launch_bounds__(NW * 64) void k_ada_flat(float* __restrict__ shard,
             }
         }
     } while (0);
-    // (A/B, off: kAdaBurst) every wave of the block has read and updated its rows before
-    // the block's writes (data, delta, alpha: a third of the kernel's bytes) leave the CU
-    if (kAdaBurst) __syncthreads();
     if (live) {
         // write-back of the touched vectors: data, delta, alpha where the last delta
         // a push left above 1 sets it (FloatMatrixStoreAdaGrad.java:268-272), and
@@ -1576,145 +1521,6 @@ __global__ __launch_bounds__(NW * 64) void k_ada_flat(float* __restrict__ shard,
     }
 }
 
-// k_ada_ident: k_ada_flat for the AdaGrad chunks the host has seen to be all identity
-// after the index (every push full-range with record r = row r, checked record by
-// record before the launch; no cutoff, no repeated row: config 4's AdaGrad steady
-// state). Same per-element arithmetic, order and maxDelta candidates as k_ada_flat
-// (bit for bit), with nothing else in it:
-//  - data / delta / alpha offsets from the wave's first row, and record offsets from
-//    its first record, are 32-bit per-lane constants that every array and push shares
-//    (buffer loads at a wave-uniform base; a lane without a vector reads zeros from the
-//    range check), no slot rows, no LDS;
-//  - every load of the wave (data, delta, all pushes) is issued before the first add;
-//  - the maxDelta candidate is reduced per wave (one entry per wave in ada.cand, no
-//    block barrier): a wave leaves as soon as its own rows are written.
-template <int J, int NW, int NB>
-__global__ __launch_bounds__(NW * 64) void k_ada_ident(float* __restrict__ shard, int64_t rows, int32_t cols, int32_t R,
-                                                   const Batch bt, int64_t stride, int K, AdaArgs ada) {
-    constexpr int VEC = 4, NBMAX = NB, nb = NB;  // NB pushes (1..4): their loads all in flight
-    const int lane = threadIdx.x & 63;
-    const int wid = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-    const int64_t t0 = ((kIdentXcd ? xcd_block() : (int64_t)blockIdx.x) * NW + wid) * R;
-    float cand_v = 0.f;
-    uint64_t cand_p = kNoPos;
-    bool cand_ok = false;
-    const bool live = t0 < rows && !(bt.prev && ctrl_abnormal(bt.prev));
-    if (kAiBar || live) {
-        const int nrow = !live ? 0 : (int)(rows - t0 < (int64_t)R ? rows - t0 : (int64_t)R);
-        const int NV = cols / VEC, nvec = nrow * NV;
-        uint32_t eoff[J], roff[J];
-        int rc[J];  // (row << 16 | vector within the row)
-#pragma unroll
-        for (int j = 0; j < J; ++j) {
-            const int v = j * 64 + lane;
-            const int rl = v / NV, cv = v - rl * NV;
-            const bool on = v < nvec;
-            rc[j] = (rl << 16) | cv;
-            eoff[j] = on ? (uint32_t)((rl * cols + cv * VEC) * 4) : kBufOff;
-            roff[j] = on ? (uint32_t)(rl * stride + K + cv * 16) : kBufOff;
-        }
-        const uint32_t espan = (uint32_t)(nrow * cols * 4), rspan = (uint32_t)(nrow * stride);
-        const int64_t e0 = t0 * (int64_t)cols;
-        const __amdgpu_buffer_rsrc_t ds = buf_rsrc(shard + e0, espan);
-        const __amdgpu_buffer_rsrc_t dd = buf_rsrc(ada.delta + e0, espan);
-        float acc[J][VEC], dl[J][VEC], lg[J][VEC], rv[J][VEC];
-        int rb[J][VEC];  // push of the element's last strict rise (-1: none)
-        u32x4 raw[NBMAX][J];
-#pragma unroll
-        for (int j = 0; j < J; ++j) {
-            unpack<float>(ldb16_nt(ds, eoff[j]), acc[j]);
-            unpack<float>(ldb16_nt(dd, eoff[j]), dl[j]);
-        }
-#pragma unroll
-        for (int b = 0; b < NBMAX; ++b)
-            if (b < nb) {
-                const __amdgpu_buffer_rsrc_t rs = buf_rsrc(bt.base[b] + t0 * stride, rspan);
-#pragma unroll
-                for (int j = 0; j < J; ++j) raw[b][j] = ldb16_nt(rs, roff[j]);
-            }
-#pragma unroll
-        for (int j = 0; j < J; ++j)
-#pragma unroll
-            for (int e = 0; e < VEC; ++e) {
-                lg[j][e] = 0.f;
-                rv[j][e] = 0.f;
-                rb[j][e] = -1;
-            }
-        // k_ada_flat's upd(), pushes in order
-#pragma unroll
-        for (int b = 0; b < NBMAX; ++b)
-            if (b < nb)
-#pragma unroll
-                for (int j = 0; j < J; ++j) {
-                    float u[VEC];
-                    unpack<float>(raw[b][j], u);
-#pragma unroll
-                    for (int e = 0; e < VEC; ++e) {
-                        acc[j][e] = __fadd_rn(acc[j][e], u[e]);
-                        const float nd = __fadd_rn(dl[j][e], __fmul_rn(u[e], u[e]));
-                        if (nd > dl[j][e]) { rv[j][e] = nd; rb[j][e] = b; }
-                        if (nd > 1.0f) lg[j][e] = nd;
-                        dl[j][e] = nd;
-                    }
-                }
-        // (A/B, off: kAiBar) the block's writes leave together
-        if (kAiBar) __syncthreads();
-        const __amdgpu_buffer_rsrc_t da = buf_rsrc(ada.alpha + e0, espan);
-        const uint64_t bi0 = (uint64_t)bt.bidx[0], bi1 = NB > 1 ? (uint64_t)bt.bidx[NB > 1 ? 1 : 0] : 0,
-                       bi2 = NB > 2 ? (uint64_t)bt.bidx[NB > 2 ? 2 : 0] : 0, bi3 = NB > 3 ? (uint64_t)bt.bidx[NB > 3 ? 3 : 0] : 0;
-#pragma unroll
-        for (int j = 0; j < J; ++j) {
-            if (eoff[j] == kBufOff) continue;
-            __builtin_amdgcn_raw_buffer_store_b128(pack<float>(acc[j]), ds, (int)eoff[j], 0, 2);
-            __builtin_amdgcn_raw_buffer_store_b128(pack<float>(dl[j]), dd, (int)eoff[j], 0, 2);
-            // alpha where the last delta a push left above 1 sets it
-            // (FloatMatrixStoreAdaGrad.java:268-272)
-            float na[VEC];
-            bool all_a = true, any_a = false;
-#pragma unroll
-            for (int e = 0; e < VEC; ++e) {
-                na[e] = 0.f;
-                if (lg[j][e] > 1.0f) {
-                    na[e] = (float)((double)ada.initial_alpha / ((double)ada.factor * sqrt((double)lg[j][e])));
-                    if (na[e] < ada.min_alpha) na[e] = ada.min_alpha;
-                    any_a = true;
-                } else {
-                    all_a = false;
-                }
-            }
-            if (all_a) {
-                __builtin_amdgcn_raw_buffer_store_b128(pack<float>(na), da, (int)eoff[j], 0, 2);
-            } else if (any_a) {
-#pragma unroll
-                for (int e = 0; e < VEC; ++e)
-                    if (lg[j][e] > 1.0f)
-                        __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(na[e]), da, (int)(eoff[j] + 4 * e), 0, 0);
-            }
-            const int rl = rc[j] >> 16, cv = rc[j] & 0xFFFF;
-#pragma unroll
-            for (int e = 0; e < VEC; ++e) {
-                if (rb[j][e] < 0) continue;
-                const int g = rb[j][e];  // (a select chain, not a per-lane index into the kernarg table)
-                const uint64_t gb = g == 0 ? bi0 : g == 1 ? bi1 : g == 2 ? bi2 : bi3;
-                const uint64_t p = pos_of(gb,
-                                          (uint64_t)((t0 + rl) * stride + K + (int64_t)(cv * VEC + e) * 4));
-                if (!cand_ok || rv[j][e] > cand_v || (rv[j][e] == cand_v && p < cand_p)) {
-                    cand_ok = true;
-                    cand_v = rv[j][e];
-                    cand_p = p;
-                }
-            }
-        }
-    }
-    cand_block_best<1>(cand_ok, cand_v, cand_p);
-    if (lane == 0) {
-        DeltaCand c;
-        c.value = cand_v;
-        c.valid = cand_ok;
-        c.pos = cand_p;
-        ada.cand[blockIdx.x * (int64_t)NW + wid] = c;
-    }
-}
 
 // Occupancy cap: dynamic LDS (unused by the kernels) so that at most `bpc`
 // 256-thread blocks fit on a CU (160 KiB of LDS per CU). 0 = no cap.
@@ -1817,7 +1623,7 @@ static hipError_t launch_auto(void* shard, int64_t rows, int32_t cols, const Bat
             if (nchunks >= 4)
                 return launch_reduce_t<T, MODE, 3, false, kC5Wpb, 1, 4, kC5Rpw>(shard, rows, cols, bt, nb, stride, K,
                                                                                slot, rowflag, ctrl, tail_cut, ada, st,
-                                                                               nblocks_out, ev, rm, kC5Bpc);
+                                                                               nblocks_out, ev, rm);
             if (cols % (64 * VEC * 2) == 0) return DML_LFN(1, 2, 4);
             if (nchunks >= 2) return DML_LN(3, 2, 4);
             if (cols % (64 * VEC) == 0) return DML_LFN(1, 1, 4);
@@ -1878,7 +1684,7 @@ static hipError_t launch_flat(void* shard, int64_t rows, int32_t cols, const Bat
 // pushes in flight, 8-wave blocks (one per CU at 2 waves per SIMD): the best of the
 // shapes scripts/ubench_flat.hip measured (config 4: 0.768 of 8 TB/s against 0.727
 // for k_reduce_flat's loop on one box).
-constexpr int kFlatIdentJ = DML_AB_FI_J;  // 16-B vectors per lane
+constexpr int kFlatIdentJ = 8;  // 16-B vectors per lane
 
 int flat_ident_rows_per_wave(int vtype, int32_t cols) {
     const int NV = cols / (vtype == kF64 ? 2 : 4);
@@ -1889,7 +1695,7 @@ template <typename T, int MODE>
 static hipError_t launch_flat_ident_t(void* shard, int64_t rows, int32_t cols, const Batch& bt, int nb,
                                       int64_t stride, int K, Ctrl* ctrl, hipStream_t st, int64_t* nblocks_out,
                                       LaunchEv ev, RowMap rm) {
-    constexpr int VEC = Elem<T>::VEC, J = kFlatIdentJ, D = DML_AB_FI_D, NW = kFlatIdentWaves;
+    constexpr int VEC = Elem<T>::VEC, J = kFlatIdentJ, D = 3, NW = kFlatIdentWaves;  // D: pushes in flight
     const int NV = cols / VEC;
     const int R = std::max(1, std::min(16, J * 64 / NV));
     const int64_t nblocks = ((rows + R - 1) / R + NW - 1) / NW;
@@ -1974,62 +1780,153 @@ static hipError_t launch_ada_flat_t(void* shard, int64_t rows, int32_t cols, con
     return hipGetLastError();
 }
 
-// k_ada_ident launch: the all-identity AdaGrad chunks of the flat shape (the host
-// checked the index's Ctrl, as for k_flat_ident), at most 4 pushes. One maxDelta
-// candidate per wave: *ncand_out = the waves launched (<= reduce_blocks(), the
-// candidate buffer's size).
-// 8 vectors per lane (10 rows of 800 B per wave), 2-wave blocks: the k_ada_ident shapes
-// measured on one box (J 2/4/8 x 1/2/4/8 waves): J 8 at 1-2 waves and J 2 at 2-4 waves
-// 8.20-8.43 ms, J 4 at any block size 8.69-8.81 ms (its 5-row waves split 64-B sectors)
-#ifndef DML_AB_AI_J
-#define DML_AB_AI_J 8
-#endif
-constexpr int kAdaIdentJ = DML_AB_AI_J, kAdaIdentWaves = DML_AB_AI_NW;
+// k_ada_ident: k_ada_flat for the AdaGrad chunks the host has seen to be all identity
+// after the index (every push full-range with record r = row r, checked record by
+// record before the launch; no cutoff, no repeated row: config 4's AdaGrad steady
+// state), at most 4 pushes, laid out as the plain data / delta stream: a thread owns U
+// 16-B vectors of the shard, 256 apart inside its block's 256·U-vector tile (each
+// wave's stores are whole 1 KiB runs), wherever rows begin; a vector's record offset
+// (row = e / cols) is computed per vector. Every load (data, delta, NB pushes) is in
+// flight before the first add. The same per-element arithmetic, order, alpha and
+// maxDelta candidates as k_ada_flat (bit for bit; the candidate is reduced per block,
+// max value then lowest position). One vector per thread (U = 1, 54-60 VGPRs, full
+// occupancy) ran 8.58-8.61 ms on the config-4 AdaGrad leg against 9.30-9.33 ms for the
+// previous row-per-wave shape (8 vectors per lane, 10 rows per wave, 2-wave blocks, 170
+// VGPRs) and 8.41-8.95 ms for 2 or 4 vectors, alternating builds on one box
+// (profiles/r06_ab_ada_vec.txt): 0.96 of the plain stream of the same bytes.
+constexpr int kAdaIdentU = 1;  // 16-B vectors per thread
 
-template <int NB>
-static hipError_t launch_ada_ident_t(void* shard, int64_t rows, int32_t cols, int R, int64_t nblocks, const Batch& bt,
+template <int U, int NB>
+__global__ __launch_bounds__(256) void k_ada_ident(float* __restrict__ shard, int64_t nvec, int32_t cols,
+                                                   const Batch bt, int64_t stride, int K, AdaArgs ada) {
+    constexpr int VEC = 4;
+    const int64_t v0 = xcd_block() * (256 * U) + threadIdx.x;
+    float cand_v = 0.f;
+    uint64_t cand_p = kNoPos;
+    bool cand_ok = false;
+    const bool live = !(bt.prev && ctrl_abnormal(bt.prev));
+    int64_t roff[U];
+    bool on[U];
+    float acc[U][VEC], dl[U][VEC], lg[U][VEC], rv[U][VEC];
+    int rb[U][VEC];  // push of the element's last strict rise (-1: none)
+    u32x4 raw[NB][U];
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+        const int64_t v = v0 + u * 256, e = v * VEC;
+        on[u] = live && v < nvec;
+        roff[u] = (e / cols) * stride + K + (e % cols) * 4;
+        const u32x4 z{0u, 0u, 0u, 0u};
+        unpack<float>(on[u] ? ldg16_nt((const uint8_t*)shard + v * 16) : z, acc[u]);
+        unpack<float>(on[u] ? ldg16_nt((const uint8_t*)ada.delta + v * 16) : z, dl[u]);
+    }
+#pragma unroll
+    for (int b = 0; b < NB; ++b)
+#pragma unroll
+        for (int u = 0; u < U; ++u) raw[b][u] = on[u] ? ldg16_nt(bt.base[b] + roff[u]) : u32x4{0u, 0u, 0u, 0u};
+#pragma unroll
+    for (int u = 0; u < U; ++u)
+#pragma unroll
+        for (int e = 0; e < VEC; ++e) {
+            lg[u][e] = 0.f;
+            rv[u][e] = 0.f;
+            rb[u][e] = -1;
+        }
+    // k_ada_flat's upd(), pushes in order
+#pragma unroll
+    for (int b = 0; b < NB; ++b)
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            float g[VEC];
+            unpack<float>(raw[b][u], g);
+#pragma unroll
+            for (int e = 0; e < VEC; ++e) {
+                acc[u][e] = __fadd_rn(acc[u][e], g[e]);
+                const float nd = __fadd_rn(dl[u][e], __fmul_rn(g[e], g[e]));
+                if (nd > dl[u][e]) { rv[u][e] = nd; rb[u][e] = b; }
+                if (nd > 1.0f) lg[u][e] = nd;
+                dl[u][e] = nd;
+            }
+        }
+    const uint64_t bi0 = (uint64_t)bt.bidx[0], bi1 = NB > 1 ? (uint64_t)bt.bidx[NB > 1 ? 1 : 0] : 0,
+                   bi2 = NB > 2 ? (uint64_t)bt.bidx[NB > 2 ? 2 : 0] : 0, bi3 = NB > 3 ? (uint64_t)bt.bidx[NB > 3 ? 3 : 0] : 0;
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+        if (!on[u]) continue;
+        const int64_t v = v0 + u * 256;
+        stg16_nt((uint8_t*)shard + v * 16, pack<float>(acc[u]));
+        stg16_nt((uint8_t*)ada.delta + v * 16, pack<float>(dl[u]));
+        // alpha where the last delta a push left above 1 sets it (FloatMatrixStoreAdaGrad.java:268-272)
+        float na[VEC];
+        bool all_a = true, any_a = false;
+#pragma unroll
+        for (int e = 0; e < VEC; ++e) {
+            na[e] = 0.f;
+            if (lg[u][e] > 1.0f) {
+                na[e] = (float)((double)ada.initial_alpha / ((double)ada.factor * sqrt((double)lg[u][e])));
+                if (na[e] < ada.min_alpha) na[e] = ada.min_alpha;
+                any_a = true;
+            } else {
+                all_a = false;
+            }
+        }
+        if (all_a) {
+            stg16_nt((uint8_t*)ada.alpha + v * 16, pack<float>(na));
+        } else if (any_a) {
+#pragma unroll
+            for (int e = 0; e < VEC; ++e)
+                if (lg[u][e] > 1.0f) ada.alpha[v * VEC + e] = na[e];
+        }
+#pragma unroll
+        for (int e = 0; e < VEC; ++e) {
+            if (rb[u][e] < 0) continue;
+            const int g = rb[u][e];  // (a select chain, not a per-lane index into the kernarg table)
+            const uint64_t gb = g == 0 ? bi0 : g == 1 ? bi1 : g == 2 ? bi2 : bi3;
+            const uint64_t p = pos_of(gb, (uint64_t)(roff[u] + e * 4));
+            if (!cand_ok || rv[u][e] > cand_v || (rv[u][e] == cand_v && p < cand_p)) {
+                cand_ok = true;
+                cand_v = rv[u][e];
+                cand_p = p;
+            }
+        }
+    }
+    cand_block_best<4>(cand_ok, cand_v, cand_p);
+    if (threadIdx.x == 0) {
+        DeltaCand c;
+        c.value = cand_v;
+        c.valid = cand_ok;
+        c.pos = cand_p;
+        ada.cand[blockIdx.x] = c;
+    }
+}
+
+template <int U, int NB>
+static hipError_t launch_ada_ident_t(void* shard, int64_t nvec, int32_t cols, int64_t nblocks, const Batch& bt,
                                      int64_t stride, int K, const AdaArgs& ada, hipStream_t st, LaunchEv ev) {
-    constexpr int J = kAdaIdentJ, NW = kAdaIdentWaves;
-    static const std::string kn = kname("k_ada_ident", J, NW, NB);
+    static const std::string kn = kname("k_ada_ident", U, NB);
     g_kernel_name = kn.c_str();
-    const unsigned lds = lds_for_blocks_per_cu(DML_AB_AI_BPC);  // (A/B: occupancy cap, 0 = none)
     if (ev.start || ev.stop)
-        hipExtLaunchKernelGGL((k_ada_ident<J, NW, NB>), dim3((unsigned)nblocks), dim3(NW * 64), lds, st, ev.start,
-                              ev.stop, 0, (float*)shard, rows, cols, R, bt, stride, K, ada);
+        hipExtLaunchKernelGGL((k_ada_ident<U, NB>), dim3((unsigned)nblocks), dim3(256), 0, st, ev.start, ev.stop, 0,
+                              (float*)shard, nvec, cols, bt, stride, K, ada);
     else
-        hipLaunchKernelGGL((k_ada_ident<J, NW, NB>), dim3((unsigned)nblocks), dim3(NW * 64), lds, st, (float*)shard,
-                           rows, cols, R, bt, stride, K, ada);
+        hipLaunchKernelGGL((k_ada_ident<U, NB>), dim3((unsigned)nblocks), dim3(256), 0, st, (float*)shard, nvec, cols,
+                           bt, stride, K, ada);
     return hipGetLastError();
 }
 
-// Rows per wave and blocks of a k_ada_ident launch. A wave's rows span a whole number of
-// 64-B sectors where any count up to its vectors allows: its non-temporal data / delta
-// stores then never share a sector with a neighbouring wave's (config-4 AdaGrad, 800-B
-// rows: 5 rows = 4 000 B ran 8.69-8.80 ms, 2 or 10 rows 8.20-8.43 ms, one box, 2 rounds).
-static int ada_ident_rows_per_wave(int32_t cols) {
-    const int rmax = std::max(1, std::min(16, kAdaIdentJ * 64 / (cols / 4)));
-    for (int r = rmax; r > 1; --r)
-        if ((int64_t)r * cols * 4 % 64 == 0) return r;
-    return rmax;
-}
-static int64_t ada_ident_blocks(int64_t rows, int32_t cols) {
-    const int R = ada_ident_rows_per_wave(cols);
-    return ((rows + R - 1) / R + kAdaIdentWaves - 1) / kAdaIdentWaves;
-}
-
+// One maxDelta candidate per block: *ncand_out = the blocks launched (<= reduce_blocks(),
+// the candidate buffer's size).
 hipError_t launch_ada_ident(void* shard, int64_t rows, int32_t cols, const Batch& bt, int nb, int64_t stride, int K,
                             const AdaArgs& ada, hipStream_t st, int64_t* ncand_out, LaunchEv ev) {
-    constexpr int NW = kAdaIdentWaves;
     if (nb <= 0 || nb > 4 || cols % 4 || (int64_t)cols * 4 >= 4096) return hipErrorInvalidValue;
-    const int R = ada_ident_rows_per_wave(cols);
-    const int64_t nblocks = ada_ident_blocks(rows, cols);
-    if (ncand_out) *ncand_out = nblocks * NW;
+    constexpr int U = kAdaIdentU;
+    const int64_t nvec = rows * cols / 4, nblocks = (nvec + 256 * U - 1) / (256 * U);
+    if (ncand_out) *ncand_out = nblocks;
     if (nblocks <= 0) return hipSuccess;
     switch (nb) {
-        case 1: return launch_ada_ident_t<1>(shard, rows, cols, R, nblocks, bt, stride, K, ada, st, ev);
-        case 2: return launch_ada_ident_t<2>(shard, rows, cols, R, nblocks, bt, stride, K, ada, st, ev);
-        case 3: return launch_ada_ident_t<3>(shard, rows, cols, R, nblocks, bt, stride, K, ada, st, ev);
-        default: return launch_ada_ident_t<4>(shard, rows, cols, R, nblocks, bt, stride, K, ada, st, ev);
+        case 1: return launch_ada_ident_t<U, 1>(shard, nvec, cols, nblocks, bt, stride, K, ada, st, ev);
+        case 2: return launch_ada_ident_t<U, 2>(shard, nvec, cols, nblocks, bt, stride, K, ada, st, ev);
+        case 3: return launch_ada_ident_t<U, 3>(shard, nvec, cols, nblocks, bt, stride, K, ada, st, ev);
+        default: return launch_ada_ident_t<U, 4>(shard, nvec, cols, nblocks, bt, stride, K, ada, st, ev);
     }
 }
 
@@ -2040,7 +1937,7 @@ hipError_t launch_ada_ident(void* shard, int64_t rows, int32_t cols, const Batch
 static hipError_t launch_ada_flat(void* shard, int64_t rows, int32_t cols, const Batch& bt, int nb, int64_t stride,
                                   int K, const int32_t* slot, const uint32_t* rowflag, Ctrl* ctrl, uint64_t tail_cut,
                                   const AdaArgs& ada, hipStream_t st, int64_t* nblocks_out, LaunchEv ev) {
-    return launch_ada_flat_t<4, 2, DML_AB_ADA_NW>(shard, rows, cols, bt, nb, stride, K, slot, rowflag, ctrl, tail_cut,
+    return launch_ada_flat_t<4, 2, kAdaFlatWaves>(shard, rows, cols, bt, nb, stride, K, slot, rowflag, ctrl, tail_cut,
                                                   ada, st, nblocks_out, ev);
 }
 
@@ -2060,12 +1957,12 @@ bool reduce_clears_slots(int vtype, int mode, int32_t cols) {
 int64_t reduce_blocks(int vtype, int64_t rows, int32_t cols) {
     // The most maxDelta candidates one AdaGrad apply writes (the candidate buffer's size):
     // k_reduce runs one row and one chunk per wave, 4 waves per block, one candidate per
-    // block; k_ada_flat fewer; k_ada_ident one per wave of its (rounded-up) grid.
+    // block; k_ada_flat fewer; k_ada_ident one per block of 256·U vectors.
     const int VEC = vtype == kF64 ? 2 : 4;
     const int64_t nchunks = (cols + 64 * VEC - 1) / (64 * VEC);
     int64_t n = (rows * nchunks + 3) / 4;
     if (vtype == kF32 && cols >= 4 && cols % 4 == 0 && (int64_t)cols * 4 < 4096)
-        n = std::max<int64_t>(n, ada_ident_blocks(rows, cols) * kAdaIdentWaves);
+        n = std::max(n, (rows * cols / 4 + 256 * kAdaIdentU - 1) / (256 * kAdaIdentU));
     return n;
 }
 
@@ -2286,10 +2183,7 @@ __global__ __launch_bounds__(256) void k_apply_dense_i32chk(int32_t* __restrict_
 // that fills every free wave slot keeps the pre-reduce's next blocks from being
 // placed (its waves need most of a SIMD's VGPRs). kApplyBlocks bounds it to two
 // blocks per CU; it still moves a config-2 shard's 192 MB well inside one call.
-#ifndef DML_AB_APPLY_BLOCKS
-#define DML_AB_APPLY_BLOCKS 512
-#endif
-constexpr unsigned kApplyBlocks = DML_AB_APPLY_BLOCKS;
+constexpr unsigned kApplyBlocks = 512;
 
 hipError_t launch_apply_dense_i32chk(int32_t* shard, const int32_t* src, int64_t n, unsigned long long* neg,
                                      hipStream_t st) {

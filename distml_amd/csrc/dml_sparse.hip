@@ -1043,12 +1043,9 @@ SpPlan sparse_plan(const Batch& bt, int nb, int64_t rows) {
 // mean, 2 959 of 2 097, into its fullest big leaf of 2^16 rows; fuller ones take the
 // exact replay). The 8 slices (pushes p % 8) must carry near-equal shares, since
 // slice x's tiles all run on one XCD.
-#ifndef DML_AB_NOBIG
-#define DML_AB_NOBIG 0
-#endif
 void sparse_plan_big(SpPlan& pl, const Batch& bt, int64_t rows) {
     pl.big = 0;
-    if (DML_AB_NOBIG || !pl.compact || pl.nb < kSpSlices || pl.nrec <= 0) return;
+    if (!pl.compact || pl.nb < kSpSlices || pl.nrec <= 0) return;
     int BL = 0;
     while (BL < 24 && ((rows + ((int64_t)1 << BL) - 1) >> BL) > kSpBigBins) ++BL;
     const int64_t nbig = (rows + ((int64_t)1 << BL) - 1) >> BL;

@@ -33,6 +33,8 @@
 
 using namespace dml;
 
+constexpr size_t kSmallStoreBytes = (size_t)1 << 20;  // shards up to 1 MiB: high-priority streams
+
 static thread_local std::string g_err;
 
 static int set_err(int code, const std::string& msg) {
@@ -47,19 +49,6 @@ int dml::set_error(int code, const std::string& msg) { return set_err(code, msg)
         if (e_ != hipSuccess) return set_err(DML_E_HIP, std::string(#x) + ": " + hipGetErrorString(e_)); \
     } while (0)
 
-// A/B switch (scripts/build_ab.sh nolisted -DDML_AB_NO_LISTED=1): no listed-row skip
-// A/B switch (scripts/build_ab.sh noadaident -DDML_AB_NO_ADA_IDENT=1): AdaGrad's identity
-// chunks through k_ada_flat instead of k_ada_ident
-#ifdef DML_AB_NO_ADA_IDENT
-constexpr bool kAdaIdent = false;
-#else
-constexpr bool kAdaIdent = true;
-#endif
-#ifdef DML_AB_NO_LISTED
-constexpr bool kListedRows = false;
-#else
-constexpr bool kListedRows = true;
-#endif
 
 namespace {
 
@@ -556,7 +545,7 @@ int launch_chunk(dml_store* s, Chunk& c, Workspace& W, const Ctrl* prev) {
         // Sparse-row chunks of k_reduce_rows (some push lists only part of the rows): the
         // index marks the rows any push lists, and the reduce skips the others' shard rows
         c.bt.listed = nullptr;
-        if (kListedRows && !c.spec && !s->adagrad && (reduce_mode(s) == kAdd || reduce_mode(s) == kAddCheckI32) &&
+        if (!c.spec && !s->adagrad && (reduce_mode(s) == kAdd || reduce_mode(s) == kAddCheckI32) &&
             !use_flat(vtype_of(s->desc), reduce_mode(s), s->cols, c.bt, c.nb, s->rows)) {
             bool part = false;
             for (int j = 0; j < c.nb && !part; ++j) part = c.bt.nrec[j] < s->rows;
@@ -573,7 +562,7 @@ int launch_chunk(dml_store* s, Chunk& c, Workspace& W, const Ctrl* prev) {
         // all-identity kernel after the wait below (k_flat_ident)
         W.flat_ident = false;
         // AdaGrad chunks checked record by record (ident_ok) likewise pick k_ada_ident
-        if (((c.spec && reduce_mode(s) == kAdd) || (kAdaIdent && s->adagrad && c.bt.ident_ok)) &&
+        if (((c.spec && reduce_mode(s) == kAdd) || (s->adagrad && c.bt.ident_ok)) &&
             c.tail_cut == kNoPos && use_flat(vtype_of(s->desc), reduce_mode(s), s->cols, c.bt, c.nb, s->rows)) {
             if (!W.hidx) HIPCHK(hipHostMalloc((void**)&W.hidx, sizeof(Ctrl), hipHostMallocDefault));
             W.hidx->cutoff = 0;  // not all-identity unless the copy lands
@@ -1110,8 +1099,17 @@ int dml_store_create_range(const dml_desc* desc, int64_t first_key, int64_t last
         return set_err(DML_E_HIP, std::string(what) + ": " + hipGetErrorString(e));
     };
     hipError_t e;
-    if ((e = hipStreamCreateWithFlags(&s->stream, hipStreamNonBlocking)) != hipSuccess) return fail(e, "stream");
     const size_t nbytes = (size_t)rows * (size_t)s->cols * (size_t)s->V;
+    // A small shard's pushes are latency-bound (a few blocks for microseconds): its
+    // streams take the high priority, so that on a GPU shared with a large store (LDA's
+    // doc-topic totals beside the word-topic rows, LightLDA.scala:238-239) its kernels
+    // are dispatched between the large store's reduce blocks instead of queueing
+    // behind the whole reduce, which would hold up the caller's next push.
+    int prio_lo = 0, prio_hi = 0;
+    if ((e = hipDeviceGetStreamPriorityRange(&prio_lo, &prio_hi)) != hipSuccess) return fail(e, "stream priorities");
+    const int prio = nbytes <= kSmallStoreBytes ? prio_hi : 0;
+    auto mkstream = [&](hipStream_t* st) { return hipStreamCreateWithPriority(st, hipStreamNonBlocking, prio); };
+    if ((e = mkstream(&s->stream)) != hipSuccess) return fail(e, "stream");
     if ((e = hipMalloc(&s->data, nbytes)) != hipSuccess) return fail(e, "shard alloc");
     if ((e = hipMemsetAsync(s->data, 0, nbytes, s->stream)) != hipSuccess) return fail(e, "shard zero");
     if (s->adagrad) {
@@ -1128,8 +1126,8 @@ int dml_store_create_range(const dml_desc* desc, int64_t first_key, int64_t last
     }
     s->slot_bytes = s->is_matrix ? (size_t)rows * kMaxW * sizeof(int32_t) : 0;
     s->ws_bytes = sizeof(Ctrl) + s->slot_bytes + (s->is_matrix ? (size_t)rows * sizeof(uint32_t) : 0);
-    if ((e = hipStreamCreateWithFlags(&s->istream, hipStreamNonBlocking)) != hipSuccess) return fail(e, "index stream");
-    if ((e = hipStreamCreateWithFlags(&s->cstream, hipStreamNonBlocking)) != hipSuccess) return fail(e, "copy stream");
+    if ((e = mkstream(&s->istream)) != hipSuccess) return fail(e, "index stream");
+    if ((e = mkstream(&s->cstream)) != hipSuccess) return fail(e, "copy stream");
     for (Workspace& W : s->ws) {
         if ((e = hipMalloc((void**)&W.base, s->ws_bytes)) != hipSuccess) return fail(e, "workspace alloc");
         W.ctrl = (Ctrl*)W.base;

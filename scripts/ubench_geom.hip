@@ -177,7 +177,7 @@ static void report(const char* label, const Geo& g, const Kern& k, int round, fl
            "\"best_us\": %.1f, \"mean_us\": %.1f, \"frac_best\": %.4f, \"frac_mean\": %.4f}\n",
            label, round, g.W, P, (long long)g.S, g.slab ? "slab" : "separate", k.U, k.D, k.K,
            k.mode == 0 ? "rmw" : k.mode == 1 ? "push reads only" : k.mode == 2 ? "shard+push reads" : "out of place", (int)k.xcd, wshare, best, mean,
-           bytes / best / 1e6 / 8000.0, bytes / mean / 1e6 / 8000.0);
+           bytes / best / 1e3 / 8000.0, bytes / mean / 1e3 / 8000.0);
     fflush(stdout);
 }
 
@@ -229,10 +229,15 @@ int main(int argc, char** argv) {
         Geo a{32, 1, 64 * MiB, true}, b{16, 1, 7630 * MiB, false};
         alloc_geo(a);
         alloc_geo(b);
+        const Kern wide = KN(16, 1, 1, 0, true);  // 16 KiB per wave per push (config 2's k_reduce_rows span)
         for (int r = 0; r < rounds; ++r) {
             float best, mean;
             time_case(a, base, 50, best, mean);
             report("alt g2: 32 x 64 MiB slab", a, base, r, best, mean);
+            time_case(a, wide, 50, best, mean);
+            report("alt g2: 32 x 64 MiB slab", a, wide, r, best, mean);
+            time_case(b, wide, 4, best, mean);
+            report("alt g4: 16 x 8 GB separate", b, wide, r, best, mean);
             time_case(b, base, 4, best, mean);
             report("alt g4: 16 x 8 GB separate", b, base, r, best, mean);
             const Kern oop = KN(4, 4, 1, 3, true);

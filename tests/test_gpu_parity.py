@@ -536,7 +536,7 @@ def test_gather_floor_diag_is_the_plain_row_sum():
     bufs = synth_device_buckets(L, fmt.to_c(), 0, rows, nrec, cols, [70 + b for b in range(6)],
                                 [(a, 13 * b) for b, a in enumerate((7, 9, 11, 13, 17, 19))])
     for b in bufs:
-        rec = b.cpu().numpy().reshape(nrec, 1 + cols).view("<i4")
+        rec = b.cpu().numpy().view("<i4").reshape(nrec, 1 + cols)
         np.add.at(want, rec[:, 0], rec[:, 1:].astype(np.int64))
     ms = bench.gather_floor(L, torch, s, bufs, rows, cols, 0, 4 + 4 * cols, 0, reps=1)
     assert ms > 0
