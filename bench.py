@@ -784,17 +784,30 @@ def sparse_leg(ctx: Ctx, L, steps: int, cpu: bool, cu_split: int = 0):
 
 
 # ---------------------------------------------------------------- config 4 (model level)
-def leg_config4(ctx: Ctx, L, args) -> dict:
+def c4_fit_rows(ctx: Ctx, w: int, cols: int = C4_COLS, cap: int = C4_ROWS) -> int:
+    """The most config-4 rows (<= cap, whole 100 000s) whose W pushes, store (two shard
+    buffers and the workspace ring) and, at N > 1, group buffers fit 90 % of the free HBM."""
+    free = ctx.torch.cuda.mem_get_info()[0]
+    world = ctx.world
+    sharded = world > 1
+    per_row = w * (4 + 4 * cols) + (2 * cols * 4 + 3 * WS_BYTES_PER_ROW) / (world if sharded else 1)
+    if sharded:
+        per_row += (2 * cols * 4 + 2 * cols * 4 / world) + 3 * WS_BYTES_PER_ROW
+    return int(min(cap, 0.9 * free / per_row) // 100_000 * 100_000)
+
+
+def leg_config4(ctx: Ctx, L, args, w: int = 0, rows: int = 0, cpu: bool = True) -> dict:
     """BASELINE config 4: Word2Vec rows 10M x 200 fp32, W full-range pushes per GPU.
     N=1: one store, the ordered batch reduce. N>1: linearSplit(N) shards, ordered
     pre-reduce of the W local pushes, RCCL reduce-scatter, owner apply (plain
-    FloatMatrixStore sum, the config's metric; weak scaling: W pushes per GPU)."""
+    FloatMatrixStore sum, the config's metric; weak scaling: W pushes per GPU).
+    `w` / `rows` override --c4-pushes / 10 M rows (SURVEY §8(d)'s W = 8 and W = 32)."""
     torch = ctx.torch
     from distml_amd import DataDesc, DataStore, KeyRange
     from distml_amd.group import ShardGroup
     from distml_amd.store import DeviceBatch
     world, rank = ctx.world, ctx.rank
-    rows, cols, w = C4_ROWS, C4_COLS, args.c4_pushes
+    rows, cols, w = rows or C4_ROWS, C4_COLS, w or args.c4_pushes
     rec = 4 + 4 * cols
     fmt = DataDesc(DataDesc.DATA_TYPE_MATRIX, DataDesc.KEY_TYPE_INT, DataDesc.ELEMENT_TYPE_FLOAT)
     st = torch.cuda.current_stream().cuda_stream
@@ -881,7 +894,7 @@ def leg_config4(ctx: Ctx, L, args) -> dict:
     del bufs, ptrs
     torch.cuda.synchronize()
     torch.cuda.empty_cache()
-    if world == 1 and not args.no_cpu:
+    if world == 1 and not args.no_cpu and cpu:
         out["cpu_baseline"] = leg_cpu_baseline("4")
     return out
 
@@ -1346,7 +1359,8 @@ def main():
                     help="also run the config-2 workload through dml_group at N = 1 (always at N > 1)")
     ap.add_argument("--group", action="store_true",
                     help="use the sharded pre-reduce/reduce-scatter path even at N=1 (path check)")
-    ap.add_argument("--legs", default="4,5,4a", help="model-level config legs in the line (4, 5, 4a; '' = none)")
+    ap.add_argument("--legs", default="4,4w,5,4a",
+                    help="model-level config legs in the line (4, 4w = config 4 at W 8 and 32, 5, 4a; '' = none)")
     ap.add_argument("--c4-pushes", type=int, default=16, help="config-4 full-range pushes per GPU (8.04 GB each)")
     ap.add_argument("--c4-order", choices=["asc", "perm"], default="asc",
                     help="config-4 row order per push: ascending (SURVEY §8d, keys implicit = row) or permuted")
@@ -1422,6 +1436,11 @@ def main():
     legs = [x for x in args.legs.split(",") if x]
     if "4" in legs:
         line["config4"] = leg_config4(ctx, L, args)
+    if "4w" in legs:
+        # config 4 at W = 8 (one push per GPU of the 8-GPU job) and W = 32 (at
+        # the most rows whose 32 pushes fit beside the store: 32 x 8.04 GB exceed 288 GB at 10 M)
+        line["config4_w8"] = leg_config4(ctx, L, args, w=8, cpu=False)
+        line["config4_w32"] = leg_config4(ctx, L, args, w=32, rows=c4_fit_rows(ctx, 32), cpu=False)
     if "5" in legs:
         line["config5"] = leg_config5(ctx, L, args)
     if "4a" in legs:
