@@ -786,14 +786,17 @@ def sparse_leg(ctx: Ctx, L, steps: int, cpu: bool, cu_split: int = 0):
 # ---------------------------------------------------------------- config 4 (model level)
 def c4_fit_rows(ctx: Ctx, w: int, cols: int = C4_COLS, cap: int = C4_ROWS) -> int:
     """The most config-4 rows (<= cap, whole 100 000s) whose W pushes, store (two shard
-    buffers and the workspace ring) and, at N > 1, group buffers fit 90 % of the free HBM."""
-    free = ctx.torch.cuda.mem_get_info()[0]
+    buffers and the workspace ring) and, at N > 1, group buffers fit the free HBM and
+    still leave the store the headroom it keeps before it allocates its speculative second
+    buffer (1/8 of the device, dml_store.hip): without it the chunks run the key index."""
+    free, total = ctx.torch.cuda.mem_get_info()
+    free = 0.97 * free - max(total / 8, 4 << 30)
     world = ctx.world
     sharded = world > 1
     per_row = w * (4 + 4 * cols) + (2 * cols * 4 + 3 * WS_BYTES_PER_ROW) / (world if sharded else 1)
     if sharded:
         per_row += (2 * cols * 4 + 2 * cols * 4 / world) + 3 * WS_BYTES_PER_ROW
-    return int(min(cap, 0.9 * free / per_row) // 100_000 * 100_000)
+    return int(min(cap, free / per_row) // 100_000 * 100_000)
 
 
 def leg_config4(ctx: Ctx, L, args, w: int = 0, rows: int = 0, cpu: bool = True) -> dict:

@@ -92,6 +92,37 @@ __global__ __launch_bounds__(256) void k_geo(Ptrs p, int W, uint8_t* shard, uint
     }
 }
 
+// Config 2's record layout: pushes of 16 384 records [key][1 024 floats], the values
+// OFF bytes into a record of STRIDE bytes (the wire: 4 / 4 100, so every 16-B value load
+// is 4-B aligned; a padded layout: 16 / 4 112, 16-B aligned); a wave owns 4 rows of
+// 4 KiB (the product's k_reduce_rows span), D pushes in flight.
+template <int OFF, int STRIDE, int D>
+__global__ __launch_bounds__(256) void k_rec(Ptrs p, int W, uint8_t* shard, uint8_t* sink) {
+    const int64_t blk = xcd_remap();
+    const int64_t g = blk * 4 + (threadIdx.x >> 6);  // wave -> rows 4g .. 4g + 3
+    const int lane = threadIdx.x & 63;
+    const auto rs = rsrc(shard + g * 4 * 4096, 4 * 4096);
+    u32x4 acc[16];
+#pragma unroll
+    for (int j = 0; j < 16; ++j) acc[j] = __builtin_amdgcn_raw_buffer_load_b128(rs, (j >> 2) * 4096 + ((j & 3) * 64 + lane) * 16, 0, 2);
+    for (int b = 0; b < W; b += D) {
+        u32x4 v[D][16];
+#pragma unroll
+        for (int d = 0; d < D; ++d) {
+            const auto rp = rsrc(p.p[b + d] + g * 4 * STRIDE, 4 * STRIDE);
+#pragma unroll
+            for (int j = 0; j < 16; ++j)
+                v[d][j] = __builtin_amdgcn_raw_buffer_load_b128(rp, (j >> 2) * STRIDE + OFF + ((j & 3) * 64 + lane) * 16, 0, 2);
+        }
+#pragma unroll
+        for (int d = 0; d < D; ++d)
+#pragma unroll
+            for (int j = 0; j < 16; ++j) acc[j] = addf(acc[j], v[d][j]);
+    }
+#pragma unroll
+    for (int j = 0; j < 16; ++j) __builtin_amdgcn_raw_buffer_store_b128(acc[j], rs, (j >> 2) * 4096 + ((j & 3) * 64 + lane) * 16, 0, 2);
+}
+
 __global__ void k_fill(uint8_t* p, int64_t n, uint32_t seed) {
     for (int64_t i = (blockIdx.x * (int64_t)blockDim.x + threadIdx.x) * 16; i < n; i += (int64_t)gridDim.x * blockDim.x * 16) {
         u32x4 v{(seed ^ (uint32_t)(i >> 4)) & 0x3fffffffu | 0x30000000u, 0x33800000u, 0x34000000u, 0x2f800000u};
@@ -224,6 +255,52 @@ int main(int argc, char** argv) {
          3},
         {"g4 slab: 16 x 8 GB slab", 16, 1, 7630 * MiB, true, {base}, 3},
     };
+    // config 2's record layouts against the flat stream, alternated in one process
+    if (!strcmp(filt, "rec")) {
+        const int64_t R = 16384;
+        uint8_t *slab4, *slab16, *shard;
+        CK(hipMalloc(&slab4, 32 * R * 4100 + 4096));
+        CK(hipMalloc(&slab16, 32 * R * 4112 + 4096));
+        CK(hipMalloc(&shard, R * 4096));
+        hipLaunchKernelGGL(k_fill, dim3(8192), dim3(256), 0, 0, slab4, 32 * R * 4100 / 16 * 16, 5u);
+        hipLaunchKernelGGL(k_fill, dim3(8192), dim3(256), 0, 0, slab16, 32 * R * 4112 / 16 * 16, 6u);
+        hipLaunchKernelGGL(k_fill, dim3(8192), dim3(256), 0, 0, shard, R * 4096, 7u);
+        Geo flat{32, 1, 64 << 20, true};
+        alloc_geo(flat);
+        Ptrs p4{}, p16{};
+        for (int b = 0; b < 32; ++b) {
+            p4.p[b] = slab4 + b * R * 4100;
+            p16.p[b] = slab16 + b * R * 4112;
+        }
+        CK(hipDeviceSynchronize());
+        const double bytes4 = 32.0 * R * 4100 + 2.0 * R * 4096, bytes16 = 32.0 * R * 4112 + 2.0 * R * 4096;
+        const unsigned grid = (unsigned)(R / 16);
+        auto timeit = [&](auto kern, const Ptrs& pp, double bytes, const char* name, int r) {
+            float best = 1e30f;
+            for (int it = 0; it <= 50; ++it) {
+                CK(hipEventRecord(e0));
+                hipLaunchKernelGGL(kern, dim3(grid), dim3(256), 0, 0, pp, 32, shard, g_sink);
+                CK(hipEventRecord(e1));
+                CK(hipEventSynchronize(e1));
+                float ms;
+                CK(hipEventElapsedTime(&ms, e0, e1));
+                if (it > 0 && ms < best) best = ms;
+            }
+            printf("{\"case\": \"%s\", \"round\": %d, \"best_us\": %.1f, \"frac_best\": %.4f}\n", name, r, best * 1e3,
+                   bytes / (best * 1e-3) / 1e9 / 8000.0);
+            fflush(stdout);
+        };
+        for (int r = 0; r < rounds; ++r) {
+            timeit(k_rec<4, 4100, 2>, p4, bytes4, "rec: values 4 B into 4100-B records (wire), D 2", r);
+            timeit(k_rec<16, 4112, 2>, p16, bytes16, "rec: values 16 B into 4112-B records (aligned), D 2", r);
+            timeit(k_rec<4, 4100, 1>, p4, bytes4, "rec: values 4 B into 4100-B records (wire), D 1", r);
+            float best, mean;
+            const Kern wide = KN(16, 1, 1, 0, true);
+            time_case(flat, wide, 50, best, mean);
+            report("rec: flat 32 x 64 MiB slab", flat, wide, r, best, mean);
+        }
+        return 0;
+    }
     // same-process alternation of the two geometries (both resident): g2, g4, g2, g4 ...
     if (!strcmp(filt, "alt")) {
         Geo a{32, 1, 64 * MiB, true}, b{16, 1, 7630 * MiB, false};
