@@ -1803,6 +1803,7 @@ __global__ __launch_bounds__(256) void k_ada_ident(float* __restrict__ shard, in
     const int64_t v0 = xcd_block() * (256 * U) + threadIdx.x;
     float cand_v = 0.f;
     uint64_t cand_p = kNoPos;
+    int cand_key = 0;
     bool cand_ok = false;
     const bool live = !(bt.prev && ctrl_abnormal(bt.prev));
     int64_t roff[U];
@@ -1876,18 +1877,27 @@ __global__ __launch_bounds__(256) void k_ada_ident(float* __restrict__ shard, in
             for (int e = 0; e < VEC; ++e)
                 if (lg[u][e] > 1.0f) ada.alpha[v * VEC + e] = na[e];
         }
+        // the thread's candidate in (push, vector, element) order, which is position
+        // order (the pushes' columns ascend, offsets grow with u and e): the position
+        // itself is formed once, for the winner
 #pragma unroll
         for (int e = 0; e < VEC; ++e) {
             if (rb[u][e] < 0) continue;
-            const int g = rb[u][e];  // (a select chain, not a per-lane index into the kernarg table)
-            const uint64_t gb = g == 0 ? bi0 : g == 1 ? bi1 : g == 2 ? bi2 : bi3;
-            const uint64_t p = pos_of(gb, (uint64_t)(roff[u] + e * 4));
-            if (!cand_ok || rv[u][e] > cand_v || (rv[u][e] == cand_v && p < cand_p)) {
+            const int key = (rb[u][e] << 16) | (u << 2) | e;
+            if (!cand_ok || rv[u][e] > cand_v || (rv[u][e] == cand_v && key < cand_key)) {
                 cand_ok = true;
                 cand_v = rv[u][e];
-                cand_p = p;
+                cand_key = key;
             }
         }
+    }
+    if (cand_ok) {
+        const int g = cand_key >> 16, u = (cand_key >> 2) & 0x3FFF, e = cand_key & 3;
+        const uint64_t gb = g == 0 ? bi0 : g == 1 ? bi1 : g == 2 ? bi2 : bi3;  // (a select chain)
+        int64_t ro = roff[0];
+#pragma unroll
+        for (int k = 1; k < U; ++k) ro = u == k ? roff[k] : ro;
+        cand_p = pos_of(gb, (uint64_t)(ro + e * 4));
     }
     cand_block_best<4>(cand_ok, cand_v, cand_p);
     if (threadIdx.x == 0) {
