@@ -796,7 +796,8 @@ def c4_fit_rows(ctx: Ctx, w: int, cols: int = C4_COLS, cap: int = C4_ROWS) -> in
     per_row = w * (4 + 4 * cols) + (2 * cols * 4 + 3 * WS_BYTES_PER_ROW) / (world if sharded else 1)
     if sharded:
         per_row += (2 * cols * 4 + 2 * cols * 4 / world) + 3 * WS_BYTES_PER_ROW
-    return int(min(cap, free / per_row) // 100_000 * 100_000)
+    rows = int(min(cap, free / per_row) // 100_000 * 100_000)
+    return int(-ctx.max(-rows))  # every rank the same model (the smallest fit)
 
 
 def leg_config4(ctx: Ctx, L, args, w: int = 0, rows: int = 0, cpu: bool = True) -> dict:

@@ -28,7 +28,7 @@ n = json.load(open("gpurun_out/bench_native.json"))["native_group"]; print("nati
 PY
 else
 TAG=line ARGS="--steps 200 --warmup 100 --no-cpu --legs 4,5,4a --c4-steps 3 --c4-warmup 1 --c5-steps 10 --c5-warmup 2 --c4a-steps 2 --c4a-warmup 1 --sparse-steps 10" bash scripts/gpu_prof.sh
-timeout -k 10 400 python bench.py --gpus 2 --rehearse-gloo --c4-pushes 4 --no-cpu --steps 50 --warmup 20 > gpurun_out/rehearse2.json 2> gpurun_out/rehearse2.err
+timeout -k 10 400 python bench.py --gpus 2 --rehearse-gloo --legs 4,5,4a --c4-pushes 4 --no-cpu --steps 50 --warmup 20 > gpurun_out/rehearse2.json 2> gpurun_out/rehearse2.err
 python3 -c "import json;d=json.load(open('gpurun_out/rehearse2.json'));print('rehearse N=2', d['n_gpus'], d['ms_per_step'], sorted(k for k in d if k.startswith('config')))"
 timeout -k 10 300 python scripts/e2e.py > gpurun_out/e2e.log 2>&1
 tail -12 gpurun_out/e2e.log
