@@ -86,3 +86,46 @@ print(json.dumps(line), flush=True)
         assert d["native_group"] == {"value": 1.0}
     else:
         assert "error" in d["native_group"] and ("boom" in d["native_group"]["error"] or "within" in d["native_group"]["error"])
+
+
+class _FakeCuda:
+    def __init__(self, free, total):
+        self._m = (free, total)
+
+    def mem_get_info(self):
+        return self._m
+
+
+class _FakeCtx:
+    """bench.Ctx's surface c4_fit_rows uses: torch.cuda.mem_get_info, world and a max
+    over ranks (here: over the other ranks' values given up front)."""
+
+    def __init__(self, free, total, world=1, others=()):
+        self.torch = type("T", (), {"cuda": _FakeCuda(free, total)})()
+        self.world, self._others = world, list(others)
+
+    def max(self, x):
+        return max([x] + self._others)
+
+
+def test_config4_w32_rows_fit_and_agree():
+    """The config-4 W = 32 leg's model size (bench.c4_fit_rows): whole 100 000s, at most
+    10 M, its pushes + store (+ group buffers at N > 1) within the free HBM less the 1/8
+    headroom the store keeps before it allocates its speculative buffer (dml_store.hip), and
+    the same on every rank (the smallest fit: a different size per rank would desynchronise
+    the collectives)."""
+    sys.path.insert(0, ROOT)
+    import bench
+    total = 309 * 2**30
+    for world in (1, 2, 8):
+        free = total - 3 * 2**30
+        rows = bench.c4_fit_rows(_FakeCtx(free, total, world), 32)
+        assert rows % 100_000 == 0 and 0 < rows <= bench.C4_ROWS
+        per_row = 32 * 804 + 2 * 800 + 3 * bench.WS_BYTES_PER_ROW
+        if world == 1:
+            assert rows * per_row <= 0.97 * free - total / 8
+            assert (rows + 100_000) * per_row > 0.97 * free - total / 8  # the most that fit
+        assert bench.c4_fit_rows(_FakeCtx(free, total, world), 8) == bench.C4_ROWS  # W = 8 fits at 10 M
+    # another rank with less free memory settles the size for all
+    small = bench.c4_fit_rows(_FakeCtx(200 * 2**30, total, 2), 32)
+    assert bench.c4_fit_rows(_FakeCtx(300 * 2**30, total, 2, others=[-small]), 32) == small
