@@ -271,6 +271,16 @@ def _sparse_perm(b, dim):
 SLAB = [True]
 
 
+def push_buffers(torch, n: int, nbytes: int):
+    """n push buffers of nbytes: slices of one receive slab (SLAB), or one allocation each.
+    Configs 2, 4 and 4a (config 4: 16 x 8.04 GB slices 2.3-3.7 % faster than separate
+    allocations in 3 of 3 rounds on one box in r06, equal in r05; profiles/r06_ab_slab_legs.txt)."""
+    if SLAB[0]:
+        slab = torch.empty(n * nbytes, dtype=torch.uint8, device="cuda")
+        return [slab[i * nbytes:(i + 1) * nbytes] for i in range(n)]
+    return [torch.empty(nbytes, dtype=torch.uint8, device="cuda") for _ in range(n)]
+
+
 def make_buckets(L, torch, fmt, n, rows_total, value_seed: int = 1000, alloc_seed: int = 0):
     st = torch.cuda.current_stream().cuda_stream
     bufs = []
@@ -821,8 +831,9 @@ def leg_config4(ctx: Ctx, L, args, w: int = 0, rows: int = 0, cpu: bool = True) 
                                  "group": group_bytes(world, rows, cols, 4) if sharded else 0})
     bufs = []
     asc = args.c4_order == "asc"
+    mem = push_buffers(torch, w, rows * rec)
     for b in range(w):
-        t = torch.empty(rows * rec, dtype=torch.uint8, device="cuda")
+        t = mem[b]
         seed = 3000 + 64 * rank + b
         pa, pc = (1, 0) if asc else (_coprime(seed * 2654435761 % rows | 1, rows), b * 7919 % rows)
         assert L.dml_synth_dense_bucket(t.data_ptr(), C.byref(fmt.to_c()), 0, rows, rows, cols, seed, pa, pc,
@@ -933,8 +944,9 @@ def leg_config4_ada(ctx: Ctx, L, args) -> dict:
     hbm_check(torch, "config4_ada", {"pushes": w * rows * rec, "store": store_bytes(S4, cols, 4, ada=True),
                                      "exchange": 0 if world == 1 else 4 * w * rows * rec})
     bufs = []
+    mem = push_buffers(torch, w, rows * rec)
     for b in range(w):
-        t = torch.empty(rows * rec, dtype=torch.uint8, device="cuda")
+        t = mem[b]
         assert L.dml_synth_dense_bucket(t.data_ptr(), C.byref(fmt.to_c()), 0, rows, rows, cols, 5000 + 64 * rank + b,
                                         1, 0, C.c_void_p(st)) == 0
         bufs.append(t)
@@ -1028,6 +1040,8 @@ def leg_config5(ctx: Ctx, L, args) -> dict:
     store.synth_fill(11)
     st = torch.cuda.current_stream().cuda_stream
     pos, neg = [], []
+    # one allocation per push: slices of one slab ran this leg 1.7-2.2 % slower in
+    # r05 and r06 (3 of 3 rounds each, profiles/r06_ab_slab_legs.txt)
     for b in range(C5_W):
         t = torch.empty(nrec * rec, dtype=torch.uint8, device="cuda")
         seed = 4000 + b
@@ -1351,7 +1365,7 @@ def main():
     ap.add_argument("--shuffle-orders", type=int, default=0, help=argparse.SUPPRESS)
     ap.add_argument("--alloc-seed", type=int, default=0, help=argparse.SUPPRESS)
     ap.add_argument("--separate-buffers", action="store_true",
-                    help="config 2: one allocation per push instead of slices of one receive slab (diagnostic)")
+                    help="configs 2, 4, 4a: one allocation per push instead of slices of one receive slab (diagnostic)")
     ap.add_argument("--shuffle-only", choices=["", "asc", "perm"], default="", help=argparse.SUPPRESS)
     ap.add_argument("--emulate-rs", type=int, default=0,
                     help="diagnostic with --group at N = 1: the owner-side HBM footprint of an N-rank "

@@ -91,8 +91,13 @@ struct Batch {
 // A chunk whose predecessor ended abnormally (error, rows to replay, or a failed
 // identity speculation) must not run ahead of the host's fix-up: its kernels
 // turn into no-ops and the host relaunches (replay) or drops (error) it.
+// Every field is read and the tests combined without short-circuit: in a kernel the
+// four loads issue together (one wait) instead of as a chain of dependent round trips
+// ahead of the block's first data load.
 __host__ __device__ inline bool ctrl_abnormal(const Ctrl* c) {
-    return c->cutoff != kNoPos || c->neg_pos != kNoPos || c->no_dup == 0u || c->spec_ok == 0u;
+    const unsigned long long cut = c->cutoff, neg = c->neg_pos;
+    const unsigned int nd = c->no_dup, ok = c->spec_ok;
+    return (cut != kNoPos) | (neg != kNoPos) | (nd == 0u) | (ok == 0u);
 }
 
 // Per-block AdaGrad candidate: the largest final delta of an element whose

@@ -1216,13 +1216,14 @@ __global__ __launch_bounds__(NW * 64) void k_flat_ident(T* __restrict__ shard, i
     const int lane = threadIdx.x & 63;
     const int wid = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     const int64_t t0 = (xcd_block() * NW + wid) * R;
-    // every wave reaches the block barrier below: a wave past the last row, or behind
-    // a predecessor that needs the host first, does no work and writes nothing
-    const bool live = t0 < rows && !(bt.prev && ctrl_abnormal(bt.prev));
-    const int nrow = !live ? 0 : (int)(rows - t0 < (int64_t)R ? rows - t0 : (int64_t)R);
+    // every wave reaches the block barrier below: a wave past the last row does no
+    // work; one behind a predecessor that needs the host first reads its rows (the
+    // check does not hold up the loads) and writes nothing
+    const bool inr = t0 < rows;
+    const int nrow = !inr ? 0 : (int)(rows - t0 < (int64_t)R ? rows - t0 : (int64_t)R);
     const int NV = cols / VEC, nvec = nrow * NV;
-    const int64_t mr0 = live ? uni64(rm.row(t0)) : 0;
-    const int64_t mrl = live ? uni64(rm.row(t0 + nrow - 1)) : 0;
+    const int64_t mr0 = inr ? uni64(rm.row(t0)) : 0;
+    const int64_t mrl = inr ? uni64(rm.row(t0 + nrow - 1)) : 0;
     // per lane j: record offset from record mr0 (push buffers), element offset from
     // row mr0 (input shard) and from the output base; kBufOff = no vector here
     uint32_t loff[J], soff[J], ooff[J];
@@ -1242,7 +1243,7 @@ __global__ __launch_bounds__(NW * 64) void k_flat_ident(T* __restrict__ shard, i
     const uint32_t sspan = (uint32_t)((mrl - mr0 + 1) * cols * (int64_t)sizeof(T));
     T acc[J][VEC];
     bool bad = false;
-    if (live) {
+    if (inr) {
         if constexpr (MODE == kAdd) {
             // the input rows: in place, or the speculative chunk's input buffer
             const T* const ib = (bt.src ? (const T*)bt.src : shard) + mr0 * cols;
@@ -1299,7 +1300,7 @@ __global__ __launch_bounds__(NW * 64) void k_flat_ident(T* __restrict__ shard, i
     }
     // every wave of the block has read its rows: the block's writes leave together
     __syncthreads();
-    if (!live) return;
+    if (!inr || (bt.prev && ctrl_abnormal(bt.prev))) return;
     T* const ob = rm.out ? (T*)rm.out + t0 * (int64_t)cols : shard + mr0 * cols;
     const __amdgpu_buffer_rsrc_t os = buf_rsrc(ob, rm.out ? (uint32_t)(nrow * cols * (int64_t)sizeof(T)) : sspan);
 #pragma unroll
@@ -1805,16 +1806,18 @@ __global__ __launch_bounds__(256) void k_ada_ident(float* __restrict__ shard, in
     uint64_t cand_p = kNoPos;
     int cand_key = 0;
     bool cand_ok = false;
-    const bool live = !(bt.prev && ctrl_abnormal(bt.prev));
     int64_t roff[U];
     bool on[U];
     float acc[U][VEC], dl[U][VEC], lg[U][VEC], rv[U][VEC];
     int rb[U][VEC];  // push of the element's last strict rise (-1: none)
     u32x4 raw[NB][U];
+    // the loads do not wait for the predecessor check (reads only; behind an abnormal
+    // predecessor nothing below is stored): a short block's data is in flight from its
+    // first instructions
 #pragma unroll
     for (int u = 0; u < U; ++u) {
         const int64_t v = v0 + u * 256, e = v * VEC;
-        on[u] = live && v < nvec;
+        on[u] = v < nvec;
         roff[u] = (e / cols) * stride + K + (e % cols) * 4;
         const u32x4 z{0u, 0u, 0u, 0u};
         unpack<float>(on[u] ? ldg16_nt((const uint8_t*)shard + v * 16) : z, acc[u]);
@@ -1850,9 +1853,10 @@ __global__ __launch_bounds__(256) void k_ada_ident(float* __restrict__ shard, in
         }
     const uint64_t bi0 = (uint64_t)bt.bidx[0], bi1 = NB > 1 ? (uint64_t)bt.bidx[NB > 1 ? 1 : 0] : 0,
                    bi2 = NB > 2 ? (uint64_t)bt.bidx[NB > 2 ? 2 : 0] : 0, bi3 = NB > 3 ? (uint64_t)bt.bidx[NB > 3 ? 3 : 0] : 0;
+    const bool live = !(bt.prev && ctrl_abnormal(bt.prev));  // predecessor needs the host first
 #pragma unroll
     for (int u = 0; u < U; ++u) {
-        if (!on[u]) continue;
+        if (!live || !on[u]) continue;
         const int64_t v = v0 + u * 256;
         stg16_nt((uint8_t*)shard + v * 16, pack<float>(acc[u]));
         stg16_nt((uint8_t*)ada.delta + v * 16, pack<float>(dl[u]));
