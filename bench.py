@@ -263,19 +263,25 @@ def _sparse_perm(b, dim):
 
 
 # ---------------------------------------------------------------- config 2
-# A PS receives a call's pushes into one device receive slab, sliced per push
-# (INTEGRATION.md): over separately allocated buffers the reduce's DRAM efficiency
-# depends on where the allocator put them (same bytes, 333-348 us per launch,
-# scripts/probe_placement.py), over slices of one slab it is the same in every order.
-# --separate-buffers restores one allocation per push (diagnostic).
-SLAB = [True]
+# Where a call's pushes sit in HBM moves the reduces' DRAM efficiency by a few per cent
+# (same bytes, same kernels; DESIGN.md §4.1 / §4.2, profiles/r06_ab_slab_legs.txt):
+#  - config 2 (32 x 64 MiB): one allocation per push, the buffers allocated first in the
+#    process, ran 330-333 us per launch against 336-338 us as slices of one slab (r06, two
+#    GPU calls, 7 of 7 alternating rounds; the driver's lines: r03 / r04 330 / 334 us with
+#    separate buffers, r05 339 us with the slab). Separate buffers allocated after and
+#    around others drew 332-348 us (r05 placement probe, scripts/probe_placement.py);
+#  - configs 4 / 4a (16 x 8 GB): slices of one slab 2-4 % faster on one box, equal on another;
+#  - config 5: one allocation per push (its slab 1.7-2.2 % slower, r05 and r06).
+# --push-layout slab / separate forces one layout on every leg (--separate-buffers =
+# separate).
+SLAB = [False]   # config 2
+SLAB4 = [True]   # configs 4 / 4a
 
 
 def push_buffers(torch, n: int, nbytes: int):
-    """n push buffers of nbytes: slices of one receive slab (SLAB), or one allocation each.
-    Configs 2, 4 and 4a (config 4: 16 x 8.04 GB slices 2.3-3.7 % faster than separate
-    allocations in 3 of 3 rounds on one box in r06, equal in r05; profiles/r06_ab_slab_legs.txt)."""
-    if SLAB[0]:
+    """n push buffers of nbytes for the config-4 legs: slices of one receive slab (SLAB4),
+    or one allocation each."""
+    if SLAB4[0]:
         slab = torch.empty(n * nbytes, dtype=torch.uint8, device="cuda")
         return [slab[i * nbytes:(i + 1) * nbytes] for i in range(n)]
     return [torch.empty(nbytes, dtype=torch.uint8, device="cuda") for _ in range(n)]
@@ -880,7 +886,8 @@ def leg_config4(ctx: Ctx, L, args, w: int = 0, rows: int = 0, cpu: bool = True) 
     out = {"workload": f"config4: Word2Vec rows {rows}x{cols} fp32 model, {w} full-range pushes per GPU "
                        f"([int32][{cols} x f32], rows {'ascending (keys implicit = row)' if asc else 'permuted per push'})",
            "value": round(algo * world * args.c4_steps / el / 2**30, 2), "unit": "GiB/s", "n_gpus": world,
-           "pushes_per_gpu": w, "steps": args.c4_steps, "ms_per_step": round(el / args.c4_steps * 1e3, 3),
+           "pushes_per_gpu": w, "push_buffers": "one receive slab" if SLAB4[0] else "one allocation per push",
+           "steps": args.c4_steps, "ms_per_step": round(el / args.c4_steps * 1e3, 3),
            "scaling": "weak", "dtype": "f32",
            "parallelism": "single shard" if not sharded else f"linearSplit({world}) + RCCL reduce-scatter",
            "algorithmic_bytes_per_step_per_gpu": algo}
@@ -985,7 +992,8 @@ def leg_config4_ada(ctx: Ctx, L, args) -> dict:
     out = {"workload": f"config4 AdaGrad: FloatMatrixStoreAdaGrad {rows}x{cols} fp32 (data + alpha + delta), {w} "
                        f"full-range pushes per GPU (rows ascending), {path}",
            "value": round(algo * world * args.c4a_steps / el / 2**30, 2), "unit": "GiB/s", "n_gpus": world,
-           "pushes_per_gpu": w, "steps": args.c4a_steps, "ms_per_step": round(el / args.c4a_steps * 1e3, 3),
+           "pushes_per_gpu": w, "push_buffers": "one receive slab" if SLAB4[0] else "one allocation per push",
+           "steps": args.c4a_steps, "ms_per_step": round(el / args.c4a_steps * 1e3, 3),
            "scaling": "weak", "dtype": "f32",
            "parallelism": "single shard (local exchange)" if world == 1 else
                           f"linearSplit({world}) + dml_shard_split + RCCL all-to-all + ordered owner apply",
@@ -1364,8 +1372,10 @@ def main():
     ap.add_argument("--shuffle-keep-parity", action="store_true", help=argparse.SUPPRESS)
     ap.add_argument("--shuffle-orders", type=int, default=0, help=argparse.SUPPRESS)
     ap.add_argument("--alloc-seed", type=int, default=0, help=argparse.SUPPRESS)
-    ap.add_argument("--separate-buffers", action="store_true",
-                    help="configs 2, 4, 4a: one allocation per push instead of slices of one receive slab (diagnostic)")
+    ap.add_argument("--push-layout", choices=["auto", "slab", "separate"], default="auto",
+                    help="push buffers: auto = config 2 and 5 one allocation per push, configs 4 / 4a one slab "
+                         "(diagnostic override for every leg)")
+    ap.add_argument("--separate-buffers", action="store_true", help="= --push-layout separate")
     ap.add_argument("--shuffle-only", choices=["", "asc", "perm"], default="", help=argparse.SUPPRESS)
     ap.add_argument("--emulate-rs", type=int, default=0,
                     help="diagnostic with --group at N = 1: the owner-side HBM footprint of an N-rank "
@@ -1399,7 +1409,9 @@ def main():
     # (RCCL refuses two ranks on one device); numbers from it are not measurements
     ap.add_argument("--rehearse-gloo", action="store_true", help=argparse.SUPPRESS)
     args = ap.parse_args()
-    SLAB[0] = not args.separate_buffers
+    layout = "separate" if args.separate_buffers else args.push_layout
+    if layout != "auto":
+        SLAB[0] = SLAB4[0] = layout == "slab"
     # RCCL's channel count for the torch binding's reduce-scatter, pinned before any GPU
     # call (RCCL reads it at communicator creation; the native group pins the same count
     # through ncclCommInitRankConfig): the one-GPU ring emulation favours
