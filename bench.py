@@ -913,7 +913,7 @@ def leg_config4(ctx: Ctx, L, args, w: int = 0, rows: int = 0, cpu: bool = True) 
         group.close()
     else:
         store.close()
-    del bufs, ptrs
+    del bufs, ptrs, mem, t  # the slab goes with its last slice
     torch.cuda.synchronize()
     torch.cuda.empty_cache()
     if world == 1 and not args.no_cpu and cpu:
@@ -1018,7 +1018,7 @@ def leg_config4_ada(ctx: Ctx, L, args) -> dict:
                                     "measured_stream_floor_frac": round(owner / (fl * 1e-3) / 1e9 / HBM_PEAK_GBS, 4),
                                     "frac_of_measured_floor": round(fl * 1e-3 / k_s, 3)})
     group.close()
-    del bufs, ptrs
+    del bufs, ptrs, mem, t  # the slab goes with its last slice
     torch.cuda.synchronize()
     torch.cuda.empty_cache()
     return out
