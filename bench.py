@@ -896,8 +896,9 @@ def leg_config4(ctx: Ctx, L, args, w: int = 0, rows: int = 0, cpu: bool = True) 
         kn = store.kernel_name()
         out["roofline"] = {"bound": "hbm", "achieved": round(algo / k_s / 1e9, 1), "peak": HBM_PEAK_GBS,
                            "unit": "GB/s", "frac": round(algo / k_s / 1e9 / HBM_PEAK_GBS, 4),
-                           **traffic_for("leg4", kn), "kernel": kn,
-                           "avg_kernel_us": round(k_s * 1e6, 1), "launches": k_n}
+                           **(traffic_for("leg4", kn) if (w, rows) == (16, C4_ROWS) else
+                              {"traffic": None, "traffic_stale": "the counters were taken at W = 16, 10 M rows"}),
+                           "kernel": kn, "avg_kernel_us": round(k_s * 1e6, 1), "launches": k_n}
         if asc:
             # the plain stream of the same bytes over the same allocations (dml_diag_dense_floor:
             # no key checks; out of place like the speculative chunk): the live ceiling
