@@ -1,6 +1,6 @@
 # A/B library variant: the in-tree sources rebuilt with extra -D switches into
-# scripts/ab/libdistml_ps_<NAME>.so (scripts/ab_bench.sh swaps it in on the box).
-#   bash scripts/build_ab.sh remap1 -DDML_AB_REMAP=1
+# scripts/ab/libdistml_ps_<NAME>.so (scripts/ab_multi.sh or scripts/gpu_leaf_ab.sh swap it in on the box).
+#   bash scripts/build_ab.sh name -DSOME_SWITCH=1
 set -e
 NAME=$1; shift
 cd "$(dirname "$0")/../distml_amd/csrc"
