@@ -235,6 +235,8 @@ int main(int argc, char** argv) {
           KN(16, 1, 1, 0, true)},
          20},
         {"g2 separate: 32 x 64 MiB", 32, 1, 64 * MiB, false, {base}, 20},
+        // per-wave span beyond k_reduce_rows' 16 KiB (4 rows x 4 KiB): 32 KiB, one push in flight
+        {"span: 32 x 64 MiB slab", 32, 1, 64 * MiB, true, {KN(16, 1, 1, 0, true), KN(32, 1, 1, 0, true), KN(16, 1, 1, 0, true), KN(32, 1, 1, 0, true)}, 20},
         // the write share of config 4 (1/18) at config 2's footprint
         {"x: 16 x 64 MiB slab", 16, 1, 64 * MiB, true, {base, KN(4, 4, 1, 1, true)}, 20},
         // shard size sweep (the 256 MiB Infinity Cache), config 2's 32 pushes and write share
