@@ -129,3 +129,34 @@ def test_config4_w32_rows_fit_and_agree():
     # another rank with less free memory settles the size for all
     small = bench.c4_fit_rows(_FakeCtx(200 * 2**30, total, 2), 32)
     assert bench.c4_fit_rows(_FakeCtx(300 * 2**30, total, 2, others=[-small]), 32) == small
+
+
+def test_push_buffers_layouts():
+    """bench.push_buffers: the config-4 legs' pushes as slices of one receive slab
+    (consecutive, non-overlapping views of one allocation) or one allocation each
+    (--push-layout separate), the same sizes either way."""
+    sys.path.insert(0, ROOT)
+    import bench
+    import torch
+
+    class _CpuTorch:  # torch with the device argument dropped (no GPU here)
+        uint8 = torch.uint8
+
+        @staticmethod
+        def empty(n, dtype, device):
+            return torch.empty(n, dtype=dtype)
+
+    keep = bench.SLAB4[0]
+    try:
+        bench.SLAB4[0] = True
+        bufs = bench.push_buffers(_CpuTorch, 4, 1000)
+        assert [b.numel() for b in bufs] == [1000] * 4
+        base = bufs[0].data_ptr()
+        assert [b.data_ptr() - base for b in bufs] == [0, 1000, 2000, 3000]
+        assert len({b.untyped_storage().data_ptr() for b in bufs}) == 1
+        bench.SLAB4[0] = False
+        bufs = bench.push_buffers(_CpuTorch, 4, 1000)
+        assert [b.numel() for b in bufs] == [1000] * 4
+        assert len({b.untyped_storage().data_ptr() for b in bufs}) == 4
+    finally:
+        bench.SLAB4[0] = keep
