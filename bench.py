@@ -800,13 +800,14 @@ def sparse_leg(ctx: Ctx, L, steps: int, cpu: bool, cu_split: int = 0):
 
 
 # ---------------------------------------------------------------- config 4 (model level)
-def c4_fit_rows(ctx: Ctx, w: int, cols: int = C4_COLS, cap: int = C4_ROWS) -> int:
+def c4_fit_rows(ctx: Ctx, w: int, cols: int = C4_COLS, cap: int = C4_ROWS, share: int = 1) -> int:
     """The most config-4 rows (<= cap, whole 100 000s) whose W pushes, store (two shard
     buffers and the workspace ring) and, at N > 1, group buffers fit the free HBM and
     still leave the store the headroom it keeps before it allocates its speculative second
-    buffer (1/8 of the device, dml_store.hip): without it the chunks run the key index."""
+    buffer (1/8 of the device, dml_store.hip): without it the chunks run the key index.
+    `share`: ranks sharing the device (the one-GPU gloo rehearsal)."""
     free, total = ctx.torch.cuda.mem_get_info()
-    free = 0.97 * free - max(total / 8, 4 << 30)
+    free = (0.97 * free - max(total / 8, 4 << 30)) / share
     world = ctx.world
     sharded = world > 1
     per_row = w * (4 + 4 * cols) + (2 * cols * 4 + 3 * WS_BYTES_PER_ROW) / (world if sharded else 1)
@@ -1470,8 +1471,9 @@ def main():
     if "4w" in legs:
         # config 4 at W = 8 (one push per GPU of the 8-GPU job) and W = 32 (at
         # the most rows whose 32 pushes fit beside the store: 32 x 8.04 GB exceed 288 GB at 10 M)
-        line["config4_w8"] = leg_config4(ctx, L, args, w=8, cpu=False)
-        line["config4_w32"] = leg_config4(ctx, L, args, w=32, rows=c4_fit_rows(ctx, 32), cpu=False)
+        share = world if args.rehearse_gloo else 1  # rehearsal: every rank on one GPU
+        line["config4_w8"] = leg_config4(ctx, L, args, w=8, rows=c4_fit_rows(ctx, 8, share=share), cpu=False)
+        line["config4_w32"] = leg_config4(ctx, L, args, w=32, rows=c4_fit_rows(ctx, 32, share=share), cpu=False)
     if "5" in legs:
         line["config5"] = leg_config5(ctx, L, args)
     if "4a" in legs:
